@@ -1,0 +1,329 @@
+"""Batched entry points over millions of markets.
+
+All array arguments are device tensors (torch, ``cuda:N``); results stay in HBM.  Each
+function is one or a few launches of the HIP kernels in ``libbce_hip.so`` on the current
+stream -- there is no CPU fallback (see :mod:`bayesian_engine._native`).
+
+Layout (include/bce.h):
+  markets  CSR  offsets int64[M+1], sid int32[N] (interned source ranks in Python
+           ``sorted()`` order), prob fp64[N]
+  sources  dense table over ranks: rel fp64[S], conf fp64[S] (cold-start defaults baked
+           in), present u8[S]; optional t_us int64[S] for decay
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, Iterable, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _native as N
+from .config import DECAY_HALF_LIFE_DAYS, DECAY_MINIMUM, DEFAULT_CONFIDENCE, DEFAULT_RELIABILITY
+
+_MODES = {"exact": N.MODE_EXACT, "fast": N.MODE_FAST}
+
+
+# ---------------------------------------------------------------------------------------
+# host-side interning and table building
+# ---------------------------------------------------------------------------------------
+def intern(ids: Iterable[str]) -> Dict[str, int]:
+    """Rank ids in Python ``sorted()`` (code-point) order: integer order == str order."""
+    return {s: i for i, s in enumerate(sorted(set(ids)))}
+
+
+@dataclass
+class SourceTable:
+    """Dense per-source table resident in HBM (bulk-loaded from a dict or SQLite)."""
+
+    rel: torch.Tensor
+    conf: torch.Tensor
+    present: torch.Tensor
+    names: List[str]
+    t_us: Optional[torch.Tensor] = None
+
+    @property
+    def n(self) -> int:
+        return len(self.names)
+
+    @classmethod
+    def from_dict(cls, names: Sequence[str], source_reliability: Optional[dict],
+                  device=None) -> "SourceTable":
+        """core.py:110-112 semantics: a key present (even with a partial dict) is not cold."""
+        S = len(names)
+        rel = np.full(max(S, 1), DEFAULT_RELIABILITY, np.float64)
+        conf = np.full(max(S, 1), DEFAULT_CONFIDENCE, np.float64)
+        present = np.zeros(max(S, 2), np.uint8)
+        sr = source_reliability or {}
+        for i, n in enumerate(names):
+            d = sr.get(n)
+            if n in sr:
+                present[i] = 1
+                if d is None:
+                    d = {}
+                r = d.get("reliability", DEFAULT_RELIABILITY)
+                c = d.get("confidence", DEFAULT_CONFIDENCE)
+                0.0 + r  # noqa: B018  -- same TypeError as core.py:120 for non-numbers
+                rel[i] = float(r)
+                conf[i] = float(c)
+        dev = device or N.device()
+        return cls(torch.from_numpy(rel).to(dev), torch.from_numpy(conf).to(dev),
+                   torch.from_numpy(present).to(dev), list(names))
+
+
+# ---------------------------------------------------------------------------------------
+# consensus
+# ---------------------------------------------------------------------------------------
+@dataclass
+class Plan:
+    """Markets binned by length (bce_plan_bins), reusable across calls on the same CSR."""
+
+    order: torch.Tensor
+    bin_start: np.ndarray
+    max_len: int
+    scratch: Optional[torch.Tensor]
+
+    @classmethod
+    def build(cls, offsets_host: np.ndarray, device=None) -> "Plan":
+        L = N.lib()
+        off = np.ascontiguousarray(offsets_host, np.int64)
+        M = len(off) - 1
+        order = np.zeros(max(M, 1), np.int32)
+        bins = np.zeros(N.NBINS + 1, np.int64)
+        mx = np.zeros(1, np.int32)
+        N.check(L.bce_plan_bins(N.ptr(off), M, N.ptr(order), N.ptr(bins), N.ptr(mx)), "plan_bins")
+        sb = int(L.bce_consensus_scratch_bytes(N.ptr(off), N.ptr(order), N.ptr(bins)))
+        dev = device or N.device()
+        scratch = torch.empty(sb, dtype=torch.uint8, device=dev) if sb > 0 else None
+        return cls(torch.from_numpy(order).to(dev), bins, int(mx[0]), scratch)
+
+
+@dataclass
+class ConsensusResult:
+    consensus: torch.Tensor      # fp64[M]  (0.0 where null)
+    confidence: torch.Tensor     # fp64[M]
+    total_weight: torch.Tensor   # fp64[M]
+    n_unique: torch.Tensor       # int32[M]
+    err_idx: Optional[torch.Tensor]   # int32[M]: first out-of-range signal, -1 if none
+    usid: Optional[torch.Tensor]      # int32[N]: rank | cold<<31 at CSR offsets
+    weight: Optional[torch.Tensor]    # fp64[N]
+    nweight: Optional[torch.Tensor]   # fp64[N]
+
+    def is_null(self, offsets: torch.Tensor) -> torch.Tensor:
+        """consensus is None: empty market (core.py:88) or total weight == 0 (core.py:131)."""
+        return (self.total_weight == 0) | (offsets[1:] == offsets[:-1])
+
+
+def _alloc(M: int, Nsig: int, dev, unique: bool, validate: bool) -> ConsensusResult:
+    f64 = dict(dtype=torch.float64, device=dev)
+    i32 = dict(dtype=torch.int32, device=dev)
+    return ConsensusResult(
+        torch.empty(M, **f64), torch.empty(M, **f64), torch.empty(M, **f64), torch.empty(M, **i32),
+        torch.empty(M, **i32) if validate else None,
+        torch.empty(max(Nsig, 1), **i32) if unique else None,
+        torch.empty(max(Nsig, 1), **f64) if unique else None,
+        torch.empty(max(Nsig, 1), **f64) if unique else None)
+
+
+def consensus(offsets: torch.Tensor, sid: torch.Tensor, prob: torch.Tensor, table: SourceTable, *,
+              plan: Optional[Plan] = None, max_len: Optional[int] = None, mode: str = "exact",
+              unique_outputs: bool = True, validate: bool = True,
+              out: Optional[ConsensusResult] = None) -> ConsensusResult:
+    """core.compute_consensus for every CSR market (+ the validation range check).
+
+    Pass ``max_len`` (<= 64: one launch, no planning) or a prebuilt :class:`Plan` for
+    ragged batches; with neither, a plan is built from a host copy of ``offsets``.
+    """
+    L = N.require_gpu()
+    M = offsets.numel() - 1
+    Nsig = sid.numel()
+    dev = offsets.device
+    res = out or _alloc(M, Nsig, dev, unique_outputs, validate)
+    common = (N.ptr(offsets), M, N.ptr(sid), N.ptr(prob), Nsig, N.ptr(table.rel), N.ptr(table.conf),
+              N.ptr(table.present), table.n)
+    outs = (N.ptr(res.consensus), N.ptr(res.confidence), N.ptr(res.total_weight), N.ptr(res.n_unique),
+            N.ptr(res.err_idx), N.ptr(res.usid), N.ptr(res.weight), N.ptr(res.nweight))
+    md = _MODES[mode]
+    if plan is None and max_len is not None and 0 < max_len <= 64:
+        rc = L.bce_consensus_csr(*common, N.ptr(None), 0, int(max_len), md, *outs, N.stream(dev))
+        N.check(rc, "bce_consensus_csr")
+        return res
+    if plan is None:
+        plan = Plan.build(offsets.cpu().numpy(), dev)
+    sb = plan.scratch.numel() if plan.scratch is not None else 0
+    rc = L.bce_consensus_planned(*common, N.ptr(plan.order), N.ptr(plan.bin_start), md, *outs,
+                                 N.ptr(plan.scratch), sb, N.stream(dev))
+    N.check(rc, "bce_consensus_planned")
+    return res
+
+
+def validate(offsets: torch.Tensor, prob: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """validate_input_payload's range check for every market: first bad index or -1."""
+    L = N.require_gpu()
+    M = offsets.numel() - 1
+    err = out if out is not None else torch.empty(max(M, 1), dtype=torch.int32, device=offsets.device)
+    N.check(L.bce_validate_csr(N.ptr(offsets), M, N.ptr(prob), N.ptr(err), N.stream(offsets.device)),
+            "bce_validate_csr")
+    return err[:M]
+
+
+# ---------------------------------------------------------------------------------------
+# decay / outcome update
+# ---------------------------------------------------------------------------------------
+def decay_view(rel: torch.Tensor, t_us: torch.Tensor, now_us: int, present: Optional[torch.Tensor] = None,
+               half_life_days: float = DECAY_HALF_LIFE_DAYS, min_rel: float = DECAY_MINIMUM,
+               default_rel: float = DEFAULT_RELIABILITY, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """get_reliability(apply_decay=True) for a whole table (reliability.py:110-131)."""
+    L = N.require_gpu()
+    n = rel.numel()
+    view = out if out is not None else torch.empty(max(n, 2), dtype=torch.float64, device=rel.device)
+    N.check(L.bce_decay_view(n, N.ptr(rel), N.ptr(t_us), N.ptr(present), int(now_us), float(half_life_days),
+                             float(min_rel), float(default_rel), N.ptr(view), N.stream(rel.device)),
+            "bce_decay_view")
+    return view[:n]
+
+
+def decay_apply(rel: Optional[torch.Tensor], elapsed_days: torch.Tensor,
+                half_life_days: float = DECAY_HALF_LIFE_DAYS, min_rel: float = DECAY_MINIMUM,
+                want_factor: bool = False):
+    """decay.compute_decay_factor / apply_reliability_decay on arrays (decay.py:31-100)."""
+    L = N.require_gpu()
+    n = elapsed_days.numel()
+    dev = elapsed_days.device
+    out = torch.empty(n, dtype=torch.float64, device=dev) if rel is not None else None
+    fac = torch.empty(n, dtype=torch.float64, device=dev) if want_factor else None
+    N.check(L.bce_decay_apply(n, N.ptr(rel), N.ptr(elapsed_days), float(half_life_days), float(min_rel),
+                              N.ptr(out), N.ptr(fac), N.stream(dev)), "bce_decay_apply")
+    return out, fac
+
+
+def outcome_update(rel: torch.Tensor, conf: torch.Tensor, t_us: torch.Tensor, present: torch.Tensor,
+                   flags: torch.Tensor, now_us: int, default_rel: float = DEFAULT_RELIABILITY,
+                   default_conf: float = DEFAULT_CONFIDENCE) -> None:
+    """In-place update_reliability math for every participant (reliability.py:142-183).
+
+    flags u8[S]: bit0 participates, bit1 correct (at most one outcome per source per call).
+    """
+    L = N.require_gpu()
+    N.check(L.bce_outcome_update(rel.numel(), N.ptr(rel), N.ptr(conf), N.ptr(t_us), N.ptr(present),
+                                 N.ptr(flags), int(now_us), float(default_rel), float(default_conf),
+                                 N.stream(rel.device)), "bce_outcome_update")
+
+
+def replay_step(rel, conf, t_us, present, flags2, now_us: int, view: torch.Tensor,
+                half_life_days: float = DECAY_HALF_LIFE_DAYS, min_rel: float = DECAY_MINIMUM) -> None:
+    """Config-4 step: decayed view at ``now_us`` then the outcome update, fused.
+
+    flags2: 2 bits per source (bit0 participates, bit1 correct), 4 sources per byte.
+    Absent rows must hold the baked cold-start values (rel 0.5, conf 0.25, t = NO_TIMESTAMP).
+    """
+    L = N.require_gpu()
+    N.check(L.bce_replay_step(rel.numel(), N.ptr(rel), N.ptr(conf), N.ptr(t_us), N.ptr(present),
+                              N.ptr(flags2), int(now_us), float(half_life_days), float(min_rel),
+                              DEFAULT_RELIABILITY, DEFAULT_CONFIDENCE, N.ptr(view), N.stream(rel.device)),
+            "bce_replay_step")
+
+
+def pack_flags2(participate: np.ndarray, correct: np.ndarray) -> np.ndarray:
+    """Host helper: (participate, correct) bool arrays -> the 2-bit packed flags2 layout."""
+    S = len(participate)
+    f = participate.astype(np.uint8) | (correct.astype(np.uint8) << 1)
+    pad = (-S) % 4
+    f = np.concatenate([f, np.zeros(pad, np.uint8)]).reshape(-1, 4)
+    return (f[:, 0] | (f[:, 1] << 2) | (f[:, 2] << 4) | (f[:, 3] << 6)).astype(np.uint8)
+
+
+# ---------------------------------------------------------------------------------------
+# tie-break, agreement statistics, re-estimation
+# ---------------------------------------------------------------------------------------
+@dataclass
+class TieBreakResult:
+    winner: torch.Tensor
+    label: torch.Tensor
+    n_groups: torch.Tensor
+    variance: torch.Tensor
+    g_key: torch.Tensor
+    g_count: torch.Tensor
+    g_density: torch.Tensor
+    g_avgconf: torch.Tensor
+    g_maxrel: torch.Tensor
+
+
+def tiebreak(offsets: torch.Tensor, pred: torch.Tensor, conf: torch.Tensor, weight: torch.Tensor,
+             rel: torch.Tensor, *, precision: int = 6, offsets_host: Optional[np.ndarray] = None) -> TieBreakResult:
+    """DeterministicTieBreaker(precision).resolve for every CSR market (tiebreak.py:73-152)."""
+    L = N.require_gpu()
+    M = offsets.numel() - 1
+    Nsig = pred.numel()
+    dev = offsets.device
+    f64 = dict(dtype=torch.float64, device=dev)
+    i32 = dict(dtype=torch.int32, device=dev)
+    r = TieBreakResult(torch.empty(M, **f64), torch.empty(M, **i32), torch.empty(M, **i32),
+                       torch.empty(M, **f64), torch.empty(max(Nsig, 1), **f64),
+                       torch.empty(max(Nsig, 1), **i32), torch.empty(max(Nsig, 1), **f64),
+                       torch.empty(max(Nsig, 1), **f64), torch.empty(max(Nsig, 1), **f64))
+    offh = offsets_host if offsets_host is not None else offsets.cpu().numpy()
+    lens = np.diff(offh)
+    long_ = np.nonzero(lens > 64)[0]
+    if len(long_) and lens.max() > 4096:
+        raise N.BCEError("tiebreak: markets longer than 4096 agents are not supported by this build")
+    outs = (N.ptr(r.winner), N.ptr(r.label), N.ptr(r.n_groups), N.ptr(r.variance), N.ptr(r.g_key),
+            N.ptr(r.g_count), N.ptr(r.g_density), N.ptr(r.g_avgconf), N.ptr(r.g_maxrel))
+    ins = (N.ptr(pred), N.ptr(conf), N.ptr(weight), N.ptr(rel))
+    st = N.stream(dev)
+    if len(long_) == 0:
+        N.check(L.bce_tiebreak_csr(N.ptr(offsets), M, N.ptr(None), 0, *ins, int(max(int(lens.max(initial=1)), 1)),
+                                   int(precision), *outs, st), "bce_tiebreak_csr")
+        return r
+    short = np.nonzero(lens <= 64)[0].astype(np.int32)
+    if len(short):
+        sl = torch.from_numpy(short).to(dev)
+        N.check(L.bce_tiebreak_csr(N.ptr(offsets), M, N.ptr(sl), len(short), *ins, 64, int(precision), *outs, st),
+                "bce_tiebreak_csr")
+    ll = torch.from_numpy(long_.astype(np.int32)).to(dev)
+    N.check(L.bce_tiebreak_csr_long(N.ptr(offsets), M, N.ptr(ll), len(long_), int(precision), *ins, *outs, st),
+            "bce_tiebreak_csr_long")
+    return r
+
+
+def agreement_stats(offsets, sid, prob, outcome, n_sources: int, correct=None, total=None):
+    """summarize_sources counts (market.py:279-304): outcome int8[M] (-1 skip, 0, 1)."""
+    L = N.require_gpu()
+    dev = offsets.device
+    if correct is None:
+        correct = torch.zeros(max(n_sources, 1), dtype=torch.int32, device=dev)
+    if total is None:
+        total = torch.zeros(max(n_sources, 1), dtype=torch.int32, device=dev)
+    N.check(L.bce_agreement_stats(N.ptr(offsets), offsets.numel() - 1, N.ptr(sid), N.ptr(prob),
+                                  N.ptr(outcome), N.ptr(correct), N.ptr(total), N.stream(dev)),
+            "bce_agreement_stats")
+    return correct, total
+
+
+def reestimate(P: torch.Tensor, iters: int, w0: float = 0.5, w: Optional[torch.Tensor] = None,
+               keep_history: bool = False):
+    """Config 5: ``iters`` rounds of consensus <-> reliability on agent-major P [A, M]."""
+    L = N.require_gpu()
+    A, M = P.shape
+    dev = P.device
+    ld = P.stride(0)
+    assert P.stride(1) == 1
+    w = torch.full((A,), w0, dtype=torch.float64, device=dev) if w is None else w
+    cons = torch.empty(M, dtype=torch.float64, device=dev)
+    nul = torch.empty(max(M, 1), dtype=torch.uint8, device=dev)
+    agree = torch.zeros(A, dtype=torch.int64, device=dev)
+    resolved = torch.zeros(1, dtype=torch.int64, device=dev)
+    hist = []
+    st = N.stream(dev)
+    for _ in range(iters):
+        N.check(L.bce_reestimate_consensus(N.ptr(P), A, M, ld, N.ptr(w), N.ptr(cons), N.ptr(nul), st),
+                "bce_reestimate_consensus")
+        agree.zero_()
+        resolved.zero_()
+        N.check(L.bce_reestimate_agreement(N.ptr(P), A, M, ld, N.ptr(cons), N.ptr(nul), N.ptr(agree),
+                                           N.ptr(resolved), st), "bce_reestimate_agreement")
+        N.check(L.bce_reestimate_weights(A, N.ptr(agree), N.ptr(resolved), N.ptr(w), st),
+                "bce_reestimate_weights")
+        if keep_history:
+            hist.append((cons.clone(), nul[:M].clone(), agree.clone(), w.clone()))
+    return w, cons, nul[:M], agree, hist

@@ -1,0 +1,121 @@
+// bce_device.hpp -- gfx950 device helpers shared by the engine's kernels.
+//
+// Wave64 cross-lane primitives (DPP, ds_swizzle, ds_bpermute), ballots and the
+// CPython-compatible scalar helpers (min/max argument order, exact decimal rounding).
+// Everything on the parity path is compiled with FP contraction OFF so that a*b+c rounds
+// twice, exactly like CPython (SURVEY.md §7 hard part 2).
+#pragma once
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bce {
+
+constexpr int kWave = 64;
+constexpr unsigned kSent32 = 0xFFFFFFFFu;
+constexpr unsigned long long kSent64 = 0xFFFFFFFFFFFFFFFFull;
+
+__device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
+
+__device__ __forceinline__ unsigned long long ballot(bool p) {
+  return __ballot(p);
+}
+
+// Exchange with lane ^ MASK inside 32-lane halves (MASK < 32) or across halves (32).
+template <int MASK>
+__device__ __forceinline__ unsigned xor_shfl(unsigned v) {
+  if constexpr (MASK == 1) {
+    return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+  } else if constexpr (MASK == 2) {
+    return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+  } else if constexpr (MASK < 32) {
+    return (unsigned)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (MASK << 10));  // bitmask mode
+  } else {
+    return (unsigned)__shfl_xor((int)v, 32);
+  }
+}
+
+__device__ __forceinline__ unsigned xor_shfl_rt(unsigned v, int m) {
+  switch (m) {
+    case 1: return xor_shfl<1>(v);
+    case 2: return xor_shfl<2>(v);
+    case 4: return xor_shfl<4>(v);
+    case 8: return xor_shfl<8>(v);
+    case 16: return xor_shfl<16>(v);
+    default: return xor_shfl<32>(v);
+  }
+}
+
+// lane-1 across the whole wave (DPP wave_shr:1); lane 0 reads `fill`.
+__device__ __forceinline__ int wave_shr1(int v, int fill) {
+  return __builtin_amdgcn_update_dpp(fill, v, 0x138, 0xF, 0xF, false);
+}
+
+// Pull from an arbitrary lane (ds_bpermute).
+__device__ __forceinline__ int pull_i32(int v, int src_lane) {
+  return __builtin_amdgcn_ds_bpermute(src_lane << 2, v);
+}
+__device__ __forceinline__ double pull_f64(double v, int src_lane) {
+  int2 x = *reinterpret_cast<int2*>(&v);
+  int2 y;
+  y.x = __builtin_amdgcn_ds_bpermute(src_lane << 2, x.x);
+  y.y = __builtin_amdgcn_ds_bpermute(src_lane << 2, x.y);
+  return *reinterpret_cast<double*>(&y);
+}
+// Push to an arbitrary lane (ds_permute): lane `dst` receives v.
+__device__ __forceinline__ int push_i32(int v, int dst_lane) {
+  return __builtin_amdgcn_ds_permute(dst_lane << 2, v);
+}
+
+// Bitonic sort (ascending) of one 32-bit key per lane inside aligned G-lane segments.
+template <int G>
+__device__ __forceinline__ unsigned bitonic_sort_seg(unsigned key, int l) {
+#pragma unroll
+  for (int k = 2; k <= G; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const unsigned other = xor_shfl_rt(key, j);
+      const bool up = (l & k) == 0;
+      const bool lower = (l & j) == 0;
+      const unsigned mn = key < other ? key : other;
+      const unsigned mx = key < other ? other : key;
+      key = (lower == up) ? mn : mx;
+    }
+  }
+  return key;
+}
+
+// CPython builtin min(a, b) / max(a, b): the second argument wins only on strict < / >.
+__device__ __forceinline__ double py_min(double a, double b) { return (b < a) ? b : a; }
+__device__ __forceinline__ double py_max(double a, double b) { return (b > a) ? b : a; }
+
+// CPython round(x, nd) for 0 <= nd <= 15: the correctly rounded decimal (half-even on
+// the exact binary value) converted back to the nearest double.  x*10^nd is split
+// exactly (hi + lo via the fma error term), the nearest integer k of hi+lo is found with
+// ties-to-even, and k/10^nd is one IEEE division (k < 2^53 is exact) == strtod of the
+// nd-digit decimal string.  For |x| >= thresh (= 2^E with ulp(x) > 10^-nd) rounding
+// moves x by less than half an ulp, so the answer is x itself (also NaN / inf).
+__device__ __forceinline__ double py_round_nd(double x, double scale, double thresh) {
+  if (!(fabs(x) < thresh)) return x;
+  const double hi = x * scale;
+  const double lo = __builtin_fma(x, scale, -hi);  // exact error of the product
+  const double k0 = rint(hi);
+  const double d = hi - k0;  // exact
+  double k = k0;
+  if (d == 0.5 || d == -0.5) {
+    if (lo != 0.0) k = ((d > 0.0) == (lo > 0.0)) ? k0 + (d > 0.0 ? 1.0 : -1.0) : k0;
+  } else if (d == 0.0 && (lo == 0.5 || lo == -0.5)) {
+    const double k1 = k0 + (lo > 0.0 ? 1.0 : -1.0);
+    k = (fmod(k0, 2.0) == 0.0) ? k0 : k1;
+  }
+  double r = k / scale;
+  if (r == 0.0) r = copysign(0.0, x);
+  return r;
+}
+
+__device__ __forceinline__ double py_round6(double x) {
+  return py_round_nd(x, 1e6, 8589934592.0 /* 2^33 */);
+}
+
+}  // namespace bce

@@ -1,0 +1,693 @@
+// consensus.hip -- batched core.compute_consensus (core.py:63-179) over CSR markets.
+//
+// Two kernels, chosen per market length bin:
+//
+//  consensus_seg<G, TM>   markets with n <= G (G in {8,16,32,64}).  One wave owns a tile of
+//                         TM markets.  Cooperative phase (lane = signal): each round loads
+//                         64/G markets (G lanes per market, coalesced), sorts (sid, input
+//                         index) keys with a register bitonic network (DPP / ds_swizzle),
+//                         dedups with ballots, sums duplicate probabilities in input order,
+//                         gathers reliability/confidence from the (L2-resident) source table
+//                         and stages per-unique (w, p*w, c*w) rows in LDS.  Serial phase
+//                         (lane = market): the LDS rows are read transposed and summed in
+//                         sorted-source order -- the reference's exact left-to-right order
+//                         (core.py:107-144) -- with all lanes busy on different markets.
+//                         Final phase (lane = unique slot): normalizedWeight and the
+//                         per-unique outputs, written coalesced at the CSR offsets.
+//
+//  consensus_long<IN_LDS> markets with n > 64.  One 256-thread workgroup per market:
+//                         64-bit (sid, index) keys bitonic-sorted in LDS (n <= 4096) or in
+//                         a global scratch slice (n > 4096), leaders of equal-sid runs sum
+//                         their run in input order, per-position (w, p*w, c*w) arrays, then
+//                         either the exact serial sum (one lane per chain) or a fixed-order
+//                         tree (BCE_MODE_FAST).
+//
+// FP contraction is off for the whole file: every mul/add rounds like CPython.
+#include "bce_device.hpp"
+#include "bce_internal.hpp"
+
+#pragma clang fp contract(off)
+
+namespace bce {
+
+struct ConsArgs {
+  const int64_t* offsets;
+  const int32_t* sid;
+  const double* prob;
+  const double* rel;
+  const double* conf;
+  const uint8_t* present;
+  const int32_t* list;  // nullable
+  int64_t n_list;       // number of markets to process
+  double* consensus;
+  double* confidence;
+  double* total_weight;
+  int32_t* n_unique;
+  int32_t* err_idx;   // nullable
+  int32_t* usid;      // nullable
+  double* weight;     // nullable
+  double* nweight;    // nullable
+  int32_t mode;
+  void* scratch;      // long kernel, global variant
+  int64_t scratch_stride;  // elements (keys) per workgroup slice
+};
+
+// ------------------------------------------------------------------------------------
+// short markets: wave-per-tile, lane-per-signal then lane-per-market
+// ------------------------------------------------------------------------------------
+template <int G, int TM>
+__global__ __launch_bounds__(64) void consensus_seg_kernel(ConsArgs a) {
+  static_assert(G == 8 || G == 16 || G == 32 || G == 64, "segment width");
+  constexpr int SPR = kWave / G;   // segments (markets) per round
+  constexpr int R = TM / SPR;      // rounds per tile
+  static_assert(R * SPR == TM, "tile must be a whole number of rounds");
+  constexpr int LOGG = (G == 8) ? 3 : (G == 16) ? 4 : (G == 32) ? 5 : 6;
+  constexpr int RS = G + 1;        // padded LDS row stride (conflict-free transposed reads)
+
+  __shared__ double sW[TM * RS];
+  __shared__ double sA[TM * RS];
+  __shared__ double sB[TM * RS];
+  __shared__ int32_t sU[TM * RS];
+  __shared__ int64_t sOff[TM];
+  __shared__ int32_t sN[TM];
+  __shared__ int32_t sM[TM];
+  __shared__ int32_t sNU[TM];
+  __shared__ int32_t sErr[TM];
+  __shared__ double sTot[TM];
+
+  const int lane = lane_id();
+  const int seg = lane / G;
+  const int t = lane & (G - 1);
+  const int seg_base = seg * G;
+  const unsigned long long segmask =
+      (G == 64) ? ~0ull : (((1ull << G) - 1ull) << seg_base);
+  const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+
+  const int64_t n_tiles = (a.n_list + TM - 1) / TM;
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    // ---- tile metadata -------------------------------------------------------------
+    if (lane < TM) {
+      const int64_t li = tile * TM + lane;
+      int32_t m = -1;
+      int64_t off = 0;
+      int32_t n = 0;
+      if (li < a.n_list) {
+        m = a.list ? a.list[li] : (int32_t)li;
+        off = a.offsets[m];
+        n = (int32_t)(a.offsets[m + 1] - off);
+      }
+      sM[lane] = m;
+      sOff[lane] = off;
+      sN[lane] = n;
+    }
+    __syncthreads();
+
+    // ---- prefetch every round's signals (coalesced within each G-lane segment) -----
+    int32_t sidv[R];
+    double pv[R];
+    bool valid[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int mk = r * SPR + seg;
+      const int32_t n = sN[mk];
+      valid[r] = t < n;
+      sidv[r] = 0;
+      pv[r] = 0.0;
+      if (valid[r]) {
+        const int64_t p = sOff[mk] + t;
+        sidv[r] = a.sid[p];
+        pv[r] = a.prob[p];
+      }
+    }
+
+    // ---- cooperative phase -----------------------------------------------------------
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int mk = r * SPR + seg;
+      unsigned key = valid[r] ? (((unsigned)sidv[r] << LOGG) | (unsigned)t) : kSent32;
+      key = bitonic_sort_seg<G>(key, t);
+      const bool kv = key != kSent32;
+      const int ssid = (int)(key >> LOGG);
+      const int sidx = (int)(key & (G - 1));
+      const double ps = pull_f64(pv[r], seg_base + sidx);  // probability in sorted order
+      const int prev = wave_shr1(ssid, -1);
+      const bool first = kv && (t == 0 || prev != ssid);
+      const unsigned long long fm = ballot(first);
+      const unsigned long long vm = ballot(kv);
+      const int j = __popcll(fm & segmask & below);
+      // run length of a leader: distance to the next leader / invalid lane / segment end
+      const unsigned long long bnd = fm | ~vm;
+      const unsigned long long above = (lane == 63) ? 0ull : (bnd >> (lane + 1));
+      const int seg_end = seg_base + G;
+      int run = above ? (__builtin_ctzll(above) + 1) : (64 - lane);
+      if (lane + run > seg_end) run = seg_end - lane;
+      const int myrun = first ? run : 1;
+      double s = 0.0 + ps;  // builtin sum() starts from int 0 (core.py:116)
+      double avg = s;
+      if (ballot(myrun > 1)) {  // duplicates present: sum the run in input order
+        for (int k = 1; k < G; ++k) {
+          const int src = (lane + k < 64) ? lane + k : 63;
+          const double pk = pull_f64(ps, src);
+          if (k < myrun) s += pk;
+          if (!ballot(k + 1 < myrun)) break;
+        }
+        avg = (myrun > 1) ? s / (double)myrun : s;
+      }
+      if (first) {
+        const double w = a.rel[ssid];      // core.py:111,119
+        const double c = a.conf[ssid];     // core.py:112
+        const bool cold = a.present[ssid] == 0;  // core.py:167-170
+        const int o = mk * RS + j;
+        sW[o] = w;
+        sA[o] = avg * w;                    // core.py:136
+        sB[o] = c * w;                      // core.py:142
+        sU[o] = ssid | (cold ? (int32_t)0x80000000 : 0);
+      }
+      // validate_input_payload range check (core.py:59-60) on the ORIGINAL order
+      const unsigned long long bad =
+          ballot(valid[r] && (pv[r] < 0.0 || pv[r] > 1.0)) & segmask;
+      if (t == 0) {
+        sNU[mk] = __popcll(fm & segmask);
+        sErr[mk] = bad ? (int)(__builtin_ctzll(bad) - seg_base) : -1;
+      }
+    }
+    __syncthreads();
+
+    // ---- serial phase: lane = market, exact left-to-right sums (core.py:107-144) ----
+    if (lane < TM) {
+      const int u = sNU[lane];
+      double total = 0.0, ws = 0.0, cs = 0.0;
+      const int base = lane * RS;
+      for (int jj = 0; jj < u; ++jj) {
+        total += sW[base + jj];
+        ws += sA[base + jj];
+        cs += sB[base + jj];
+      }
+      sTot[lane] = total;
+      const int32_t m = sM[lane];
+      if (m >= 0) {
+        const bool null_ = (total == 0.0);
+        a.consensus[m] = null_ ? 0.0 : ws / total;
+        a.confidence[m] = null_ ? 0.0 : cs / total;
+        a.total_weight[m] = total;
+        a.n_unique[m] = u;
+        if (a.err_idx) a.err_idx[m] = sErr[lane];
+      }
+    }
+    __syncthreads();
+
+    // ---- per-unique outputs (coalesced at CSR offsets) --------------------------------
+    if (a.usid || a.weight || a.nweight) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int mk = r * SPR + seg;
+        if (t < sNU[mk]) {
+          const int64_t p = sOff[mk] + t;
+          const double w = sW[mk * RS + t];
+          const double tot = sTot[mk];
+          if (a.usid) a.usid[p] = sU[mk * RS + t];
+          if (a.weight) a.weight[p] = w;
+          if (a.nweight) a.nweight[p] = (tot > 0.0) ? w / tot : 0.0;  // core.py:151
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// long markets: workgroup per market
+// ------------------------------------------------------------------------------------
+constexpr int kLongThreads = 256;
+constexpr int kLongMaxLds = 4096;
+
+// Fixed-order (deterministic) tree sum over the workgroup (BCE_MODE_FAST).
+__device__ __forceinline__ double block_sum_tree(double v, double* red) {
+  const int tid = threadIdx.x;
+  red[tid] = v;
+  __syncthreads();
+  for (int s = kLongThreads / 2; s > 0; s >>= 1) {
+    if (tid < s) red[tid] = red[tid] + red[tid + s];
+    __syncthreads();
+  }
+  const double r = red[0];
+  __syncthreads();
+  return r;
+}
+
+// Pass structure per market (all arrays length P = next pow2 >= n):
+//   0  keys[t] = sid<<32 | t, Pr[t] = prob (input order); first out-of-range index
+//   1  bitonic sort of keys (ascending sid, then input index == core.py:103,115)
+//   2  leaders (first position of each sid run) sum their run's probabilities in input
+//      order (core.py:116), compact index j by block scan -> Av[j] = avg, Sj[j] = sid
+//   3  per unique j: w = rel, W[j] = w, A[j] = avg*w, C[j] = conf*w, per-unique outputs
+//   4  ordered sums over j (exact: one lane per chain; fast: fixed tree)
+//   5  normalizedWeight[j] = W[j] / total
+template <bool IN_LDS>
+__global__ __launch_bounds__(kLongThreads) void consensus_long_kernel(ConsArgs a) {
+  constexpr int NT = kLongThreads;
+  constexpr int NW = NT / kWave;
+  constexpr int CAP = IN_LDS ? kLongMaxLds : 1;
+  __shared__ unsigned long long lKeys[CAP];  // keys, then W (double)
+  __shared__ double lP[CAP];                 // probabilities, then A
+  __shared__ double lC[CAP];                 // avg, then C
+  __shared__ int32_t lS[CAP];                // sid of unique j
+  __shared__ double red[NT];
+  __shared__ int32_t sInt[NW + 2];
+  __shared__ double sTot[4];
+
+  const int tid = threadIdx.x;
+  const int lane = lane_id();
+  const int wv = tid / kWave;
+  const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+
+  for (int64_t li = blockIdx.x; li < a.n_list; li += gridDim.x) {
+    const int32_t m = a.list ? a.list[li] : (int32_t)li;
+    const int64_t off = a.offsets[m];
+    const int32_t n = (int32_t)(a.offsets[m + 1] - off);
+    int P = 1;
+    while (P < n) P <<= 1;
+
+    unsigned long long* keys;
+    double* Pr;
+    double* Cv;
+    int32_t* Sj;
+    if constexpr (IN_LDS) {
+      keys = lKeys;
+      Pr = lP;
+      Cv = lC;
+      Sj = lS;
+    } else {
+      unsigned long long* base = reinterpret_cast<unsigned long long*>(a.scratch) +
+                                 (int64_t)blockIdx.x * 4 * a.scratch_stride;
+      keys = base;
+      Pr = reinterpret_cast<double*>(base + a.scratch_stride);
+      Cv = reinterpret_cast<double*>(base + 2 * a.scratch_stride);
+      Sj = reinterpret_cast<int32_t*>(base + 3 * a.scratch_stride);
+    }
+    double* Wv = reinterpret_cast<double*>(keys);
+
+    // ---- pass 0 ------------------------------------------------------------------------
+    if (tid == 0) sInt[0] = 0x7fffffff;
+    __syncthreads();
+    int myerr = 0x7fffffff;
+    for (int i = tid; i < P; i += NT) {
+      if (i < n) {
+        const double p = a.prob[off + i];
+        keys[i] = ((unsigned long long)(unsigned)a.sid[off + i] << 32) | (unsigned)i;
+        Pr[i] = p;
+        if ((p < 0.0 || p > 1.0) && i < myerr) myerr = i;  // core.py:59-60
+      } else {
+        keys[i] = kSent64;
+      }
+    }
+    if (myerr != 0x7fffffff) atomicMin(&sInt[0], myerr);
+    __syncthreads();
+    const int errv = sInt[0];
+
+    // ---- pass 1: bitonic sort ----------------------------------------------------------
+    for (int k = 2; k <= P; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int c = tid; c < (P >> 1); c += NT) {
+          const int lo = ((c & ~(j - 1)) << 1) | (c & (j - 1));
+          const int hi = lo | j;
+          const bool up = (lo & k) == 0;
+          const unsigned long long x = keys[lo], y = keys[hi];
+          if ((x > y) == up) {
+            keys[lo] = y;
+            keys[hi] = x;
+          }
+        }
+        __syncthreads();
+      }
+    }
+
+    // ---- pass 2: leaders, run sums in input order, compact index ------------------------
+    int u = 0;
+    for (int c0 = 0; c0 < n; c0 += NT) {
+      const int tpos = c0 + tid;
+      bool first = false;
+      int ssid = 0;
+      double avg = 0.0;
+      if (tpos < n) {
+        ssid = (int)(keys[tpos] >> 32);
+        first = (tpos == 0) || ((int)(keys[tpos - 1] >> 32) != ssid);
+        if (first) {
+          double s = 0.0;  // builtin sum() from 0 (core.py:116)
+          int cnt = 0;
+          for (int q = tpos; q < n; ++q) {
+            const unsigned long long kq = keys[q];
+            if ((int)(kq >> 32) != ssid) break;
+            s += Pr[(int)(kq & 0xffffffffu)];
+            ++cnt;
+          }
+          avg = (cnt > 1) ? s / (double)cnt : s;
+        }
+      }
+      const unsigned long long bm = ballot(first);
+      if (lane == 0) sInt[2 + wv] = __popcll(bm);
+      __syncthreads();
+      int before = u, chunk = 0;
+#pragma unroll
+      for (int q = 0; q < NW; ++q) {
+        const int cq = sInt[2 + q];
+        if (q < wv) before += cq;
+        chunk += cq;
+      }
+      if (first) {
+        const int j = before + __popcll(bm & below);
+        Cv[j] = avg;
+        Sj[j] = ssid;
+      }
+      u += chunk;
+      __syncthreads();
+    }
+
+    // ---- pass 3: gather + per-unique products (keys/probs are dead now) -----------------
+    for (int j = tid; j < u; j += NT) {
+      const int s = Sj[j];
+      const double w = a.rel[s];   // core.py:111,119
+      const double c = a.conf[s];  // core.py:112
+      const double avg = Cv[j];
+      Wv[j] = w;
+      Pr[j] = avg * w;  // core.py:136
+      Cv[j] = c * w;    // core.py:142
+      const int64_t p = off + j;
+      if (a.usid) a.usid[p] = s | (a.present[s] ? 0 : (int32_t)0x80000000);
+      if (a.weight) a.weight[p] = w;
+    }
+    __syncthreads();
+
+    // ---- pass 4: ordered sums ----------------------------------------------------------
+    if (a.mode == BCE_MODE_EXACT) {
+      if (tid < 3) {  // three independent chains on three lanes of wave 0
+        const double* arr = (tid == 0) ? Wv : (tid == 1) ? Pr : Cv;
+        double acc = 0.0;
+        for (int j = 0; j < u; ++j) acc += arr[j];
+        sTot[tid] = acc;
+      }
+      __syncthreads();
+    } else {
+      double pw = 0.0, pa = 0.0, pc = 0.0;
+      for (int j = tid; j < u; j += NT) {
+        pw += Wv[j];
+        pa += Pr[j];
+        pc += Cv[j];
+      }
+      const double tw = block_sum_tree(pw, red);
+      const double ta = block_sum_tree(pa, red);
+      const double tc = block_sum_tree(pc, red);
+      if (tid == 0) {
+        sTot[0] = tw;
+        sTot[1] = ta;
+        sTot[2] = tc;
+      }
+      __syncthreads();
+    }
+    const double total = sTot[0];
+    if (tid == 0) {
+      const bool null_ = (n == 0) || (total == 0.0);
+      a.consensus[m] = null_ ? 0.0 : sTot[1] / total;
+      a.confidence[m] = null_ ? 0.0 : sTot[2] / total;
+      a.total_weight[m] = total;
+      a.n_unique[m] = u;
+      if (a.err_idx) a.err_idx[m] = (errv == 0x7fffffff) ? -1 : errv;
+    }
+
+    // ---- pass 5: normalizedWeight (core.py:151) ----------------------------------------
+    if (a.nweight) {
+      for (int j = tid; j < u; j += NT) a.nweight[off + j] = (total > 0.0) ? Wv[j] / total : 0.0;
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace bce
+
+// ======================================================================================
+// host launchers
+// ======================================================================================
+namespace bce {
+namespace {
+
+template <int G, int TM>
+int launch_seg(const ConsArgs& a, hipStream_t st) {
+  const int64_t tiles = (a.n_list + TM - 1) / TM;
+  if (tiles == 0) return BCE_OK;
+  const int64_t cap = (int64_t)cu_count() * 24;  // grid-stride beyond ~24 waves per CU
+  const int grid = (int)(tiles < cap ? tiles : cap);
+  hipLaunchKernelGGL((consensus_seg_kernel<G, TM>), dim3(grid), dim3(64), 0, st, a);
+  return check_launch("consensus_seg_kernel");
+}
+
+int launch_seg_for_len(int max_len, const ConsArgs& a, hipStream_t st) {
+  if (max_len <= 8) return launch_seg<8, 64>(a, st);
+  if (max_len <= 16) return launch_seg<16, 32>(a, st);
+  if (max_len <= 32) return launch_seg<32, 16>(a, st);
+  return launch_seg<64, 8>(a, st);
+}
+
+int launch_long_lds(const ConsArgs& a, hipStream_t st) {
+  if (a.n_list == 0) return BCE_OK;
+  const int64_t cap = (int64_t)cu_count() * 2;
+  const int grid = (int)(a.n_list < cap ? a.n_list : cap);
+  hipLaunchKernelGGL((consensus_long_kernel<true>), dim3(grid), dim3(kLongThreads), 0, st, a);
+  return check_launch("consensus_long_kernel<lds>");
+}
+
+constexpr int kHugeGrid = 512;
+
+int64_t next_pow2(int64_t n) {
+  int64_t p = 1;
+  while (p < n) p <<= 1;
+  return p;
+}
+
+int launch_long_global(ConsArgs a, int64_t max_len, void* scratch, int64_t scratch_bytes,
+                       hipStream_t st) {
+  if (a.n_list == 0) return BCE_OK;
+  const int grid = (int)(a.n_list < kHugeGrid ? a.n_list : kHugeGrid);
+  const int64_t P = next_pow2(max_len);
+  const int64_t need = (int64_t)grid * 4 * P * 8;
+  BCE_REQUIRE(scratch && scratch_bytes >= need, "consensus: scratch too small (%lld < %lld)",
+              (long long)scratch_bytes, (long long)need);
+  a.scratch = scratch;
+  a.scratch_stride = P;
+  hipLaunchKernelGGL((consensus_long_kernel<false>), dim3(grid), dim3(kLongThreads), 0, st, a);
+  return check_launch("consensus_long_kernel<global>");
+}
+
+__global__ void max_len_kernel(const int64_t* offsets, int64_t n, const int32_t* list, int64_t n_list,
+                               unsigned long long* out) {
+  int64_t best = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n_list;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = list ? list[i] : i;
+    const int64_t len = offsets[m + 1] - offsets[m];
+    best = len > best ? len : best;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const int64_t x = __shfl_xor(best, o);
+    best = x > best ? x : best;
+  }
+  if ((threadIdx.x & 63) == 0) atomicMax(out, (unsigned long long)best);
+}
+
+int check_common(const int64_t* offsets, int64_t n_markets, const int32_t* sid, const double* prob,
+                 const double* rel, const double* conf, const uint8_t* present, int32_t n_sources,
+                 double* consensus, double* confidence, double* total_weight, int32_t* n_unique) {
+  BCE_REQUIRE(n_markets >= 0, "consensus: n_markets < 0");
+  BCE_REQUIRE(n_markets == 0 || offsets, "consensus: offsets is NULL");
+  BCE_REQUIRE(n_markets == 0 || (consensus && confidence && total_weight && n_unique),
+              "consensus: per-market outputs must be non-NULL");
+  BCE_REQUIRE(n_sources >= 0 && (n_sources == 0 || (rel && conf && present)),
+              "consensus: source table is NULL");
+  (void)sid;
+  (void)prob;
+  return BCE_OK;
+}
+
+}  // namespace
+}  // namespace bce
+
+using namespace bce;
+
+extern "C" int bce_consensus_csr(const int64_t* offsets, int64_t n_markets, const int32_t* sid,
+                                 const double* prob, int64_t n_signals, const double* rel,
+                                 const double* conf, const uint8_t* present, int32_t n_sources,
+                                 const int32_t* market_list, int64_t n_list, int32_t max_len,
+                                 int32_t mode, double* consensus, double* confidence,
+                                 double* total_weight, int32_t* n_unique, int32_t* err_idx,
+                                 int32_t* usid, double* weight, double* nweight, void* stream) {
+  int rc = check_common(offsets, n_markets, sid, prob, rel, conf, present, n_sources, consensus,
+                        confidence, total_weight, n_unique);
+  if (rc) return rc;
+  BCE_REQUIRE(mode == BCE_MODE_EXACT || mode == BCE_MODE_FAST, "consensus: bad mode %d", mode);
+  BCE_REQUIRE(n_signals == 0 || (sid && prob), "consensus: sid/prob NULL");
+  hipStream_t st = as_stream(stream);
+  ConsArgs a{};
+  a.offsets = offsets; a.sid = sid; a.prob = prob; a.rel = rel; a.conf = conf; a.present = present;
+  a.list = market_list; a.n_list = market_list ? n_list : n_markets;
+  a.consensus = consensus; a.confidence = confidence; a.total_weight = total_weight;
+  a.n_unique = n_unique; a.err_idx = err_idx; a.usid = usid; a.weight = weight; a.nweight = nweight;
+  a.mode = mode;
+  if (a.n_list == 0) return BCE_OK;
+  int64_t L = max_len;
+  if (L <= 0) {  // unknown: measure on device (synchronises)
+    unsigned long long* d = nullptr;
+    BCE_HIP(hipMallocAsync((void**)&d, sizeof(unsigned long long), st));
+    BCE_HIP(hipMemsetAsync(d, 0, sizeof(unsigned long long), st));
+    hipLaunchKernelGGL(max_len_kernel, dim3(256), dim3(256), 0, st, offsets, n_markets, market_list,
+                       a.n_list, d);
+    unsigned long long h = 0;
+    BCE_HIP(hipMemcpyAsync(&h, d, sizeof h, hipMemcpyDeviceToHost, st));
+    BCE_HIP(hipFreeAsync(d, st));
+    BCE_HIP(hipStreamSynchronize(st));
+    L = (int64_t)h;
+  }
+  // the 32-bit (sid, index) key of the segment kernel needs sid < 2^(31 - log2 G)
+  if (L <= 64 && n_sources <= (1 << 25)) return launch_seg_for_len((int)(L < 1 ? 1 : L), a, st);
+  if (L <= kLongMaxLds) return launch_long_lds(a, st);
+  const int grid = (int)(a.n_list < kHugeGrid ? a.n_list : kHugeGrid);
+  const int64_t bytes = (int64_t)grid * 4 * next_pow2(L) * 8;
+  void* scratch = nullptr;
+  BCE_HIP(hipMallocAsync(&scratch, (size_t)bytes, st));
+  rc = launch_long_global(a, L, scratch, bytes, st);
+  BCE_HIP(hipFreeAsync(scratch, st));
+  return rc;
+}
+
+static int bin_of(int64_t n) {
+  if (n <= 8) return 0;
+  if (n <= 16) return 1;
+  if (n <= 32) return 2;
+  if (n <= 64) return 3;
+  if (n <= kLongMaxLds) return 4;
+  return 5;
+}
+
+extern "C" int bce_plan_bins(const int64_t* offsets_host, int64_t n_markets, int32_t* order_host,
+                             int64_t* bin_start_host, int32_t* max_len_host) {
+  BCE_REQUIRE(n_markets >= 0 && offsets_host && order_host && bin_start_host,
+              "plan_bins: NULL argument");
+  int64_t cnt[BCE_NBINS] = {0};
+  int64_t mx = 0;
+  for (int64_t m = 0; m < n_markets; ++m) {
+    const int64_t n = offsets_host[m + 1] - offsets_host[m];
+    BCE_REQUIRE(n >= 0, "plan_bins: offsets not monotone at market %lld", (long long)m);
+    cnt[bin_of(n)]++;
+    mx = n > mx ? n : mx;
+  }
+  bin_start_host[0] = 0;
+  for (int b = 0; b < BCE_NBINS; ++b) bin_start_host[b + 1] = bin_start_host[b] + cnt[b];
+  int64_t pos[BCE_NBINS];
+  for (int b = 0; b < BCE_NBINS; ++b) pos[b] = bin_start_host[b];
+  for (int64_t m = 0; m < n_markets; ++m) {
+    const int64_t n = offsets_host[m + 1] - offsets_host[m];
+    order_host[pos[bin_of(n)]++] = (int32_t)m;
+  }
+  if (max_len_host) *max_len_host = (int32_t)(mx > 0x7fffffff ? 0x7fffffff : mx);
+  return BCE_OK;
+}
+
+extern "C" int64_t bce_consensus_scratch_bytes(const int64_t* offsets_host, const int32_t* order_host,
+                                               const int64_t* bin_start_host) {
+  const int64_t b0 = bin_start_host[BCE_NBINS - 1], b1 = bin_start_host[BCE_NBINS];
+  if (b1 <= b0) return 0;
+  int64_t mx = 0;
+  for (int64_t i = b0; i < b1; ++i) {
+    const int32_t m = order_host[i];
+    const int64_t n = offsets_host[m + 1] - offsets_host[m];
+    mx = n > mx ? n : mx;
+  }
+  const int64_t cnt = b1 - b0;
+  const int grid = (int)(cnt < kHugeGrid ? cnt : kHugeGrid);
+  return (int64_t)grid * 4 * next_pow2(mx) * 8;
+}
+
+extern "C" int bce_consensus_planned(const int64_t* offsets, int64_t n_markets, const int32_t* sid,
+                                     const double* prob, int64_t n_signals, const double* rel,
+                                     const double* conf, const uint8_t* present, int32_t n_sources,
+                                     const int32_t* order, const int64_t* bin_start_host,
+                                     int32_t mode, double* consensus, double* confidence,
+                                     double* total_weight, int32_t* n_unique, int32_t* err_idx,
+                                     int32_t* usid, double* weight, double* nweight, void* scratch,
+                                     int64_t scratch_bytes, void* stream) {
+  int rc = check_common(offsets, n_markets, sid, prob, rel, conf, present, n_sources, consensus,
+                        confidence, total_weight, n_unique);
+  if (rc) return rc;
+  BCE_REQUIRE(bin_start_host && (order || n_markets == 0), "planned: missing plan");
+  BCE_REQUIRE(mode == BCE_MODE_EXACT || mode == BCE_MODE_FAST, "planned: bad mode %d", mode);
+  BCE_REQUIRE(n_signals == 0 || (sid && prob), "planned: sid/prob NULL");
+  hipStream_t st = as_stream(stream);
+  ConsArgs base{};
+  base.offsets = offsets; base.sid = sid; base.prob = prob; base.rel = rel; base.conf = conf;
+  base.present = present; base.consensus = consensus; base.confidence = confidence;
+  base.total_weight = total_weight; base.n_unique = n_unique; base.err_idx = err_idx;
+  base.usid = usid; base.weight = weight; base.nweight = nweight; base.mode = mode;
+  const bool seg_ok = n_sources <= (1 << 25);
+  for (int b = 0; b < BCE_NBINS; ++b) {
+    ConsArgs a = base;
+    a.list = order + bin_start_host[b];
+    a.n_list = bin_start_host[b + 1] - bin_start_host[b];
+    if (a.n_list == 0) continue;
+    if (b <= 3 && seg_ok) {
+      static const int lens[4] = {8, 16, 32, 64};
+      rc = launch_seg_for_len(lens[b], a, st);
+    } else if (b <= 4) {
+      rc = launch_long_lds(a, st);
+    } else {
+      int64_t mx = 0;
+      (void)mx;
+      // scratch stride from the caller's sizing (bce_consensus_scratch_bytes)
+      const int grid = (int)(a.n_list < kHugeGrid ? a.n_list : kHugeGrid);
+      const int64_t P = scratch_bytes / ((int64_t)grid * 4 * 8);
+      BCE_REQUIRE(P > kLongMaxLds, "planned: scratch too small for the >4096 bin");
+      a.scratch = scratch;
+      a.scratch_stride = P;
+      hipLaunchKernelGGL((consensus_long_kernel<false>), dim3(grid), dim3(kLongThreads), 0, st, a);
+      rc = check_launch("consensus_long_kernel<global>");
+    }
+    if (rc) return rc;
+  }
+  return BCE_OK;
+}
+
+// ======================================================================================
+// validation only: core.validate_input_payload range check (core.py:59-60)
+// ======================================================================================
+namespace bce {
+__global__ __launch_bounds__(256) void validate_kernel(const int64_t* offsets, int64_t n_markets,
+                                                       const double* prob, int32_t* err_idx) {
+  const int lane = lane_id();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t m = wave; m < n_markets; m += nwaves) {
+    const int64_t a = offsets[m], b = offsets[m + 1];
+    int32_t e = -1;
+    for (int64_t base = a; base < b; base += 64) {
+      const int64_t i = base + lane;
+      const double p = (i < b) ? prob[i] : 0.5;
+      const unsigned long long bad = ballot(p < 0.0 || p > 1.0);  // NaN passes
+      if (bad) {
+        e = (int32_t)(base - a) + __builtin_ctzll(bad);
+        break;
+      }
+    }
+    if (lane == 0) err_idx[m] = e;
+  }
+}
+}  // namespace bce
+
+extern "C" int bce_validate_csr(const int64_t* offsets, int64_t n_markets, const double* prob,
+                                int32_t* err_idx, void* stream) {
+  BCE_REQUIRE(n_markets >= 0, "validate: n_markets < 0");
+  if (n_markets == 0) return BCE_OK;
+  BCE_REQUIRE(offsets && prob && err_idx, "validate: NULL argument");
+  int64_t blocks = (n_markets + 3) / 4;
+  const int64_t cap = (int64_t)cu_count() * 16;
+  if (blocks > cap) blocks = cap;
+  hipLaunchKernelGGL(validate_kernel, dim3((int)blocks), dim3(256), 0, as_stream(stream), offsets,
+                     n_markets, prob, err_idx);
+  return check_launch("validate_kernel");
+}

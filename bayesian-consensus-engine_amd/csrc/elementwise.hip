@@ -1,0 +1,225 @@
+// elementwise.hip -- fused elementwise kernels over the dense source table.
+//
+//   decay_view     get_reliability(apply_decay=True)  (reliability.py:110-131,
+//                  decay.py:61-145): view = max(m, min(1, m + (r-m)*2^(-days/h)))
+//   outcome_update compute_update / update_reliability (reliability.py:142-183)
+//   replay_step    config 4: both in one pass (view at `now`, then the update)
+//
+// HBM-bound: each thread owns two consecutive sources so every table stream is read
+// and written with 16-byte accesses.  FP contraction off (CPython rounding).
+#include "bce_device.hpp"
+#include "bce_internal.hpp"
+
+#pragma clang fp contract(off)
+
+namespace bce {
+
+struct DecayConst {
+  int64_t now_us;
+  double half_life;
+  double min_rel;
+  double default_rel;
+  double default_conf;
+};
+
+// decay.py:52-58 and 90-100, with days from decay.py:140-145.
+__device__ __forceinline__ double decayed(double r, int64_t t_us, const DecayConst& k) {
+  if (t_us == BCE_NO_TIMESTAMP) return r;
+  const double secs = (double)(k.now_us - t_us) / 1e6;  // timedelta.total_seconds()
+  const double days = py_max(0.0, secs / 86400.0);
+  if (!(days > 0.0)) return r;
+  const double f = pow(2.0, -days / k.half_life);
+  const double d = k.min_rel + (r - k.min_rel) * f;
+  return py_max(k.min_rel, py_min(1.0, d));
+}
+
+// reliability.py:163-173 for one participant.
+__device__ __forceinline__ void update_one(double& r, double& c, bool correct) {
+  const double direction = correct ? 1.0 : -1.0;
+  const double raw = 0.15 * direction;                      // _BASE_LEARNING_RATE
+  const double capped = py_max(-0.10, py_min(0.10, raw));   // MAX_UPDATE_STEP
+  r = py_max(0.0, py_min(1.0, r + capped));
+  c = py_min(1.0, c + (1.0 - c) * 0.10);
+}
+
+__global__ __launch_bounds__(256) void decay_view_kernel(int64_t n, const double* __restrict__ rel,
+                                                         const int64_t* __restrict__ t_us,
+                                                         const uint8_t* __restrict__ present,
+                                                         DecayConst k, double* __restrict__ view) {
+  const int64_t npair = n >> 1;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < npair;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const double2 r = reinterpret_cast<const double2*>(rel)[i];
+    const longlong2 t = reinterpret_cast<const longlong2*>(t_us)[i];
+    double v0 = decayed(r.x, t.x, k), v1 = decayed(r.y, t.y, k);
+    if (present) {
+      const uchar2 p = reinterpret_cast<const uchar2*>(present)[i];
+      if (!p.x) v0 = k.default_rel;
+      if (!p.y) v1 = k.default_rel;
+    }
+    reinterpret_cast<double2*>(view)[i] = make_double2(v0, v1);
+  }
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    const int64_t s = n - 1;
+    double v = decayed(rel[s], t_us[s], k);
+    if (present && !present[s]) v = k.default_rel;
+    view[s] = v;
+  }
+}
+
+// decay.compute_decay_factor / apply_reliability_decay on elapsed-day arrays
+// (decay.py:52-58, 90-100).
+__global__ __launch_bounds__(256) void decay_apply_kernel(int64_t n, const double* __restrict__ rel,
+                                                          const double* __restrict__ days, double h,
+                                                          double mn, double* __restrict__ out,
+                                                          double* __restrict__ factor) {
+  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < n;
+       s += (int64_t)gridDim.x * blockDim.x) {
+    const double e = days[s];
+    const double f = (e <= 0) ? 1.0 : pow(2.0, -e / h);
+    if (factor) factor[s] = f;
+    if (out) {
+      const double r = rel[s];
+      if (e <= 0) {
+        out[s] = r;
+      } else {
+        const double d = mn + (r - mn) * f;
+        out[s] = py_max(mn, py_min(1.0, d));
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void outcome_update_kernel(int64_t n, double* rel, double* conf,
+                                                             int64_t* t_us, uint8_t* present,
+                                                             const uint8_t* __restrict__ flags,
+                                                             DecayConst k) {
+  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < n;
+       s += (int64_t)gridDim.x * blockDim.x) {
+    const uint8_t f = flags[s];
+    if (!(f & 1)) continue;
+    const bool pres = present ? present[s] != 0 : true;
+    double r = pres ? rel[s] : k.default_rel;   // reliability.py:133-140 cold start
+    double c = pres ? conf[s] : k.default_conf;
+    update_one(r, c, (f & 2) != 0);
+    rel[s] = r;
+    conf[s] = c;
+    t_us[s] = k.now_us;  // reliability.py:175
+    if (present) present[s] = 1;
+  }
+}
+
+// Config-4 step.  Absent rows must carry the baked cold-start values
+// (rel = default_rel, conf = default_conf, t = BCE_NO_TIMESTAMP), so the view needs no
+// `present` read; `present` is only written (rows that now exist).
+__global__ __launch_bounds__(256) void replay_step_kernel(int64_t n, double* __restrict__ rel,
+                                                          double* __restrict__ conf,
+                                                          int64_t* __restrict__ t_us,
+                                                          uint8_t* __restrict__ present,
+                                                          const uint8_t* __restrict__ flags2,
+                                                          DecayConst k, double* __restrict__ view) {
+  const int64_t npair = n >> 1;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < npair;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    double2 r = reinterpret_cast<const double2*>(rel)[i];
+    longlong2 t = reinterpret_cast<const longlong2*>(t_us)[i];
+    const uint8_t fb = flags2[i >> 1];
+    const unsigned f = (fb >> ((i & 1) * 4)) & 0xF;  // 2 bits per source, sources 2i, 2i+1
+    reinterpret_cast<double2*>(view)[i] = make_double2(decayed(r.x, t.x, k), decayed(r.y, t.y, k));
+    if (f & 0x5) {  // any participant in the pair
+      double2 c = reinterpret_cast<const double2*>(conf)[i];
+      if (f & 1) {
+        update_one(r.x, c.x, (f & 2) != 0);
+        t.x = k.now_us;
+        present[2 * i] = 1;
+      }
+      if (f & 4) {
+        update_one(r.y, c.y, (f & 8) != 0);
+        t.y = k.now_us;
+        present[2 * i + 1] = 1;
+      }
+      reinterpret_cast<double2*>(rel)[i] = r;
+      reinterpret_cast<double2*>(conf)[i] = c;
+      reinterpret_cast<longlong2*>(t_us)[i] = t;
+    }
+  }
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    const int64_t s = n - 1;
+    const unsigned f = (flags2[s >> 2] >> (2 * (s & 3))) & 3;
+    double r = rel[s];
+    view[s] = decayed(r, t_us[s], k);
+    if (f & 1) {
+      double c = conf[s];
+      update_one(r, c, (f & 2) != 0);
+      rel[s] = r;
+      conf[s] = c;
+      t_us[s] = k.now_us;
+      present[s] = 1;
+    }
+  }
+}
+
+static int grid_for(int64_t work, int threads) {
+  int64_t g = (work + threads - 1) / threads;
+  const int64_t cap = (int64_t)cu_count() * 16;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace bce
+
+using namespace bce;
+
+extern "C" int bce_decay_view(int64_t n, const double* rel, const int64_t* t_us,
+                              const uint8_t* present, int64_t now_us, double half_life_days,
+                              double min_rel, double default_rel, double* view, void* stream) {
+  BCE_REQUIRE(n >= 0, "decay_view: n < 0");
+  if (n == 0) return BCE_OK;
+  BCE_REQUIRE(rel && t_us && view, "decay_view: NULL array");
+  BCE_REQUIRE(((uintptr_t)rel | (uintptr_t)t_us | (uintptr_t)view) % 16 == 0,
+              "decay_view: arrays must be 16-byte aligned");
+  BCE_REQUIRE(present == nullptr || (uintptr_t)present % 2 == 0, "decay_view: present alignment");
+  DecayConst k{now_us, half_life_days, min_rel, default_rel, 0.25};
+  hipLaunchKernelGGL(decay_view_kernel, dim3(grid_for(n / 2 + 1, 256)), dim3(256), 0,
+                     as_stream(stream), n, rel, t_us, present, k, view);
+  return check_launch("decay_view_kernel");
+}
+
+extern "C" int bce_decay_apply(int64_t n, const double* rel, const double* elapsed_days,
+                               double half_life_days, double min_rel, double* out, double* factor,
+                               void* stream) {
+  BCE_REQUIRE(n >= 0, "decay_apply: n < 0");
+  if (n == 0) return BCE_OK;
+  BCE_REQUIRE(elapsed_days && (out == nullptr || rel) && (out || factor), "decay_apply: NULL array");
+  hipLaunchKernelGGL(decay_apply_kernel, dim3(grid_for(n, 256)), dim3(256), 0, as_stream(stream), n,
+                     rel, elapsed_days, half_life_days, min_rel, out, factor);
+  return check_launch("decay_apply_kernel");
+}
+
+extern "C" int bce_outcome_update(int64_t n, double* rel, double* conf, int64_t* t_us,
+                                  uint8_t* present, const uint8_t* flags, int64_t now_us,
+                                  double default_rel, double default_conf, void* stream) {
+  BCE_REQUIRE(n >= 0, "outcome_update: n < 0");
+  if (n == 0) return BCE_OK;
+  BCE_REQUIRE(rel && conf && t_us && flags, "outcome_update: NULL array");
+  DecayConst k{now_us, 30.0, 0.1, default_rel, default_conf};
+  hipLaunchKernelGGL(outcome_update_kernel, dim3(grid_for(n, 256)), dim3(256), 0,
+                     as_stream(stream), n, rel, conf, t_us, present, flags, k);
+  return check_launch("outcome_update_kernel");
+}
+
+extern "C" int bce_replay_step(int64_t n, double* rel, double* conf, int64_t* t_us,
+                               uint8_t* present, const uint8_t* flags2, int64_t now_us,
+                               double half_life_days, double min_rel, double default_rel,
+                               double default_conf, double* view, void* stream) {
+  BCE_REQUIRE(n >= 0, "replay_step: n < 0");
+  if (n == 0) return BCE_OK;
+  BCE_REQUIRE(rel && conf && t_us && present && flags2 && view, "replay_step: NULL array");
+  BCE_REQUIRE(((uintptr_t)rel | (uintptr_t)conf | (uintptr_t)t_us | (uintptr_t)view) % 16 == 0,
+              "replay_step: arrays must be 16-byte aligned");
+  DecayConst k{now_us, half_life_days, min_rel, default_rel, default_conf};
+  hipLaunchKernelGGL(replay_step_kernel, dim3(grid_for(n / 2 + 1, 256)), dim3(256), 0,
+                     as_stream(stream), n, rel, conf, t_us, present, flags2, k, view);
+  return check_launch("replay_step_kernel");
+}

@@ -1,0 +1,383 @@
+// tiebreak.hip -- DeterministicTieBreaker.resolve (tiebreak.py:73-152) per CSR market.
+//
+// One wave per market (n <= 64 agents; lane = agent), or one 256-thread workgroup per
+// market with the agents staged in LDS (64 < n <= 4096).  Grouping key = CPython
+// round(prediction, 6) (tiebreak.py:54) restated exactly (bce::py_round_nd).  A group's
+// leader is its first-seen member, so groups come out in dict insertion order for free.
+// Group sums (weight, confidence) run in input order, max reliability keeps the first
+// maximum (builtin max), and the winner is the lexicographic max of
+// (density, max_rel, -key) -- distinct groups never tie on the full tuple, so any
+// reduction order selects the same winner.
+#include "bce_device.hpp"
+#include "bce_internal.hpp"
+
+#pragma clang fp contract(off)
+
+namespace bce {
+
+struct TbArgs {
+  const int64_t* offsets;
+  int64_t n_markets;
+  const double* pred;
+  const double* conf;
+  const double* weight;
+  const double* rel;
+  double* winner;
+  int32_t* label;
+  int32_t* n_groups;
+  double* variance;
+  double* g_key;
+  int32_t* g_count;
+  double* g_density;
+  double* g_avgconf;
+  double* g_maxrel;
+  double rscale;   // 10^ndigits
+  double rthresh;  // see py_round_nd
+};
+
+__device__ __forceinline__ bool key_eq(double a, double b) { return a == b; }  // -0.0 == 0.0
+
+// (d1, m1, k1) strictly better than (d2, m2, k2) under Python tuple order of
+// (density, max_reliability, -key).
+__device__ __forceinline__ bool tb_better(double d1, double m1, double k1, double d2, double m2,
+                                          double k2) {
+  if (d1 != d2) return d1 > d2;
+  if (m1 != m2) return m1 > m2;
+  return (-k1) > (-k2);
+}
+
+__device__ __forceinline__ double rl_f64(double v, int l) {
+  int2 x = *reinterpret_cast<int2*>(&v);
+  int2 y;
+  y.x = __builtin_amdgcn_readlane(x.x, l);
+  y.y = __builtin_amdgcn_readlane(x.y, l);
+  return *reinterpret_cast<double*>(&y);
+}
+
+__global__ __launch_bounds__(256) void tiebreak_wave_kernel(TbArgs a, const int32_t* list,
+                                                            int64_t n_list) {
+  const int lane = lane_id();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int64_t li = wave; li < n_list; li += nwaves) {
+    const int64_t m = list ? list[li] : li;
+    const int64_t off = a.offsets[m];
+    const int n = (int)(a.offsets[m + 1] - off);
+    if (n == 0) {  // tiebreak.py:86-87 (ValueError)
+      if (lane == 0) {
+        a.winner[m] = 0.0; a.label[m] = -1; a.n_groups[m] = -1; a.variance[m] = 0.0;
+      }
+      continue;
+    }
+    const bool v = lane < n;
+    double p = 0.0, c = 0.0, w = 0.0, r = 0.0;
+    if (v) {
+      p = a.pred[off + lane];
+      c = a.conf[off + lane];
+      w = a.weight[off + lane];
+      r = a.rel[off + lane];
+    }
+    if (n == 1) {  // tiebreak.py:89-96
+      if (lane == 0) {
+        a.winner[m] = p; a.label[m] = BCE_TB_SINGLE_AGENT; a.n_groups[m] = 1; a.variance[m] = 0.0;
+        if (a.g_key) a.g_key[off] = p;
+        if (a.g_count) a.g_count[off] = 1;
+        if (a.g_density) a.g_density[off] = w;
+        if (a.g_avgconf) a.g_avgconf[off] = c;
+        if (a.g_maxrel) a.g_maxrel[off] = r;
+      }
+      continue;
+    }
+    const double key = py_round_nd(p, a.rscale, a.rthresh);
+    // leader = first index with an equal key (dict insertion order)
+    int leader = lane;
+    for (int j = 0; j < n; ++j) {
+      const double kj = rl_f64(key, j);
+      if (v && j < leader && key_eq(kj, key)) leader = j;
+    }
+    const bool is_leader = v && leader == lane;
+    // group metrics in input order (tiebreak.py:58-71), accumulated by the leader lane
+    double tot = 0.0, cs = 0.0, mx = r;
+    int cnt = 0;
+    double csum_all = 0.0;
+    for (int j = 0; j < n; ++j) {
+      const int lj = __builtin_amdgcn_readlane(leader, j);
+      const double wj = rl_f64(w, j), cj = rl_f64(c, j), rj = rl_f64(r, j);
+      csum_all += cj;
+      if (lj == lane) {
+        tot += wj;
+        cs += cj;
+        ++cnt;
+        if (j != lane && rj > mx) mx = rj;  // builtin max: first maximum kept
+      }
+    }
+    const double dens = is_leader ? tot / (double)cnt : 0.0;
+    const double avgc = is_leader ? cs / (double)cnt : 0.0;
+    // variance of all confidences (tiebreak.py:104-106): sequential sums
+    const double mean = csum_all / (double)n;
+    double vs = 0.0;
+    for (int j = 0; j < n; ++j) {
+      const double d = rl_f64(c, j) - mean;
+      vs += d * d;
+    }
+    const unsigned long long lm = ballot(is_leader);
+    const int ng = __popcll(lm);
+    // winner: lexicographic max over leaders
+    int best = -1;
+    double bd = 0.0, bm = 0.0, bk = 0.0;
+    for (int j = 0; j < n; ++j) {
+      if (!((lm >> j) & 1ull)) continue;
+      const double dj = rl_f64(dens, j), mj = rl_f64(mx, j), kj = rl_f64(key, j);
+      if (best < 0 || tb_better(dj, mj, kj, bd, bm, bk)) {
+        best = j; bd = dj; bm = mj; bk = kj;
+      }
+    }
+    const bool tie = is_leader && lane != best && dens == bd && mx == bm;
+    int lab = BCE_TB_WEIGHT_DENSITY;
+    if (ng == 1) lab = BCE_TB_UNANIMOUS;
+    else if (ballot(tie)) lab = BCE_TB_PREDICTION_VALUE_SMALLEST;
+    if (lane == 0) {
+      a.winner[m] = bk;
+      a.label[m] = lab;
+      a.n_groups[m] = ng;
+      a.variance[m] = vs / (double)n;
+    }
+    if (is_leader) {
+      const int64_t g = off + __popcll(lm & below);
+      if (a.g_key) a.g_key[g] = key;
+      if (a.g_count) a.g_count[g] = cnt;
+      if (a.g_density) a.g_density[g] = dens;
+      if (a.g_avgconf) a.g_avgconf[g] = avgc;
+      if (a.g_maxrel) a.g_maxrel[g] = mx;
+    }
+  }
+}
+
+// 64 < n <= 4096: one workgroup per market.  (rounded key, index) pairs are bitonic-
+// sorted in LDS, so every group is a run whose members appear in input order; the run
+// head owns the group (its first member is the dict-insertion leader).
+constexpr int kTbThreads = 256;
+constexpr int kTbMax = 4096;
+constexpr unsigned long long kNanKey = 0xFFFFFFFFFFFFF000ull;
+
+__global__ __launch_bounds__(kTbThreads) void tiebreak_block_kernel(TbArgs a, const int32_t* list,
+                                                                    int64_t n_list) {
+  __shared__ unsigned long long sk[kTbMax];  // ordered key bits
+  __shared__ int32_t sIdx[kTbMax];           // original index
+  __shared__ int32_t sRank[kTbMax];          // leader flag, then first-seen rank
+  __shared__ double cD[kTbThreads], cM[kTbThreads], cK[kTbThreads];
+  __shared__ int32_t cI[kTbThreads];
+  __shared__ int32_t sW[kTbThreads / 64 + 1];
+  __shared__ int32_t sFlag;
+  __shared__ double sVar;
+  const int tid = threadIdx.x;
+  const int lane = lane_id();
+  const int wv = tid >> 6;
+  const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int64_t li = blockIdx.x; li < n_list; li += gridDim.x) {
+    const int64_t m = list[li];
+    const int64_t off = a.offsets[m];
+    const int n = (int)(a.offsets[m + 1] - off);
+    int P = 1;
+    while (P < n) P <<= 1;
+    for (int i = tid; i < P; i += kTbThreads) {
+      unsigned long long kk = ~0ull;
+      if (i < n) {
+        double k = py_round_nd(a.pred[off + i], a.rscale, a.rthresh);
+        if (k == 0.0) k = 0.0;  // -0.0 and 0.0 share one dict slot
+        unsigned long long b = (unsigned long long)__double_as_longlong(k);
+        kk = (b >> 63) ? ~b : (b | 0x8000000000000000ull);  // total order on doubles
+        if (k != k) kk = kNanKey;                            // NaN never equals: own group
+        sRank[i] = 0;
+      }
+      sk[i] = kk;
+      sIdx[i] = i;
+    }
+    if (tid == 0) sFlag = 0;
+    __syncthreads();
+    for (int k = 2; k <= P; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int c = tid; c < (P >> 1); c += kTbThreads) {
+          const int lo = ((c & ~(j - 1)) << 1) | (c & (j - 1));
+          const int hi = lo | j;
+          const bool up = (lo & k) == 0;
+          const unsigned long long x = sk[lo], y = sk[hi];
+          const int xi = sIdx[lo], yi = sIdx[hi];
+          const bool gt = (x > y) || (x == y && xi > yi);
+          if (gt == up) {
+            sk[lo] = y; sk[hi] = x;
+            sIdx[lo] = yi; sIdx[hi] = xi;
+          }
+        }
+        __syncthreads();
+      }
+    }
+    // run heads mark their leader (first-seen member) in original index space
+    for (int t = tid; t < n; t += kTbThreads) {
+      const bool head = (t == 0) || sk[t] == kNanKey || sk[t - 1] != sk[t];
+      if (head) sRank[sIdx[t]] = 1;
+    }
+    __syncthreads();
+    // exclusive scan of leader flags in original order -> first-seen group rank
+    int carry = 0;
+    for (int c0 = 0; c0 < n; c0 += kTbThreads) {
+      const int i = c0 + tid;
+      const bool f = (i < n) && sRank[i] != 0;
+      const unsigned long long bm = ballot(f);
+      if (lane == 0) sW[wv] = __popcll(bm);
+      __syncthreads();
+      int before = carry, chunk = 0;
+      for (int q = 0; q < kTbThreads / 64; ++q) {
+        if (q < wv) before += sW[q];
+        chunk += sW[q];
+      }
+      if (i < n) sRank[i] = f ? before + __popcll(bm & below) : -1;
+      carry += chunk;
+      __syncthreads();
+    }
+    const int ng = carry;
+    // group metrics by run heads (members in input order), winner candidates
+    double bd = 0.0, bmx = 0.0, bk = 0.0;
+    int bi = -1;
+    for (int t = tid; t < n; t += kTbThreads) {
+      const bool head = (t == 0) || sk[t] == kNanKey || sk[t - 1] != sk[t];
+      if (!head) continue;
+      const int i0 = sIdx[t];
+      double tot = 0.0, cs = 0.0, mx = a.rel[off + i0];
+      int cnt = 0;
+      for (int q = t; q < n; ++q) {
+        if (q > t && (sk[q] == kNanKey || sk[q] != sk[t])) break;
+        const int iq = sIdx[q];
+        tot += a.weight[off + iq];
+        cs += a.conf[off + iq];
+        ++cnt;
+        const double rq = a.rel[off + iq];
+        if (q != t && rq > mx) mx = rq;
+        if (sk[t] == kNanKey) break;
+      }
+      const double dens = tot / (double)cnt;
+      const double key = py_round_nd(a.pred[off + i0], a.rscale, a.rthresh);
+      const int64_t g = off + sRank[i0];
+      if (a.g_key) a.g_key[g] = key;
+      if (a.g_count) a.g_count[g] = cnt;
+      if (a.g_density) a.g_density[g] = dens;
+      if (a.g_avgconf) a.g_avgconf[g] = cs / (double)cnt;
+      if (a.g_maxrel) a.g_maxrel[g] = mx;
+      if (bi < 0 || tb_better(dens, mx, key, bd, bmx, bk)) {
+        bi = i0; bd = dens; bmx = mx; bk = key;
+      }
+    }
+    cD[tid] = bd; cM[tid] = bmx; cK[tid] = bk; cI[tid] = bi;
+    __syncthreads();
+    for (int s = kTbThreads / 2; s > 0; s >>= 1) {
+      if (tid < s && cI[tid + s] >= 0 &&
+          (cI[tid] < 0 || tb_better(cD[tid + s], cM[tid + s], cK[tid + s], cD[tid], cM[tid], cK[tid]))) {
+        cD[tid] = cD[tid + s]; cM[tid] = cM[tid + s]; cK[tid] = cK[tid + s]; cI[tid] = cI[tid + s];
+      }
+      __syncthreads();
+    }
+    const double wd = cD[0], wm = cM[0], wk = cK[0];
+    const int wi = cI[0];
+    // label: does another group tie the winner on (density, max_rel)?
+    for (int t = tid; t < n; t += kTbThreads) {
+      const bool head = (t == 0) || sk[t] == kNanKey || sk[t - 1] != sk[t];
+      if (!head || sIdx[t] == wi) continue;
+      double tot = 0.0, mx = a.rel[off + sIdx[t]];
+      int cnt = 0;
+      for (int q = t; q < n; ++q) {
+        if (q > t && (sk[q] == kNanKey || sk[q] != sk[t])) break;
+        const int iq = sIdx[q];
+        tot += a.weight[off + iq];
+        ++cnt;
+        const double rq = a.rel[off + iq];
+        if (q != t && rq > mx) mx = rq;
+        if (sk[t] == kNanKey) break;
+      }
+      if (tot / (double)cnt == wd && mx == wm) sFlag = 1;
+    }
+    // confidence variance (tiebreak.py:104-106): sequential, one lane
+    if (tid == 0) {
+      double csum = 0.0;
+      for (int i = 0; i < n; ++i) csum += a.conf[off + i];
+      const double mean = csum / (double)n;
+      double vs = 0.0;
+      for (int i = 0; i < n; ++i) {
+        const double d = a.conf[off + i] - mean;
+        vs += d * d;
+      }
+      sVar = vs / (double)n;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      a.winner[m] = wk;
+      a.label[m] = (ng == 1) ? BCE_TB_UNANIMOUS
+                             : (sFlag ? BCE_TB_PREDICTION_VALUE_SMALLEST : BCE_TB_WEIGHT_DENSITY);
+      a.n_groups[m] = ng;
+      a.variance[m] = sVar;
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace bce
+
+using namespace bce;
+
+static double round_scale(int nd) {
+  double s = 1.0;
+  for (int i = 0; i < nd; ++i) s *= 10.0;  // exact for nd <= 22
+  return s;
+}
+// 2^E with E = floor(52 - nd*log2(10)) + 1: the smallest power of two whose ulp exceeds 10^-nd
+static double round_thresh(int nd) {
+  const double y = nd * 3.321928094887362;
+  const int E = (int)floor(52.0 - y) + 1;
+  return ldexp(1.0, E);
+}
+
+extern "C" int bce_tiebreak_csr(const int64_t* offsets, int64_t n_markets, const int32_t* market_list,
+                                int64_t n_list, const double* pred, const double* conf,
+                                const double* weight, const double* rel, int32_t max_len,
+                                int32_t ndigits, double* winner, int32_t* label, int32_t* n_groups,
+                                double* variance, double* g_key, int32_t* g_count, double* g_density,
+                                double* g_avgconf, double* g_maxrel, void* stream) {
+  BCE_REQUIRE(n_markets >= 0, "tiebreak: n_markets < 0");
+  const int64_t nl = market_list ? n_list : n_markets;
+  if (nl == 0) return BCE_OK;
+  BCE_REQUIRE(offsets && pred && conf && weight && rel && winner && label && n_groups && variance,
+              "tiebreak: NULL argument");
+  BCE_REQUIRE(max_len > 0 && max_len <= 64,
+              "tiebreak: max_len must be in 1..64 (longer markets: bce_tiebreak_csr_long)");
+  BCE_REQUIRE(ndigits >= 0 && ndigits <= 15, "tiebreak: ndigits must be in [0, 15]");
+  TbArgs a{offsets, n_markets, pred, conf, weight, rel, winner, label, n_groups, variance,
+           g_key, g_count, g_density, g_avgconf, g_maxrel, round_scale(ndigits), round_thresh(ndigits)};
+  int64_t blocks = (nl + 3) / 4;
+  const int64_t cap = (int64_t)cu_count() * 16;
+  if (blocks > cap) blocks = cap;
+  hipLaunchKernelGGL(tiebreak_wave_kernel, dim3((int)blocks), dim3(256), 0, as_stream(stream), a,
+                     market_list, nl);
+  return check_launch("tiebreak_wave_kernel");
+}
+
+extern "C" int bce_tiebreak_csr_long(const int64_t* offsets, int64_t n_markets, const int32_t* list,
+                                     int64_t n_list, int32_t ndigits, const double* pred,
+                                     const double* conf, const double* weight, const double* rel,
+                                     double* winner, int32_t* label, int32_t* n_groups,
+                                     double* variance, double* g_key, int32_t* g_count,
+                                     double* g_density, double* g_avgconf, double* g_maxrel,
+                                     void* stream) {
+  BCE_REQUIRE(n_list >= 0 && (n_list == 0 || list), "tiebreak_long: bad list");
+  if (n_list == 0) return BCE_OK;
+  BCE_REQUIRE(offsets && pred && conf && weight && rel && winner && label && n_groups && variance,
+              "tiebreak_long: NULL argument");
+  BCE_REQUIRE(ndigits >= 0 && ndigits <= 15, "tiebreak: ndigits must be in [0, 15]");
+  TbArgs a{offsets, n_markets, pred, conf, weight, rel, winner, label, n_groups, variance,
+           g_key, g_count, g_density, g_avgconf, g_maxrel, round_scale(ndigits), round_thresh(ndigits)};
+  int64_t blocks = n_list;
+  const int64_t cap = (int64_t)cu_count() * 2;
+  if (blocks > cap) blocks = cap;
+  hipLaunchKernelGGL(tiebreak_block_kernel, dim3((int)blocks), dim3(kTbThreads), 0,
+                     as_stream(stream), a, list, n_list);
+  return check_launch("tiebreak_block_kernel");
+}

@@ -1,0 +1,202 @@
+/*
+ * bce.h -- C ABI of the MI355X-native batched consensus engine (libbce_hip.so).
+ *
+ * This is the drop-in boundary for the reference's hot path
+ * (consensus-nexus/bayesian-consensus-engine, src/bayesian_engine/).  The reference is
+ * pure Python and exposes no plugin registry, so the boundary is
+ * this C ABI, bound from Python with ctypes (see INTEGRATION.md for the binding a
+ * maintainer of the reference would add).  Every entry point names the reference
+ * function it replaces.
+ *
+ * Conventions
+ *  - All arrays are DEVICE pointers (hipMalloc / torch tensors on cuda:N) unless the
+ *    name ends in _host.  Work is enqueued on `stream` (a hipStream_t; NULL = the
+ *    legacy default stream).  Nothing synchronises unless stated.
+ *  - Every entry point returns an int status: BCE_OK (0) or a negative BCE_E*; the
+ *    library keeps no global mutable state besides the last-error string
+ *    (bce_last_error(), thread-local).  The caller owns every buffer; the library never
+ *    frees caller memory.
+ *  - Markets are CSR: offsets[M+1] int64 (offsets[0] may be non-zero: a shard view),
+ *    sid[N] int32 = interned source rank ids whose integer order equals Python's
+ *    sorted() order of the sourceId strings (code-point order), prob[N] fp64.
+ *  - The source table is dense over rank ids: rel[S], conf[S] fp64 with the cold-start
+ *    defaults (config.py:17-18) baked in for absent keys, present[S] u8 = "sourceId is
+ *    a key of source_reliability" (core.py:167-170).
+ *  - Per-unique-source outputs are written at the market's CSR offsets: slot
+ *    offsets[m]+j for j < n_unique[m] (slots beyond are left untouched).  usid carries
+ *    the cold-start bit in bit 31 (value = rank | cold << 31).
+ *  - Floating point follows CPython: no fused multiply-add anywhere on the parity path,
+ *    sums in the reference's order in BCE_MODE_EXACT (bit-exact vs the reference).
+ */
+#ifndef BCE_H
+#define BCE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BCE_ABI_VERSION 1
+
+enum bce_status {
+    BCE_OK = 0,
+    BCE_EINVAL = -1,      /* bad argument (null pointer, size, sid out of range) */
+    BCE_EHIP = -2,        /* a HIP runtime call failed (message in bce_last_error) */
+    BCE_EUNSUPPORTED = -3 /* shape outside what this build handles */
+};
+
+enum bce_mode {
+    BCE_MODE_EXACT = 0, /* reference summation order: bit-exact outputs */
+    BCE_MODE_FAST = 1   /* tree reductions for long markets (<= 1e-9 abs vs reference) */
+};
+
+/* Tie-break labels (tiebreak.py:123-133, 89-96). */
+enum bce_tb_label {
+    BCE_TB_UNANIMOUS = 0,
+    BCE_TB_WEIGHT_DENSITY = 1,
+    BCE_TB_PREDICTION_VALUE_SMALLEST = 2,
+    BCE_TB_SINGLE_AGENT = 3
+};
+
+#define BCE_NO_TIMESTAMP INT64_MIN /* falsy / unparseable updated_at (decay.py:125-131) */
+
+/* ---- library ------------------------------------------------------------------ */
+int bce_abi_version(void);
+const char* bce_last_error(void);
+/* Number of visible devices (0 on a machine without a GPU; never fails). */
+int bce_device_count(void);
+
+/* ---- consensus: core.compute_consensus (core.py:63-179) + validation -------------
+ *
+ * Replaces: core.compute_consensus(signals, source_reliability) for every market of
+ * the batch, and the numeric part of core.validate_input_payload (core.py:59-60):
+ * err_idx[m] = first signal index whose probability is < 0 or > 1 (NaN passes), -1 if
+ * none.  Also the batch loop MarketStore.compute_all_consensus (market.py:200-221).
+ *
+ * Outputs per market: consensus (0.0 where null), confidence, total_weight,
+ * n_unique, err_idx (may be NULL to skip).  null <=> total_weight == 0 (core.py:131)
+ * or the market is empty (core.py:88-96).  Per unique source (sorted by rank):
+ * usid (rank | cold<<31), weight (= reliability, core.py:119), nweight
+ * (core.py:151).  Any of usid/weight/nweight may be NULL ("compact" mode).
+ *
+ * market_list (nullable): process only markets market_list[0..n_list) (ascending
+ * market indices recommended).  NULL = all markets 0..n_markets.  max_len is an
+ * upper bound on the market lengths processed (0 = unknown: the library computes it,
+ * which synchronises the stream).  n_sources bounds sid.
+ */
+int bce_consensus_csr(const int64_t* offsets, int64_t n_markets, const int32_t* sid,
+                      const double* prob, int64_t n_signals, const double* rel,
+                      const double* conf, const uint8_t* present, int32_t n_sources,
+                      const int32_t* market_list, int64_t n_list, int32_t max_len, int32_t mode,
+                      double* consensus, double* confidence, double* total_weight,
+                      int32_t* n_unique, int32_t* err_idx, int32_t* usid, double* weight,
+                      double* nweight, void* stream);
+
+/* Validation only (core.validate_input_payload's numeric check, core.py:59-60):
+ * err_idx[m] = first signal index with probability < 0 or > 1 (NaN passes), -1 if none.
+ * The structural/type checks (core.py:34-58) are done where the Python objects live. */
+int bce_validate_csr(const int64_t* offsets, int64_t n_markets, const double* prob,
+                     int32_t* err_idx, void* stream);
+
+/* Host-planned variant for ragged batches: the caller bins markets by length once
+ * (bce_plan_bins on HOST offsets) and passes the device copy of the ordered market
+ * list plus the bin boundaries.  bin_start has BCE_NBINS+1 entries (host array). */
+#define BCE_NBINS 6 /* n<=8, <=16, <=32, <=64, <=4096 (LDS), >4096 (global scratch) */
+int bce_plan_bins(const int64_t* offsets_host, int64_t n_markets, int32_t* order_host,
+                  int64_t* bin_start_host, int32_t* max_len_host);
+/* Bytes of device scratch bce_consensus_planned needs for the >4096 bin. */
+int64_t bce_consensus_scratch_bytes(const int64_t* offsets_host, const int32_t* order_host,
+                                    const int64_t* bin_start_host);
+int bce_consensus_planned(const int64_t* offsets, int64_t n_markets, const int32_t* sid,
+                          const double* prob, int64_t n_signals, const double* rel,
+                          const double* conf, const uint8_t* present, int32_t n_sources,
+                          const int32_t* order, const int64_t* bin_start_host, int32_t mode,
+                          double* consensus, double* confidence, double* total_weight,
+                          int32_t* n_unique, int32_t* err_idx, int32_t* usid, double* weight,
+                          double* nweight, void* scratch, int64_t scratch_bytes, void* stream);
+
+/* ---- decay: get_reliability(apply_decay=True) over a table ----------------------
+ * Replaces: decay.apply_reliability_decay (decay.py:61-100) composed with
+ * decay.days_since_update (decay.py:103-145) as used by
+ * SQLiteReliabilityStore.get_reliability (reliability.py:110-131).
+ * view[s] = present[s] ? decay(rel[s], days(now_us - t_us[s])) : default_rel.
+ * present may be NULL (all present).  t_us[s] == BCE_NO_TIMESTAMP means no decay. */
+int bce_decay_view(int64_t n, const double* rel, const int64_t* t_us, const uint8_t* present,
+                   int64_t now_us, double half_life_days, double min_rel, double default_rel,
+                   double* view, void* stream);
+
+/* ---- decay on elapsed days: decay.compute_decay_factor (decay.py:31-58) and
+ * decay.apply_reliability_decay (decay.py:61-100), elementwise.  factor (nullable) gets
+ * 2^(-days/h) (1.0 where days <= 0); out (nullable) gets the decayed reliability. */
+int bce_decay_apply(int64_t n, const double* rel, const double* elapsed_days,
+                    double half_life_days, double min_rel, double* out, double* factor,
+                    void* stream);
+
+/* ---- outcome update: compute_update / update_reliability (reliability.py:142-233) --
+ * One outcome per source per call: flags[s] bit0 = participates, bit1 = correct.
+ * Participants: rel = clamp(rel +- MAX_UPDATE_STEP) (reliability.py:163-169),
+ * conf = min(1, conf + (1-conf)*0.1) (:172-173), t_us = now_us (:175), present = 1.
+ * Absent rows start from (default_rel, default_conf) (reliability.py:133-140). */
+int bce_outcome_update(int64_t n, double* rel, double* conf, int64_t* t_us, uint8_t* present,
+                       const uint8_t* flags, int64_t now_us, double default_rel,
+                       double default_conf, void* stream);
+
+/* ---- replay step (config 4): decayed view at now_us, then the outcome update --------
+ * flags2 is 2-bit packed: source s uses bits 2*(s%4)..+1 of byte s/4 (bit0 participates,
+ * bit1 correct).  Equivalent to bce_decay_view followed by bce_outcome_update. */
+int bce_replay_step(int64_t n, double* rel, double* conf, int64_t* t_us, uint8_t* present,
+                    const uint8_t* flags2, int64_t now_us, double half_life_days,
+                    double min_rel, double default_rel, double default_conf, double* view,
+                    void* stream);
+
+/* ---- tie-break: DeterministicTieBreaker.resolve (tiebreak.py:73-152) per market -----
+ * Per signal: pred (AgentSignal.prediction), conf, weight, rel (reliability_score).
+ * Per market: winner (rounded group key, or the raw prediction for a single agent),
+ * label (enum bce_tb_label; -1 for an empty market = the reference's ValueError),
+ * n_groups, variance (unrounded population variance of conf, tiebreak.py:104-106).
+ * Per group, first-seen order, at CSR offsets: key, count, weight density, avg conf,
+ * max reliability (tiebreak.py:58-71).  Group pointers may be NULL.  ndigits is the
+ * DeterministicTieBreaker precision (0..15).
+ * bce_tiebreak_csr: markets market_list[0..n_list) (NULL = all), every length <= max_len
+ * <= 64 (one wave per market).  bce_tiebreak_csr_long: 64 < n <= 4096 (one workgroup per
+ * market, LDS-sorted). */
+int bce_tiebreak_csr(const int64_t* offsets, int64_t n_markets, const int32_t* market_list,
+                     int64_t n_list, const double* pred, const double* conf, const double* weight,
+                     const double* rel, int32_t max_len, int32_t ndigits, double* winner,
+                     int32_t* label, int32_t* n_groups, double* variance, double* g_key,
+                     int32_t* g_count, double* g_density, double* g_avgconf, double* g_maxrel,
+                     void* stream);
+int bce_tiebreak_csr_long(const int64_t* offsets, int64_t n_markets, const int32_t* list,
+                          int64_t n_list, int32_t ndigits, const double* pred, const double* conf,
+                          const double* weight, const double* rel, double* winner, int32_t* label,
+                          int32_t* n_groups, double* variance, double* g_key, int32_t* g_count,
+                          double* g_density, double* g_avgconf, double* g_maxrel, void* stream);
+
+/* ---- agreement statistics: CrossMarketAggregator.summarize_sources counts -----------
+ * (market.py:279-304).  outcome[m]: -1 skip (unresolved), 0 false, 1 true.
+ * correct[sid] / total[sid] are ACCUMULATED (zero them first); int32 atomics, exact. */
+int bce_agreement_stats(const int64_t* offsets, int64_t n_markets, const int32_t* sid,
+                        const double* prob, const int8_t* outcome, int32_t* correct,
+                        int32_t* total, void* stream);
+
+/* ---- re-estimation (config 5): consensus <-> reliability over a dense matrix --------
+ * P is agent-major [A][ld] fp64 (column m of market m; ld >= M).  One pass:
+ *   consensus[m] = sum_a P[a][m]*w[a] / sum_a w[a]  (agent order, core.py:130-144),
+ *   null[m] = (sum_a w[a] == 0);
+ * then agreement[a] += #{m not null : (P[a][m] >= 0.5) == (consensus[m] >= 0.5)}
+ * (market.py:298-304) and resolved += #{m not null}.  w_new[a] = agree/resolved
+ * (0.5 if resolved == 0, market.py:310) is bce_reestimate_weights. */
+int bce_reestimate_consensus(const double* P, int64_t A, int64_t M, int64_t ld, const double* w,
+                             double* consensus, uint8_t* null_out, void* stream);
+int bce_reestimate_agreement(const double* P, int64_t A, int64_t M, int64_t ld,
+                             const double* consensus, const uint8_t* null_in,
+                             int64_t* agreement, int64_t* resolved, void* stream);
+int bce_reestimate_weights(int64_t A, const int64_t* agreement, const int64_t* resolved,
+                           double* w, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BCE_H */

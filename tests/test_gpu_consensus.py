@@ -1,0 +1,121 @@
+"""GPU parity: batched consensus kernels vs the oracle and the reference's golden vectors.
+
+Bit-exact in BCE_MODE_EXACT (Python == on every float); BCE_MODE_FAST
+(tree sums for long markets) within the north-star tolerance 1e-9 absolute.
+"""
+import numpy as np
+import pytest
+import torch
+
+from golden_util import case_to_csr, load_json, load_npz
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(a, dt=None):
+    return torch.from_numpy(np.ascontiguousarray(a if dt is None else a.astype(dt))).cuda()
+
+
+def _run(g, mode="exact", max_len=None, plan=True):
+    from bayesian_engine import batch
+    table = batch.SourceTable(_dev(g["rel"]), _dev(g["conf"]), _dev(g["present"]),
+                              [str(i) for i in range(len(g["rel"]))])
+    off = _dev(g["offsets"])
+    r = batch.consensus(off, _dev(g["sid"], np.int32), _dev(g["prob"]), table, mode=mode,
+                        max_len=max_len, plan=None)
+    torch.cuda.synchronize()
+    return {k: (getattr(r, k).cpu().numpy() if getattr(r, k) is not None else None)
+            for k in ("consensus", "confidence", "total_weight", "n_unique", "err_idx", "usid", "weight",
+                      "nweight")}
+
+
+def _compare(out, exp, offsets, exact=True, tol=1e-9):
+    M = len(offsets) - 1
+    assert np.array_equal(out["n_unique"], exp["n_unique"])
+    assert np.array_equal(out["err_idx"], exp["err_idx"])
+    for k in ("consensus", "confidence", "total_weight"):
+        if exact:
+            assert np.array_equal(out[k], exp[k], equal_nan=True), k
+        else:
+            np.testing.assert_allclose(out[k], exp[k], rtol=0, atol=tol)
+    for m in range(M):
+        a, u = int(offsets[m]), int(exp["n_unique"][m])
+        sl = slice(a, a + u)
+        assert np.array_equal(out["usid"][sl], exp["usid"][sl]), m
+        assert np.array_equal(out["weight"][sl], exp["weight"][sl]), m
+        if exact:
+            assert np.array_equal(out["nweight"][sl], exp["nweight"][sl], equal_nan=True), m
+        else:
+            np.testing.assert_allclose(out["nweight"][sl], exp["nweight"][sl], rtol=0, atol=tol)
+
+
+@pytest.mark.parametrize("name", ["c2_slice.npz", "c3_slice.npz"])
+def test_slices_vs_oracle_and_reference(name):
+    g = load_npz(name)
+    exp = orc.consensus_csr(g["offsets"], g["sid"], g["prob"], g["rel"], g["conf"], g["present"])
+    out = _run(g)
+    _compare(out, exp, g["offsets"])
+    # and straight against the reference's own outputs captured in the fixture
+    assert np.array_equal(out["consensus"], g["consensus"], equal_nan=True)
+    assert np.array_equal(out["err_idx"], g["err_idx"])
+
+
+def test_c2_direct_launch_max_len():
+    g = load_npz("c2_slice.npz")
+    exp = orc.consensus_csr(g["offsets"], g["sid"], g["prob"], g["rel"], g["conf"], g["present"])
+    _compare(_run(g, max_len=32), exp, g["offsets"])
+
+
+def test_c3_fast_mode_tolerance():
+    g = load_npz("c3_slice.npz")
+    exp = orc.consensus_csr(g["offsets"], g["sid"], g["prob"], g["rel"], g["conf"], g["present"])
+    _compare(_run(g, mode="fast"), exp, g["offsets"], exact=False)
+
+
+@pytest.mark.parametrize("L,S,M", [(1, 5, 3000), (7, 3, 500), (8, 1000, 4000), (13, 20, 2000), (16, 10000, 3000),
+                                   (31, 40, 1000), (32, 10000, 5000), (33, 100, 700), (64, 64, 1000),
+                                   (64, 100000, 800), (65, 30, 100), (500, 200, 40), (4096, 5000, 6),
+                                   (5000, 3000, 3), (9000, 20000, 2)])
+def test_random_uniform_lengths(L, S, M):
+    rng = np.random.default_rng(L * 1000 + S)
+    sid = rng.integers(0, S, M * L).astype(np.int32)
+    prob = rng.random(M * L)
+    prob[rng.random(M * L) < 0.01] = 1.25
+    off = np.arange(0, M * L + 1, L, dtype=np.int64)
+    rel = rng.uniform(0, 1, S)
+    conf = rng.random(S)
+    present = (rng.random(S) < 0.7).astype(np.uint8)
+    rel[present == 0] = 0.5
+    conf[present == 0] = 0.25
+    g = dict(offsets=off, sid=sid, prob=prob, rel=rel, conf=conf, present=present)
+    exp = orc.consensus_csr(off, sid, prob, rel, conf, present)
+    _compare(_run(g), exp, off)
+
+
+def test_ragged_with_empty_and_huge_markets():
+    rng = np.random.default_rng(7)
+    lens = np.concatenate([[0, 0, 1, 64, 65, 4096, 4097, 0, 12000], rng.integers(0, 300, 400)])
+    rng.shuffle(lens)
+    off = np.zeros(len(lens) + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    S = 3000
+    n = int(off[-1])
+    sid = (rng.zipf(1.3, n) % S).astype(np.int32)
+    prob = rng.random(n)
+    rel = rng.uniform(0, 1, S)
+    conf = rng.random(S)
+    present = (rng.random(S) < 0.8).astype(np.uint8)
+    g = dict(offsets=off, sid=sid, prob=prob, rel=rel, conf=conf, present=present)
+    exp = orc.consensus_csr(off, sid, prob, rel, conf, present)
+    _compare(_run(g), exp, off)
+
+
+@pytest.mark.parametrize("case", load_json("consensus_cases.json"), ids=lambda c: c["name"])
+def test_single_market_cases(case):
+    if not case["signals"]:
+        pytest.skip("empty market handled on host (core.py:88-96)")
+    names, offsets, sid, prob, rel, conf, present = case_to_csr(case["signals"], case["source_reliability"])
+    g = dict(offsets=offsets, sid=sid, prob=prob, rel=rel, conf=conf, present=present)
+    exp = orc.consensus_csr(offsets, sid, prob, rel, conf, present)
+    _compare(_run(g), exp, offsets)
