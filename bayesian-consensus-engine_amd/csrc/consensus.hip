@@ -28,6 +28,17 @@
 
 #pragma clang fp contract(off)
 
+// Experiment-only switches (tools/ablate.py builds variants; the product build uses 0).
+#ifndef BCE_ABLATE
+#define BCE_ABLATE 0
+#endif
+#ifndef BCE_SEG32_TM
+#define BCE_SEG32_TM 16
+#endif
+#ifndef BCE_SEG_GRID_PER_CU
+#define BCE_SEG_GRID_PER_CU 24
+#endif
+
 namespace bce {
 
 struct ConsArgs {
@@ -125,7 +136,7 @@ __global__ __launch_bounds__(64) void consensus_seg_kernel(ConsArgs a) {
     for (int r = 0; r < R; ++r) {
       const int mk = r * SPR + seg;
       unsigned key = valid[r] ? (((unsigned)sidv[r] << LOGG) | (unsigned)t) : kSent32;
-      key = bitonic_sort_seg<G>(key, t);
+      if constexpr (!(BCE_ABLATE & 1)) key = bitonic_sort_seg<G>(key, t);
       const bool kv = key != kSent32;
       const int ssid = (int)(key >> LOGG);
       const int sidx = (int)(key & (G - 1));
@@ -144,7 +155,7 @@ __global__ __launch_bounds__(64) void consensus_seg_kernel(ConsArgs a) {
       const int myrun = first ? run : 1;
       double s = 0.0 + ps;  // builtin sum() starts from int 0 (core.py:116)
       double avg = s;
-      if (ballot(myrun > 1)) {  // duplicates present: sum the run in input order
+      if (!(BCE_ABLATE & 16) && ballot(myrun > 1)) {  // duplicates: sum the run in input order
         for (int k = 1; k < G; ++k) {
           const int src = (lane + k < 64) ? lane + k : 63;
           const double pk = pull_f64(ps, src);
@@ -154,9 +165,13 @@ __global__ __launch_bounds__(64) void consensus_seg_kernel(ConsArgs a) {
         avg = (myrun > 1) ? s / (double)myrun : s;
       }
       if (first) {
-        const double w = a.rel[ssid];      // core.py:111,119
-        const double c = a.conf[ssid];     // core.py:112
-        const bool cold = a.present[ssid] == 0;  // core.py:167-170
+        double w = 0.5, c = 0.25;
+        bool cold = false;
+        if constexpr (!(BCE_ABLATE & 2)) {
+          w = a.rel[ssid];                  // core.py:111,119
+          c = a.conf[ssid];                 // core.py:112
+          cold = a.present[ssid] == 0;      // core.py:167-170
+        }
         const int o = mk * RS + j;
         sW[o] = w;
         sA[o] = avg * w;                    // core.py:136
@@ -178,10 +193,16 @@ __global__ __launch_bounds__(64) void consensus_seg_kernel(ConsArgs a) {
       const int u = sNU[lane];
       double total = 0.0, ws = 0.0, cs = 0.0;
       const int base = lane * RS;
-      for (int jj = 0; jj < u; ++jj) {
-        total += sW[base + jj];
-        ws += sA[base + jj];
-        cs += sB[base + jj];
+      if constexpr (!(BCE_ABLATE & 4)) {
+        for (int jj = 0; jj < u; ++jj) {
+          total += sW[base + jj];
+          ws += sA[base + jj];
+          cs += sB[base + jj];
+        }
+      } else {
+        total = sW[base] + (double)u;
+        ws = sA[base];
+        cs = sB[base];
       }
       sTot[lane] = total;
       const int32_t m = sM[lane];
@@ -197,7 +218,7 @@ __global__ __launch_bounds__(64) void consensus_seg_kernel(ConsArgs a) {
     __syncthreads();
 
     // ---- per-unique outputs (coalesced at CSR offsets) --------------------------------
-    if (a.usid || a.weight || a.nweight) {
+    if ((a.usid || a.weight || a.nweight) && !(BCE_ABLATE & 8)) {
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const int mk = r * SPR + seg;
@@ -434,7 +455,7 @@ template <int G, int TM>
 int launch_seg(const ConsArgs& a, hipStream_t st) {
   const int64_t tiles = (a.n_list + TM - 1) / TM;
   if (tiles == 0) return BCE_OK;
-  const int64_t cap = (int64_t)cu_count() * 24;  // grid-stride beyond ~24 waves per CU
+  const int64_t cap = (int64_t)cu_count() * BCE_SEG_GRID_PER_CU;  // grid-stride beyond this
   const int grid = (int)(tiles < cap ? tiles : cap);
   hipLaunchKernelGGL((consensus_seg_kernel<G, TM>), dim3(grid), dim3(64), 0, st, a);
   return check_launch("consensus_seg_kernel");
@@ -443,7 +464,7 @@ int launch_seg(const ConsArgs& a, hipStream_t st) {
 int launch_seg_for_len(int max_len, const ConsArgs& a, hipStream_t st) {
   if (max_len <= 8) return launch_seg<8, 64>(a, st);
   if (max_len <= 16) return launch_seg<16, 32>(a, st);
-  if (max_len <= 32) return launch_seg<32, 16>(a, st);
+  if (max_len <= 32) return launch_seg<32, BCE_SEG32_TM>(a, st);
   return launch_seg<64, 8>(a, st);
 }
 
