@@ -46,12 +46,13 @@ _SIGS = {
     "bce_abi_version": (C.c_int, []),
     "bce_last_error": (C.c_char_p, []),
     "bce_device_count": (C.c_int, []),
-    "bce_consensus_csr": (C.c_int, [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _i32, _vp, _i64, _i32,
+    "bce_consensus_csr": (C.c_int, [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _i32, _vp, _i64, _i32,
                                     _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "bce_table_pack": (C.c_int, [_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "bce_validate_csr": (C.c_int, [_vp, _i64, _vp, _vp, _vp]),
     "bce_plan_bins": (C.c_int, [_vp, _i64, _vp, _vp, _vp]),
     "bce_consensus_scratch_bytes": (C.c_int64, [_vp, _vp, _vp]),
-    "bce_consensus_planned": (C.c_int, [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _i32, _vp, _vp, _i32,
+    "bce_consensus_planned": (C.c_int, [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _i32, _vp, _vp, _i32,
                                         _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
     "bce_decay_view": (C.c_int, [_i64, _vp, _vp, _vp, _i64, _f64, _f64, _f64, _vp, _vp]),
     "bce_decay_apply": (C.c_int, [_i64, _vp, _vp, _f64, _f64, _vp, _vp, _vp]),

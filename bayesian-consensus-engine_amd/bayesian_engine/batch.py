@@ -34,11 +34,15 @@ def intern(ids: Iterable[str]) -> Dict[str, int]:
 
 @dataclass
 class SourceTable:
-    """Dense per-source table resident in HBM (bulk-loaded from a dict or SQLite)."""
+    """Dense per-source table resident in HBM, in the consensus kernel's layout.
 
-    rel: torch.Tensor
-    conf: torch.Tensor
-    present: torch.Tensor
+    relconf [S, 2] fp64: interleaved {reliability, confidence} -> one 16-B gather per
+    unique source; bits [ceil(S/32)] int32: present bitmask ("sourceId is a key of the
+    reliability dict", core.py:167-170).  Cold-start defaults are baked into relconf.
+    """
+
+    relconf: torch.Tensor
+    bits: torch.Tensor
     names: List[str]
     t_us: Optional[torch.Tensor] = None
 
@@ -46,29 +50,82 @@ class SourceTable:
     def n(self) -> int:
         return len(self.names)
 
+    @property
+    def rel(self) -> torch.Tensor:
+        return self.relconf[:, 0]
+
+    @property
+    def conf(self) -> torch.Tensor:
+        return self.relconf[:, 1]
+
     @classmethod
-    def from_dict(cls, names: Sequence[str], source_reliability: Optional[dict],
-                  device=None) -> "SourceTable":
+    def from_arrays(cls, rel: torch.Tensor, conf: torch.Tensor, present: Optional[torch.Tensor],
+                    names: Optional[Sequence[str]] = None, t_us: Optional[torch.Tensor] = None) -> "SourceTable":
+        """Pack device arrays with bce_table_pack (one launch)."""
+        L = N.require_gpu()
+        S = rel.numel()
+        dev = rel.device
+        relconf = torch.empty((max(S, 1), 2), dtype=torch.float64, device=dev)
+        bits = torch.zeros(max((S + 31) // 32, 1), dtype=torch.int32, device=dev)
+        rel = rel.to(torch.float64).contiguous()
+        conf = conf.to(torch.float64).contiguous()
+        pres = present.to(torch.uint8).contiguous() if present is not None else None
+        N.check(L.bce_table_pack(S, N.ptr(rel), N.ptr(conf), N.ptr(pres), N.ptr(relconf), N.ptr(bits),
+                                 N.stream(dev)), "bce_table_pack")
+        return cls(relconf, bits, list(names) if names is not None else [""] * S, t_us)
+
+    @classmethod
+    def from_dict(cls, names: Sequence[str], source_reliability: Optional[dict], device=None) -> "SourceTable":
         """core.py:110-112 semantics: a key present (even with a partial dict) is not cold."""
         S = len(names)
         rel = np.full(max(S, 1), DEFAULT_RELIABILITY, np.float64)
         conf = np.full(max(S, 1), DEFAULT_CONFIDENCE, np.float64)
-        present = np.zeros(max(S, 2), np.uint8)
+        present = np.zeros(max(S, 1), np.uint8)
         sr = source_reliability or {}
         for i, n in enumerate(names):
-            d = sr.get(n)
             if n in sr:
                 present[i] = 1
-                if d is None:
-                    d = {}
+                d = sr.get(n) or {}
                 r = d.get("reliability", DEFAULT_RELIABILITY)
                 c = d.get("confidence", DEFAULT_CONFIDENCE)
-                0.0 + r  # noqa: B018  -- same TypeError as core.py:120 for non-numbers
+                acc = 0.0
+                acc += r  # same TypeError as core.py:120 for non-numbers
                 rel[i] = float(r)
                 conf[i] = float(c)
         dev = device or N.device()
-        return cls(torch.from_numpy(rel).to(dev), torch.from_numpy(conf).to(dev),
-                   torch.from_numpy(present).to(dev), list(names))
+        T = lambda a: torch.from_numpy(a).to(dev)  # noqa: E731
+        return cls.from_arrays(T(rel[:S]), T(conf[:S]), T(present[:S]), names)
+
+
+@dataclass
+class ReliabilityTable:
+    """Store-side table (SoA) for the streaming decay / outcome-update kernels.
+
+    rel, conf fp64[S], t_us int64[S] (updated_at as microseconds, NO_TIMESTAMP if
+    falsy/unparseable), present u8[S] (a row exists).  Absent rows hold the baked
+    cold-start values (0.5, 0.25, NO_TIMESTAMP), reliability.py:133-140.
+    """
+
+    rel: torch.Tensor
+    conf: torch.Tensor
+    t_us: torch.Tensor
+    present: torch.Tensor
+    names: List[str]
+
+    @property
+    def n(self) -> int:
+        return len(self.names)
+
+    def view(self, now_us: int) -> torch.Tensor:
+        """get_reliability(apply_decay=True).reliability of every source."""
+        return decay_view(self.rel, self.t_us, now_us, present=self.present)
+
+    def consensus_table(self, now_us: Optional[int] = None, all_present: bool = True) -> "SourceTable":
+        """Packed consensus table; reliability decayed at ``now_us`` when given.  Callers that
+        fetch every source through get_reliability (market.py:209-219, cli.py:37-44) put
+        every sourceId in the dict, hence ``all_present``."""
+        rel = self.view(now_us) if now_us is not None else self.rel
+        return SourceTable.from_arrays(rel, self.conf, None if all_present else self.present, self.names)
 
 
 # ---------------------------------------------------------------------------------------
@@ -139,8 +196,8 @@ def consensus(offsets: torch.Tensor, sid: torch.Tensor, prob: torch.Tensor, tabl
     Nsig = sid.numel()
     dev = offsets.device
     res = out or _alloc(M, Nsig, dev, unique_outputs, validate)
-    common = (N.ptr(offsets), M, N.ptr(sid), N.ptr(prob), Nsig, N.ptr(table.rel), N.ptr(table.conf),
-              N.ptr(table.present), table.n)
+    common = (N.ptr(offsets), M, N.ptr(sid), N.ptr(prob), Nsig, N.ptr(table.relconf), N.ptr(table.bits),
+              table.n)
     outs = (N.ptr(res.consensus), N.ptr(res.confidence), N.ptr(res.total_weight), N.ptr(res.n_unique),
             N.ptr(res.err_idx), N.ptr(res.usid), N.ptr(res.weight), N.ptr(res.nweight))
     md = _MODES[mode]

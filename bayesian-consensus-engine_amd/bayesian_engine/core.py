@@ -153,7 +153,7 @@ def compute_consensus(
     N.require_gpu()
     dev = N.device()
     T = lambda a: torch.from_numpy(a).to(dev, non_blocking=False)  # noqa: E731
-    table = batch.SourceTable(T(rel), T(conf), T(present), source_ids)
+    table = batch.SourceTable.from_arrays(T(rel), T(conf), T(present[:S]), source_ids)
     off = torch.tensor([0, n], dtype=torch.int64, device=dev)
     res = batch.consensus(off, T(sid), T(prob), table, max_len=n if n <= 64 else None, validate=False)
     cons = float(res.consensus[0].item())

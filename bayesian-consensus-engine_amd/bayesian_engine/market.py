@@ -32,7 +32,8 @@ from . import batch
 from .config import DEFAULT_CONFIDENCE, DEFAULT_RELIABILITY, SCHEMA_VERSION
 from .core import compute_consensus
 from .reliability import SQLiteReliabilityStore
-from .timeutil import NO_TIMESTAMP, iso_to_us, now_us
+from . import decay as _decay
+from .timeutil import NO_TIMESTAMP, dt_to_us, iso_to_us
 
 __all__ = ["MarketId", "MarketStatus", "Market", "MarketStore", "SourcePerformance", "CrossMarketAggregator"]
 
@@ -206,12 +207,12 @@ def _batched_consensus(markets: List[Market], store: Optional[SQLiteReliabilityS
                     rel[k], conf[k], t_us[k] = row[0], row[1], iso_to_us(row[2])
                 k += 1
         T = lambda a: torch.from_numpy(a).to(dev)  # noqa: E731
-        view = batch.decay_view(T(rel), T(t_us), now_us())  # get_reliability(apply_decay=True)
-        d_rel = view.contiguous() if view.numel() == rel.size else torch.cat([view, T(rel[view.numel():])])
-        table = batch.SourceTable(d_rel, T(conf), T(present), key_names)
+        rt = batch.ReliabilityTable(T(rel[:S]), T(conf[:S]), T(t_us[:S]), T(present[:S]), key_names)
+        # get_reliability(apply_decay=True) for every pair, "now" read like decay.py:136-137
+        table = rt.consensus_table(dt_to_us(_decay.datetime.now(timezone.utc)))
     else:
         T = lambda a: torch.from_numpy(a).to(dev)  # noqa: E731
-        table = batch.SourceTable(T(rel), T(conf), T(present), key_names)
+        table = batch.SourceTable.from_arrays(T(rel[:S]), T(conf[:S]), T(present[:S]), key_names)
     off = np.array(offsets, np.int64)
     T = lambda a: torch.from_numpy(a).to(dev)  # noqa: E731
     res = batch.consensus(T(off), T(np.array(sid_list, np.int32)), T(np.array(prob_list, np.float64)), table,

@@ -166,7 +166,7 @@ class SQLiteReliabilityStore:
 
     # ------------------------------------------------------------------ bulk paths (f1)
     def load_table(self, market_id: str, names: Optional[Sequence[str]] = None,
-                   device=None) -> batch.SourceTable:
+                   device=None) -> batch.ReliabilityTable:
         """Dense HBM table for one scope.  ``names`` (sorted) fixes the rank space (e.g. all
         sourceIds of a batch); absent rows get the baked cold-start values."""
         rows = self._conn.execute(
@@ -176,10 +176,10 @@ class SQLiteReliabilityStore:
             names = [r[0] for r in rows]
         idx = {n: i for i, n in enumerate(names)}
         S = len(names)
-        rel = np.full(max(S, 2), DEFAULT_RELIABILITY)
-        conf = np.full(max(S, 2), DEFAULT_CONFIDENCE)
-        t_us = np.full(max(S, 2), NO_TIMESTAMP, np.int64)
-        present = np.zeros(max(S, 2), np.uint8)
+        rel = np.full(S, DEFAULT_RELIABILITY)
+        conf = np.full(S, DEFAULT_CONFIDENCE)
+        t_us = np.full(S, NO_TIMESTAMP, np.int64)
+        present = np.zeros(S, np.uint8)
         for sid, r, c, ts in rows:
             i = idx.get(sid)
             if i is None:
@@ -187,12 +187,11 @@ class SQLiteReliabilityStore:
             rel[i], conf[i], t_us[i], present[i] = r, c, iso_to_us(ts), 1
         dev = device or N.device()
         T = lambda a: torch.from_numpy(a).to(dev)  # noqa: E731
-        return batch.SourceTable(T(rel), T(conf), T(present), list(names), T(t_us))
+        return batch.ReliabilityTable(T(rel), T(conf), T(t_us), T(present), list(names))
 
-    def decayed_view(self, table: batch.SourceTable, now: Optional[datetime] = None) -> torch.Tensor:
+    def decayed_view(self, table: batch.ReliabilityTable, now: Optional[datetime] = None) -> torch.Tensor:
         """get_reliability(apply_decay=True).reliability for every source of ``table``."""
-        now_us = dt_to_us(now or datetime.now(timezone.utc))
-        return batch.decay_view(table.rel, table.t_us, now_us, present=table.present)
+        return table.view(dt_to_us(now or datetime.now(timezone.utc)))
 
     def apply_outcomes(self, market_id: str, outcomes: Mapping[str, bool], dry_run: bool = False,
                        now: Optional[datetime] = None) -> Dict[str, ReliabilityRecord]:
@@ -200,7 +199,7 @@ class SQLiteReliabilityStore:
         names = sorted(outcomes)
         table = self.load_table(market_id, names)
         S = len(names)
-        flags = np.zeros(max(S, 2), np.uint8)
+        flags = np.zeros(S, np.uint8)
         for i, n in enumerate(names):
             flags[i] = 1 | (2 if outcomes[n] else 0)
         now_us = dt_to_us(now or datetime.now(timezone.utc))

@@ -1,0 +1,60 @@
+"""Multi-GPU partitioning: one process per GPU, torch.distributed over
+RCCL/xGMI (backend "nccl"; "gloo" for CPU tests).
+
+* Markets (configs 2/3) shard with ZERO communication: contiguous market ranges split at
+  equal signal counts (prefix sum of the CSR offsets), source table replicated (e1).
+* Sources (config 4) shard by an owner hash; the only exchange is the per-source outcome
+  flags produced by market shards, combined with one all-reduce (e2).  Flags are combined
+  as a bitwise OR of (participates, correct) bits packed in uint8 -- expressed as a SUM
+  all-reduce over disjoint contributions (each (source, step) outcome is produced by
+  exactly one market shard), which RCCL implements natively.
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def shard_markets(offsets_host: np.ndarray, world: int, rank: int) -> Tuple[int, int]:
+    """Contiguous market range [m0, m1) of ``rank`` so every rank gets ~N/world signals."""
+    off = np.asarray(offsets_host, np.int64)
+    M = len(off) - 1
+    if world <= 1:
+        return 0, M
+    total = int(off[-1] - off[0])
+    targets = off[0] + (total * np.arange(world + 1, dtype=np.float64) / world)
+    cuts = np.searchsorted(off, targets, side="left")
+    cuts[0], cuts[-1] = 0, M
+    cuts = np.maximum.accumulate(np.clip(cuts, 0, M))
+    return int(cuts[rank]), int(cuts[rank + 1])
+
+
+def owner_of(source_ids: np.ndarray, world: int) -> np.ndarray:
+    """Owner rank of each source rank id (multiplicative hash, stable across ranks)."""
+    h = (np.asarray(source_ids, np.uint64) * np.uint64(0x9E3779B97F4A7C15)) >> np.uint64(40)
+    return (h % np.uint64(max(world, 1))).astype(np.int32)
+
+
+def combine_flags(local_flags: torch.Tensor) -> torch.Tensor:
+    """All-reduce per-source outcome flags produced by disjoint market shards (e2).
+
+    ``local_flags`` uint8[S]: bit0 participates, bit1 correct, zero where this rank's
+    markets produced no outcome.  Contributions are disjoint, so SUM == OR.
+    """
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return local_flags
+    t = local_flags.to(torch.int32) if local_flags.device.type == "cpu" else local_flags
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t.to(torch.uint8)
+
+
+def allreduce_counts(correct: torch.Tensor, total: torch.Tensor) -> None:
+    """Sum per-source agreement counts over market shards (summarize_sources, market.py:293-304)."""
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        both = torch.stack([correct, total])
+        dist.all_reduce(both, op=dist.ReduceOp.SUM)
+        correct.copy_(both[0])
+        total.copy_(both[1])

@@ -45,9 +45,10 @@ struct ConsArgs {
   const int64_t* offsets;
   const int32_t* sid;
   const double* prob;
-  const double* rel;
-  const double* conf;
-  const uint8_t* present;
+  const double2* relconf;    // [S] interleaved {reliability, confidence}: one 16-B gather
+  const uint32_t* pbits;     // [ceil(S/32)] present bitmask (bit s%32 of word s/32)
+  int32_t n_sources;
+  int64_t n_signals;
   const int32_t* list;  // nullable
   int64_t n_list;       // number of markets to process
   double* consensus;
@@ -62,6 +63,12 @@ struct ConsArgs {
   void* scratch;      // long kernel, global variant
   int64_t scratch_stride;  // elements (keys) per workgroup slice
 };
+
+constexpr int kBitsLds = 512;  // present bitmask words staged in LDS (S <= 16384)
+
+__device__ __forceinline__ bool is_present(const uint32_t* bits, int s) {
+  return ((bits[s >> 5] >> (s & 31)) & 1u) != 0;
+}
 
 // ------------------------------------------------------------------------------------
 // short markets: wave-per-tile, lane-per-signal then lane-per-market
@@ -85,6 +92,7 @@ __global__ __launch_bounds__(64) void consensus_seg_kernel(ConsArgs a) {
   __shared__ int32_t sNU[TM];
   __shared__ int32_t sErr[TM];
   __shared__ double sTot[TM];
+  __shared__ uint32_t sBits[kBitsLds];
 
   const int lane = lane_id();
   const int seg = lane / G;
@@ -93,6 +101,18 @@ __global__ __launch_bounds__(64) void consensus_seg_kernel(ConsArgs a) {
   const unsigned long long segmask =
       (G == 64) ? ~0ull : (((1ull << G) - 1ull) << seg_base);
   const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+
+  // present bitmask: staged once per (persistent) workgroup when it fits in LDS
+  const int nwords = (a.n_sources + 31) >> 5;
+  const bool bits_in_lds = nwords <= kBitsLds;
+  if (bits_in_lds)
+    for (int i = lane; i < nwords; i += kWave) sBits[i] = a.pbits[i];
+  // input staging for contiguous tiles, aliased onto sA/sB (dead until the cooperative
+  // phase): sids at sStageI[e - a0], probabilities at sStageP[e - a0p]
+  static_assert(TM * RS * 8 >= (TM * G + 8) * 4, "sid staging fits in sA");
+  static_assert(TM * RS * 8 >= (TM * G + 4) * 8, "prob staging fits in sB");
+  int32_t* sStageI = reinterpret_cast<int32_t*>(sA);
+  double* sStageP = sB;
 
   const int64_t n_tiles = (a.n_list + TM - 1) / TM;
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
@@ -113,21 +133,57 @@ __global__ __launch_bounds__(64) void consensus_seg_kernel(ConsArgs a) {
     }
     __syncthreads();
 
-    // ---- prefetch every round's signals (coalesced within each G-lane segment) -----
+    // ---- load every round's signals ----------------------------------------------------
     int32_t sidv[R];
     double pv[R];
     bool valid[R];
+    if (a.list == nullptr) {
+      // contiguous tile: stream [base, end) with 16-B loads into LDS, then each lane picks
+      // its (market, t) element -- sids in 4-element chunks, probabilities in 2-element.
+      const int64_t base = sOff[0];
+      int64_t end = base;
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int mk = r * SPR + seg;
-      const int32_t n = sN[mk];
-      valid[r] = t < n;
-      sidv[r] = 0;
-      pv[r] = 0.0;
-      if (valid[r]) {
+      for (int q = 0; q < TM; ++q) end = (sN[q] > 0) ? sOff[q] + sN[q] : end;
+      const int64_t a0 = base & ~3ll, a0p = base & ~1ll;
+      for (int64_t e = a0 + 4 * lane; e < end; e += 4 * kWave) {
+        if (e + 4 <= a.n_signals) {
+          const int4 v = *reinterpret_cast<const int4*>(a.sid + e);
+          *reinterpret_cast<int4*>(sStageI + (e - a0)) = v;
+        } else {
+          for (int q = 0; q < 4 && e + q < a.n_signals; ++q) sStageI[e - a0 + q] = a.sid[e + q];
+        }
+      }
+      for (int64_t e = a0p + 2 * lane; e < end; e += 2 * kWave) {
+        if (e + 2 <= a.n_signals) {
+          const double2 v = *reinterpret_cast<const double2*>(a.prob + e);
+          *reinterpret_cast<double2*>(sStageP + (e - a0p)) = v;
+        } else {
+          sStageP[e - a0p] = a.prob[e];
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int mk = r * SPR + seg;
+        valid[r] = t < sN[mk];
         const int64_t p = sOff[mk] + t;
-        sidv[r] = a.sid[p];
-        pv[r] = a.prob[p];
+        sidv[r] = valid[r] ? sStageI[p - a0] : 0;
+        pv[r] = valid[r] ? sStageP[p - a0p] : 0.0;
+      }
+      __syncthreads();  // staging (aliased on sA/sB) is dead from here on
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int mk = r * SPR + seg;
+        const int32_t n = sN[mk];
+        valid[r] = t < n;
+        sidv[r] = 0;
+        pv[r] = 0.0;
+        if (valid[r]) {
+          const int64_t p = sOff[mk] + t;
+          sidv[r] = a.sid[p];
+          pv[r] = a.prob[p];
+        }
       }
     }
 
@@ -168,9 +224,11 @@ __global__ __launch_bounds__(64) void consensus_seg_kernel(ConsArgs a) {
         double w = 0.5, c = 0.25;
         bool cold = false;
         if constexpr (!(BCE_ABLATE & 2)) {
-          w = a.rel[ssid];                  // core.py:111,119
-          c = a.conf[ssid];                 // core.py:112
-          cold = a.present[ssid] == 0;      // core.py:167-170
+          const double2 rc = a.relconf[ssid];  // core.py:111-112,119 (one 16-B gather)
+          w = rc.x;
+          c = rc.y;
+          const uint32_t word = bits_in_lds ? sBits[ssid >> 5] : a.pbits[ssid >> 5];
+          cold = ((word >> (ssid & 31)) & 1u) == 0;  // core.py:167-170
         }
         const int o = mk * RS + j;
         sW[o] = w;
@@ -387,14 +445,15 @@ __global__ __launch_bounds__(kLongThreads) void consensus_long_kernel(ConsArgs a
     // ---- pass 3: gather + per-unique products (keys/probs are dead now) -----------------
     for (int j = tid; j < u; j += NT) {
       const int s = Sj[j];
-      const double w = a.rel[s];   // core.py:111,119
-      const double c = a.conf[s];  // core.py:112
+      const double2 rc = a.relconf[s];
+      const double w = rc.x;  // core.py:111,119
+      const double c = rc.y;  // core.py:112
       const double avg = Cv[j];
       Wv[j] = w;
       Pr[j] = avg * w;  // core.py:136
       Cv[j] = c * w;    // core.py:142
       const int64_t p = off + j;
-      if (a.usid) a.usid[p] = s | (a.present[s] ? 0 : (int32_t)0x80000000);
+      if (a.usid) a.usid[p] = s | (is_present(a.pbits, s) ? 0 : (int32_t)0x80000000);
       if (a.weight) a.weight[p] = w;
     }
     __syncthreads();
@@ -515,14 +574,15 @@ __global__ void max_len_kernel(const int64_t* offsets, int64_t n, const int32_t*
 }
 
 int check_common(const int64_t* offsets, int64_t n_markets, const int32_t* sid, const double* prob,
-                 const double* rel, const double* conf, const uint8_t* present, int32_t n_sources,
+                 const double* relconf, const uint32_t* present_bits, int32_t n_sources,
                  double* consensus, double* confidence, double* total_weight, int32_t* n_unique) {
   BCE_REQUIRE(n_markets >= 0, "consensus: n_markets < 0");
   BCE_REQUIRE(n_markets == 0 || offsets, "consensus: offsets is NULL");
   BCE_REQUIRE(n_markets == 0 || (consensus && confidence && total_weight && n_unique),
               "consensus: per-market outputs must be non-NULL");
-  BCE_REQUIRE(n_sources >= 0 && (n_sources == 0 || (rel && conf && present)),
+  BCE_REQUIRE(n_sources >= 0 && (n_sources == 0 || (relconf && present_bits)),
               "consensus: source table is NULL");
+  BCE_REQUIRE((uintptr_t)relconf % 16 == 0, "consensus: relconf must be 16-byte aligned");
   (void)sid;
   (void)prob;
   return BCE_OK;
@@ -534,20 +594,22 @@ int check_common(const int64_t* offsets, int64_t n_markets, const int32_t* sid, 
 using namespace bce;
 
 extern "C" int bce_consensus_csr(const int64_t* offsets, int64_t n_markets, const int32_t* sid,
-                                 const double* prob, int64_t n_signals, const double* rel,
-                                 const double* conf, const uint8_t* present, int32_t n_sources,
+                                 const double* prob, int64_t n_signals, const double* relconf,
+                                 const uint32_t* present_bits, int32_t n_sources,
                                  const int32_t* market_list, int64_t n_list, int32_t max_len,
                                  int32_t mode, double* consensus, double* confidence,
                                  double* total_weight, int32_t* n_unique, int32_t* err_idx,
                                  int32_t* usid, double* weight, double* nweight, void* stream) {
-  int rc = check_common(offsets, n_markets, sid, prob, rel, conf, present, n_sources, consensus,
+  int rc = check_common(offsets, n_markets, sid, prob, relconf, present_bits, n_sources, consensus,
                         confidence, total_weight, n_unique);
   if (rc) return rc;
   BCE_REQUIRE(mode == BCE_MODE_EXACT || mode == BCE_MODE_FAST, "consensus: bad mode %d", mode);
   BCE_REQUIRE(n_signals == 0 || (sid && prob), "consensus: sid/prob NULL");
   hipStream_t st = as_stream(stream);
   ConsArgs a{};
-  a.offsets = offsets; a.sid = sid; a.prob = prob; a.rel = rel; a.conf = conf; a.present = present;
+  a.offsets = offsets; a.sid = sid; a.prob = prob;
+  a.relconf = reinterpret_cast<const double2*>(relconf); a.pbits = present_bits;
+  a.n_sources = n_sources; a.n_signals = n_signals;
   a.list = market_list; a.n_list = market_list ? n_list : n_markets;
   a.consensus = consensus; a.confidence = confidence; a.total_weight = total_weight;
   a.n_unique = n_unique; a.err_idx = err_idx; a.usid = usid; a.weight = weight; a.nweight = nweight;
@@ -627,14 +689,14 @@ extern "C" int64_t bce_consensus_scratch_bytes(const int64_t* offsets_host, cons
 }
 
 extern "C" int bce_consensus_planned(const int64_t* offsets, int64_t n_markets, const int32_t* sid,
-                                     const double* prob, int64_t n_signals, const double* rel,
-                                     const double* conf, const uint8_t* present, int32_t n_sources,
+                                     const double* prob, int64_t n_signals, const double* relconf,
+                                     const uint32_t* present_bits, int32_t n_sources,
                                      const int32_t* order, const int64_t* bin_start_host,
                                      int32_t mode, double* consensus, double* confidence,
                                      double* total_weight, int32_t* n_unique, int32_t* err_idx,
                                      int32_t* usid, double* weight, double* nweight, void* scratch,
                                      int64_t scratch_bytes, void* stream) {
-  int rc = check_common(offsets, n_markets, sid, prob, rel, conf, present, n_sources, consensus,
+  int rc = check_common(offsets, n_markets, sid, prob, relconf, present_bits, n_sources, consensus,
                         confidence, total_weight, n_unique);
   if (rc) return rc;
   BCE_REQUIRE(bin_start_host && (order || n_markets == 0), "planned: missing plan");
@@ -642,8 +704,9 @@ extern "C" int bce_consensus_planned(const int64_t* offsets, int64_t n_markets, 
   BCE_REQUIRE(n_signals == 0 || (sid && prob), "planned: sid/prob NULL");
   hipStream_t st = as_stream(stream);
   ConsArgs base{};
-  base.offsets = offsets; base.sid = sid; base.prob = prob; base.rel = rel; base.conf = conf;
-  base.present = present; base.consensus = consensus; base.confidence = confidence;
+  base.offsets = offsets; base.sid = sid; base.prob = prob;
+  base.relconf = reinterpret_cast<const double2*>(relconf); base.pbits = present_bits;
+  base.n_sources = n_sources; base.n_signals = n_signals; base.consensus = consensus; base.confidence = confidence;
   base.total_weight = total_weight; base.n_unique = n_unique; base.err_idx = err_idx;
   base.usid = usid; base.weight = weight; base.nweight = nweight; base.mode = mode;
   const bool seg_ok = n_sources <= (1 << 25);
@@ -711,4 +774,37 @@ extern "C" int bce_validate_csr(const int64_t* offsets, int64_t n_markets, const
   hipLaunchKernelGGL(validate_kernel, dim3((int)blocks), dim3(256), 0, as_stream(stream), offsets,
                      n_markets, prob, err_idx);
   return check_launch("validate_kernel");
+}
+
+// ======================================================================================
+// source-table packing: separate (rel, conf, present) -> the consensus layout
+// ======================================================================================
+namespace bce {
+__global__ __launch_bounds__(256) void table_pack_kernel(int64_t n, const double* rel, const double* conf,
+                                                         const uint8_t* present, double2* relconf,
+                                                         uint32_t* bits) {
+  const int lane = lane_id();
+  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < ((n + 63) & ~63ll);
+       s += (int64_t)gridDim.x * blockDim.x) {
+    const bool in = s < n;
+    if (in) relconf[s] = make_double2(rel[s], conf[s]);
+    const unsigned long long b = ballot(in && (present == nullptr || present[s] != 0));
+    if (lane == 0 && s < n) bits[s >> 5] = (uint32_t)b;
+    if (lane == 32 && s < n) bits[s >> 5] = (uint32_t)(b >> 32);
+  }
+}
+}  // namespace bce
+
+extern "C" int bce_table_pack(int64_t n, const double* rel, const double* conf, const uint8_t* present,
+                              double* relconf, uint32_t* present_bits, void* stream) {
+  BCE_REQUIRE(n >= 0, "table_pack: n < 0");
+  if (n == 0) return BCE_OK;
+  BCE_REQUIRE(rel && conf && relconf && present_bits, "table_pack: NULL argument");
+  BCE_REQUIRE((uintptr_t)relconf % 16 == 0, "table_pack: relconf must be 16-byte aligned");
+  int64_t blocks = (n + 255) / 256;
+  const int64_t cap = (int64_t)cu_count() * 16;
+  if (blocks > cap) blocks = cap;
+  hipLaunchKernelGGL(table_pack_kernel, dim3((int)blocks), dim3(256), 0, as_stream(stream), n, rel, conf,
+                     present, reinterpret_cast<double2*>(relconf), present_bits);
+  return check_launch("table_pack_kernel");
 }

@@ -133,8 +133,8 @@ def bench_c2(args, world, rank):
     d_off = torch.from_numpy(offsets).to(dev)
     d_sid = torch.from_numpy(sid).to(dev)
     d_prob = torch.from_numpy(prob).to(dev)
-    table = batch.SourceTable(torch.from_numpy(rel).to(dev), torch.from_numpy(conf).to(dev),
-                              torch.from_numpy(present).to(dev), [""] * S)
+    table = batch.SourceTable.from_arrays(torch.from_numpy(rel).to(dev), torch.from_numpy(conf).to(dev),
+                                          torch.from_numpy(present).to(dev))
     res = batch._alloc(M, M * L, dev, True, True)
     stream = torch.cuda.current_stream(dev)
 
@@ -165,7 +165,7 @@ def bench_c2(args, world, rank):
     # algorithmic bytes per launch
     sum_u = int(res.n_unique.sum().item())
     n_sig = M * L
-    bytes_per_launch = 12 * n_sig + (8 * (M + 1)) + 32 * M + 20 * sum_u + 17 * S
+    bytes_per_launch = 12 * n_sig + (8 * (M + 1)) + 32 * M + 20 * sum_u + 16 * S + (S + 7) // 8
     achieved_gbs = bytes_per_launch / avg_kernel_s / 1e9
 
     total_signals = sum_over_ranks(float(n_sig * args.steps), world)

@@ -19,9 +19,12 @@
  *  - Markets are CSR: offsets[M+1] int64 (offsets[0] may be non-zero: a shard view),
  *    sid[N] int32 = interned source rank ids whose integer order equals Python's
  *    sorted() order of the sourceId strings (code-point order), prob[N] fp64.
- *  - The source table is dense over rank ids: rel[S], conf[S] fp64 with the cold-start
- *    defaults (config.py:17-18) baked in for absent keys, present[S] u8 = "sourceId is
- *    a key of source_reliability" (core.py:167-170).
+ *  - The consensus source table is dense over rank ids and laid out for the gather:
+ *    relconf[2*S] fp64 = interleaved {reliability, confidence} pairs (16-byte aligned, one
+ *    16-B load per unique source) with the cold-start defaults (config.py:17-18) baked in
+ *    for absent keys, and present_bits[ceil(S/32)] u32 = bit s%32 of word s/32 set iff
+ *    the sourceId is a key of source_reliability (core.py:167-170).  bce_table_pack
+ *    builds it from separate rel/conf/present arrays.
  *  - Per-unique-source outputs are written at the market's CSR offsets: slot
  *    offsets[m]+j for j < n_unique[m] (slots beyond are left untouched).  usid carries
  *    the cold-start bit in bit 31 (value = rank | cold << 31).
@@ -87,12 +90,17 @@ int bce_device_count(void);
  * which synchronises the stream).  n_sources bounds sid.
  */
 int bce_consensus_csr(const int64_t* offsets, int64_t n_markets, const int32_t* sid,
-                      const double* prob, int64_t n_signals, const double* rel,
-                      const double* conf, const uint8_t* present, int32_t n_sources,
+                      const double* prob, int64_t n_signals, const double* relconf,
+                      const uint32_t* present_bits, int32_t n_sources,
                       const int32_t* market_list, int64_t n_list, int32_t max_len, int32_t mode,
                       double* consensus, double* confidence, double* total_weight,
                       int32_t* n_unique, int32_t* err_idx, int32_t* usid, double* weight,
                       double* nweight, void* stream);
+
+/* Pack separate rel[S], conf[S], present[S] (u8, nullable = all present) into the
+ * consensus table layout: relconf[2*S] interleaved, present_bits[ceil(S/32)]. */
+int bce_table_pack(int64_t n, const double* rel, const double* conf, const uint8_t* present,
+                   double* relconf, uint32_t* present_bits, void* stream);
 
 /* Validation only (core.validate_input_payload's numeric check, core.py:59-60):
  * err_idx[m] = first signal index with probability < 0 or > 1 (NaN passes), -1 if none.
@@ -110,8 +118,8 @@ int bce_plan_bins(const int64_t* offsets_host, int64_t n_markets, int32_t* order
 int64_t bce_consensus_scratch_bytes(const int64_t* offsets_host, const int32_t* order_host,
                                     const int64_t* bin_start_host);
 int bce_consensus_planned(const int64_t* offsets, int64_t n_markets, const int32_t* sid,
-                          const double* prob, int64_t n_signals, const double* rel,
-                          const double* conf, const uint8_t* present, int32_t n_sources,
+                          const double* prob, int64_t n_signals, const double* relconf,
+                          const uint32_t* present_bits, int32_t n_sources,
                           const int32_t* order, const int64_t* bin_start_host, int32_t mode,
                           double* consensus, double* confidence, double* total_weight,
                           int32_t* n_unique, int32_t* err_idx, int32_t* usid, double* weight,

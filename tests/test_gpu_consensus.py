@@ -19,8 +19,7 @@ def _dev(a, dt=None):
 
 def _run(g, mode="exact", max_len=None, plan=True):
     from bayesian_engine import batch
-    table = batch.SourceTable(_dev(g["rel"]), _dev(g["conf"]), _dev(g["present"]),
-                              [str(i) for i in range(len(g["rel"]))])
+    table = batch.SourceTable.from_arrays(_dev(g["rel"]), _dev(g["conf"]), _dev(g["present"]))
     off = _dev(g["offsets"])
     r = batch.consensus(off, _dev(g["sid"], np.int32), _dev(g["prob"]), table, mode=mode,
                         max_len=max_len, plan=None)

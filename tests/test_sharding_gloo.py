@@ -1,0 +1,87 @@
+"""Multi-process (world_size 2, gloo, CPU) checks of the N>1 path: market shards need no
+communication and reassemble to the 1-process result; per-source flags / agreement counts
+are combined with one all-reduce."""
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "bayesian-consensus-engine_amd"))
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from bayesian_engine.sharding import allreduce_counts, combine_flags, shard_markets
+    from oracle import oracle as orc
+
+    rng = np.random.default_rng(5)
+    lens = rng.integers(0, 300, 400)
+    off = np.zeros(len(lens) + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    S = 500
+    sid = rng.integers(0, S, off[-1]).astype(np.int32)
+    prob = rng.random(off[-1])
+    rel, conf = rng.random(S), rng.random(S)
+    present = (rng.random(S) < 0.8).astype(np.uint8)
+    m0, m1 = shard_markets(off, world, rank)
+    sub = off[m0:m1 + 1]
+    local = orc.consensus_csr(sub - sub[0], sid[sub[0]:sub[-1]], prob[sub[0]:sub[-1]], rel, conf, present)
+    parts = [None] * world
+    dist.all_gather_object(parts, (m0, m1, local["consensus"].tolist(), local["n_unique"].tolist()))
+    # outcome flags from disjoint market shards -> one all-reduce
+    outcome = (rng.random(len(lens)) < 0.5).astype(np.int8)
+    outcome[rng.random(len(lens)) < 0.2] = -1
+    c_loc = np.zeros(S, np.int32)
+    t_loc = np.zeros(S, np.int32)
+    mask = np.full(len(lens), -1, np.int8)
+    mask[m0:m1] = outcome[m0:m1]
+    c, t = orc.agreement_stats(off, sid, prob, mask, S)
+    ct, tt = torch.from_numpy(c.astype(np.int64)), torch.from_numpy(t.astype(np.int64))
+    allreduce_counts(ct, tt)
+    flags = torch.zeros(S, dtype=torch.uint8)
+    mine = np.arange(S) % world == rank
+    flags[torch.from_numpy(mine)] = 1
+    comb = combine_flags(flags)
+    if rank == 0:
+        full = orc.consensus_csr(off, sid, prob, rel, conf, present)
+        call, tall = orc.agreement_stats(off, sid, prob, outcome, S)
+        q.put(dict(parts=parts, full_cons=full["consensus"].tolist(), full_nu=full["n_unique"].tolist(),
+                   counts_ok=bool(np.array_equal(ct.numpy(), call) and np.array_equal(tt.numpy(), tall)),
+                   flags_ok=bool(torch.all(comb == 1).item())))
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_sharding():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    cons, nu = [], []
+    parts = sorted(res["parts"])
+    assert parts[0][0] == 0 and parts[-1][1] == len(res["full_cons"])
+    for m0, m1, c, n in parts:
+        cons += c
+        nu += n
+    assert cons == res["full_cons"] and nu == res["full_nu"]
+    assert res["counts_ok"] and res["flags_ok"]

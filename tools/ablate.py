@@ -30,6 +30,8 @@ VARIANTS = {
     "tm32": ["-DBCE_SEG32_TM=32"],
     "grid8": ["-DBCE_SEG_GRID_PER_CU=8"],
     "grid64": ["-DBCE_SEG_GRID_PER_CU=64"],
+    "grid4": ["-DBCE_SEG_GRID_PER_CU=4"],
+    "grid12": ["-DBCE_SEG_GRID_PER_CU=12"],
 }
 SRCS = ["capi.hip", "consensus.hip"]
 
@@ -63,6 +65,8 @@ def run(names, rounds, steps):
     i32 = dict(dtype=torch.int32, device=dev)
     outs = [torch.empty(M, **f64), torch.empty(M, **f64), torch.empty(M, **f64), torch.empty(M, **i32),
             torch.empty(M, **i32), torch.empty(M * L, **i32), torch.empty(M * L, **f64), torch.empty(M * L, **f64)]
+    from bayesian_engine import batch
+    table = batch.SourceTable.from_arrays(d[3], d[4], d[5])
     libs = {}
     for n in names:
         lib = C.CDLL(os.path.join(OUT, f"lib_{n}.so"))
@@ -72,8 +76,8 @@ def run(names, rounds, steps):
     p = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
 
     def call(lib):
-        rc = lib.bce_consensus_csr(p(d[0]), C.c_int64(M), p(d[1]), p(d[2]), C.c_int64(M * L), p(d[3]), p(d[4]),
-                                   p(d[5]), C.c_int32(S), C.c_void_p(0), C.c_int64(0), C.c_int32(L), C.c_int32(0),
+        rc = lib.bce_consensus_csr(p(d[0]), C.c_int64(M), p(d[1]), p(d[2]), C.c_int64(M * L), p(table.relconf),
+                                   p(table.bits), C.c_int32(S), C.c_void_p(0), C.c_int64(0), C.c_int32(L), C.c_int32(0),
                                    *[p(o) for o in outs], C.c_void_p(st.cuda_stream))
         assert rc == 0, rc
 
