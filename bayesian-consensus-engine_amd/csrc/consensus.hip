@@ -36,7 +36,13 @@
 #define BCE_SEG32_TM 16
 #endif
 #ifndef BCE_SEG_GRID_PER_CU
-#define BCE_SEG_GRID_PER_CU 24
+#define BCE_SEG_GRID_PER_CU 0  // 0 = exactly the resident occupancy (persistent grid)
+#endif
+#ifndef BCE_SEG_WPE
+#define BCE_SEG_WPE 1  // __launch_bounds__ min waves per SIMD for the segment kernel
+#endif
+#ifndef BCE_STAGE
+#define BCE_STAGE 1  // LDS-staged 16-B input loads for contiguous tiles
 #endif
 
 namespace bce {
@@ -74,18 +80,22 @@ __device__ __forceinline__ bool is_present(const uint32_t* bits, int s) {
 // short markets: wave-per-tile, lane-per-signal then lane-per-market
 // ------------------------------------------------------------------------------------
 template <int G, int TM>
-__global__ __launch_bounds__(64) void consensus_seg_kernel(ConsArgs a) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BCE_SEG_WPE, 8)))
+void consensus_seg_kernel(ConsArgs a) {
   static_assert(G == 8 || G == 16 || G == 32 || G == 64, "segment width");
   constexpr int SPR = kWave / G;   // segments (markets) per round
   constexpr int R = TM / SPR;      // rounds per tile
   static_assert(R * SPR == TM, "tile must be a whole number of rounds");
   constexpr int LOGG = (G == 8) ? 3 : (G == 16) ? 4 : (G == 32) ? 5 : 6;
   constexpr int RS = G + 1;        // padded LDS row stride (conflict-free transposed reads)
+  constexpr int NI = (TM * G + 3 + 4 * kWave - 1) / (4 * kWave);  // 16-B sid chunks per lane
+  constexpr int NP = (TM * G + 1 + 2 * kWave - 1) / (2 * kWave);  // 16-B prob chunks per lane
 
-  __shared__ double sW[TM * RS];
-  __shared__ double sA[TM * RS];
-  __shared__ double sB[TM * RS];
-  __shared__ int32_t sU[TM * RS];
+  // One LDS array, carved by hand (cdna guide §5 trap 4a): W | A | B rows (fp64,
+  // TM x RS each), then usid rows, per-market scalars and the present bitmask.
+  constexpr int ROWS = TM * RS;
+  __shared__ double sWAB[3 * ROWS];
+  __shared__ int32_t sU[ROWS];
   __shared__ int64_t sOff[TM];
   __shared__ int32_t sN[TM];
   __shared__ int32_t sM[TM];
@@ -93,13 +103,16 @@ __global__ __launch_bounds__(64) void consensus_seg_kernel(ConsArgs a) {
   __shared__ int32_t sErr[TM];
   __shared__ double sTot[TM];
   __shared__ uint32_t sBits[kBitsLds];
+  double* const sW = sWAB;
+  double* const sA = sWAB + ROWS;
+  double* const sB = sWAB + 2 * ROWS;
 
   const int lane = lane_id();
   const int seg = lane / G;
   const int t = lane & (G - 1);
   const int seg_base = seg * G;
   const unsigned long long segmask =
-      (G == 64) ? ~0ull : (((1ull << G) - 1ull) << seg_base);
+      (G >= 64) ? ~0ull : (((1ull << (G & 63)) - 1ull) << seg_base);
   const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 
   // present bitmask: staged once per (persistent) workgroup when it fits in LDS
@@ -107,12 +120,13 @@ __global__ __launch_bounds__(64) void consensus_seg_kernel(ConsArgs a) {
   const bool bits_in_lds = nwords <= kBitsLds;
   if (bits_in_lds)
     for (int i = lane; i < nwords; i += kWave) sBits[i] = a.pbits[i];
-  // input staging for contiguous tiles, aliased onto sA/sB (dead until the cooperative
-  // phase): sids at sStageI[e - a0], probabilities at sStageP[e - a0p]
-  static_assert(TM * RS * 8 >= (TM * G + 8) * 4, "sid staging fits in sA");
-  static_assert(TM * RS * 8 >= (TM * G + 4) * 8, "prob staging fits in sB");
-  int32_t* sStageI = reinterpret_cast<int32_t*>(sA);
-  double* sStageP = sB;
+  // input staging for contiguous tiles, aliased onto the W|A|B rows (dead until the
+  // cooperative phase): sids at sStageI[e - a0] in W, probabilities at sStageP[e - a0p]
+  // from A on.
+  static_assert(ROWS * 8 >= NI * 4 * kWave * 4, "sid staging fits in the W rows");
+  static_assert(2 * ROWS * 8 >= NP * 2 * kWave * 8, "prob staging fits in the A|B rows");
+  int32_t* sStageI = reinterpret_cast<int32_t*>(sW);
+  double* sStageP = sA;
 
   const int64_t n_tiles = (a.n_list + TM - 1) / TM;
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
@@ -133,34 +147,49 @@ __global__ __launch_bounds__(64) void consensus_seg_kernel(ConsArgs a) {
     }
     __syncthreads();
 
-    // ---- load every round's signals ----------------------------------------------------
+    // ---- load every round's signals; all loads in flight before the first use -------
     int32_t sidv[R];
     double pv[R];
     bool valid[R];
-    if (a.list == nullptr) {
-      // contiguous tile: stream [base, end) with 16-B loads into LDS, then each lane picks
-      // its (market, t) element -- sids in 4-element chunks, probabilities in 2-element.
+    if (BCE_STAGE && a.list == nullptr) {
+      // contiguous tile: [base, end) streamed with 16-B loads into LDS, then each lane
+      // picks its (market, slot) element.
       const int64_t base = sOff[0];
       int64_t end = base;
 #pragma unroll
       for (int q = 0; q < TM; ++q) end = (sN[q] > 0) ? sOff[q] + sN[q] : end;
       const int64_t a0 = base & ~3ll, a0p = base & ~1ll;
-      for (int64_t e = a0 + 4 * lane; e < end; e += 4 * kWave) {
-        if (e + 4 <= a.n_signals) {
-          const int4 v = *reinterpret_cast<const int4*>(a.sid + e);
-          *reinterpret_cast<int4*>(sStageI + (e - a0)) = v;
-        } else {
-          for (int q = 0; q < 4 && e + q < a.n_signals; ++q) sStageI[e - a0 + q] = a.sid[e + q];
+      int4 vi[NI];
+      double2 vp[NP];
+#pragma unroll
+      for (int q = 0; q < NI; ++q) {
+        const int64_t e = a0 + 4 * (lane + kWave * q);
+        vi[q] = make_int4(0, 0, 0, 0);
+        if (e < end) {
+          if (e + 4 <= a.n_signals) {
+            vi[q] = *reinterpret_cast<const int4*>(a.sid + e);
+          } else {
+            vi[q].x = a.sid[e];
+            if (e + 1 < a.n_signals) vi[q].y = a.sid[e + 1];
+            if (e + 2 < a.n_signals) vi[q].z = a.sid[e + 2];
+          }
         }
       }
-      for (int64_t e = a0p + 2 * lane; e < end; e += 2 * kWave) {
-        if (e + 2 <= a.n_signals) {
-          const double2 v = *reinterpret_cast<const double2*>(a.prob + e);
-          *reinterpret_cast<double2*>(sStageP + (e - a0p)) = v;
-        } else {
-          sStageP[e - a0p] = a.prob[e];
+#pragma unroll
+      for (int q = 0; q < NP; ++q) {
+        const int64_t e = a0p + 2 * (lane + kWave * q);
+        vp[q] = make_double2(0.0, 0.0);
+        if (e < end) {
+          if (e + 2 <= a.n_signals) vp[q] = *reinterpret_cast<const double2*>(a.prob + e);
+          else vp[q].x = a.prob[e];
         }
       }
+#pragma unroll
+      for (int q = 0; q < NI; ++q)
+        *reinterpret_cast<int4*>(sStageI + 4 * (lane + kWave * q)) = vi[q];
+#pragma unroll
+      for (int q = 0; q < NP; ++q)
+        *reinterpret_cast<double2*>(sStageP + 2 * (lane + kWave * q)) = vp[q];
       __syncthreads();
 #pragma unroll
       for (int r = 0; r < R; ++r) {
@@ -187,6 +216,22 @@ __global__ __launch_bounds__(64) void consensus_seg_kernel(ConsArgs a) {
       }
     }
 
+    // ---- source-table gathers for every round, by ORIGINAL lane, all in flight ------
+    // (core.py:110-112): one 16-B {reliability, confidence} load per signal; the sorted
+    // lanes later pull the values of the lane that holds the same sid (ds_bpermute), so
+    // no L2 round trip sits inside the per-round dependency chain.
+    double2 rc[R];
+    uint32_t pw[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      rc[r] = make_double2(0.5, 0.25);
+      pw[r] = 0xffffffffu;
+      if (!(BCE_ABLATE & 2) && valid[r]) {
+        rc[r] = a.relconf[sidv[r]];
+        if (!bits_in_lds) pw[r] = a.pbits[sidv[r] >> 5];
+      }
+    }
+
     // ---- cooperative phase -----------------------------------------------------------
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -195,8 +240,8 @@ __global__ __launch_bounds__(64) void consensus_seg_kernel(ConsArgs a) {
       if constexpr (!(BCE_ABLATE & 1)) key = bitonic_sort_seg<G>(key, t);
       const bool kv = key != kSent32;
       const int ssid = (int)(key >> LOGG);
-      const int sidx = (int)(key & (G - 1));
-      const double ps = pull_f64(pv[r], seg_base + sidx);  // probability in sorted order
+      const int src = seg_base + (int)(key & (G - 1));  // lane holding this signal
+      const double ps = pull_f64(pv[r], src);            // probability in sorted order
       const int prev = wave_shr1(ssid, -1);
       const bool first = kv && (t == 0 || prev != ssid);
       const unsigned long long fm = ballot(first);
@@ -213,27 +258,22 @@ __global__ __launch_bounds__(64) void consensus_seg_kernel(ConsArgs a) {
       double avg = s;
       if (!(BCE_ABLATE & 16) && ballot(myrun > 1)) {  // duplicates: sum the run in input order
         for (int k = 1; k < G; ++k) {
-          const int src = (lane + k < 64) ? lane + k : 63;
-          const double pk = pull_f64(ps, src);
+          const int sl = (lane + k < 64) ? lane + k : 63;
+          const double pk = pull_f64(ps, sl);
           if (k < myrun) s += pk;
           if (!ballot(k + 1 < myrun)) break;
         }
         avg = (myrun > 1) ? s / (double)myrun : s;
       }
+      const double w = pull_f64(rc[r].x, src);  // core.py:111,119
+      const double c = pull_f64(rc[r].y, src);  // core.py:112
+      const uint32_t word = bits_in_lds ? sBits[ssid >> 5] : (uint32_t)pull_i32((int)pw[r], src);
       if (first) {
-        double w = 0.5, c = 0.25;
-        bool cold = false;
-        if constexpr (!(BCE_ABLATE & 2)) {
-          const double2 rc = a.relconf[ssid];  // core.py:111-112,119 (one 16-B gather)
-          w = rc.x;
-          c = rc.y;
-          const uint32_t word = bits_in_lds ? sBits[ssid >> 5] : a.pbits[ssid >> 5];
-          cold = ((word >> (ssid & 31)) & 1u) == 0;  // core.py:167-170
-        }
+        const bool cold = ((word >> (ssid & 31)) & 1u) == 0;  // core.py:167-170
         const int o = mk * RS + j;
         sW[o] = w;
-        sA[o] = avg * w;                    // core.py:136
-        sB[o] = c * w;                      // core.py:142
+        sA[o] = avg * w;  // core.py:136
+        sB[o] = c * w;    // core.py:142
         sU[o] = ssid | (cold ? (int32_t)0x80000000 : 0);
       }
       // validate_input_payload range check (core.py:59-60) on the ORIGINAL order
@@ -247,15 +287,20 @@ __global__ __launch_bounds__(64) void consensus_seg_kernel(ConsArgs a) {
     __syncthreads();
 
     // ---- serial phase: lane = market, exact left-to-right sums (core.py:107-144) ----
+    // Fixed trip count with predication so every LDS read can be issued ahead of the
+    // dependent adds; adding nothing for j >= u keeps the exact order.
     if (lane < TM) {
       const int u = sNU[lane];
       double total = 0.0, ws = 0.0, cs = 0.0;
       const int base = lane * RS;
       if constexpr (!(BCE_ABLATE & 4)) {
-        for (int jj = 0; jj < u; ++jj) {
-          total += sW[base + jj];
-          ws += sA[base + jj];
-          cs += sB[base + jj];
+#pragma unroll
+        for (int jj = 0; jj < G; ++jj) {
+          if (jj < u) {
+            total += sW[base + jj];
+            ws += sA[base + jj];
+            cs += sB[base + jj];
+          }
         }
       } else {
         total = sW[base] + (double)u;
@@ -514,7 +559,17 @@ template <int G, int TM>
 int launch_seg(const ConsArgs& a, hipStream_t st) {
   const int64_t tiles = (a.n_list + TM - 1) / TM;
   if (tiles == 0) return BCE_OK;
-  const int64_t cap = (int64_t)cu_count() * BCE_SEG_GRID_PER_CU;  // grid-stride beyond this
+  // persistent grid: every workgroup resident at once, tiles dealt round-robin
+  static int per_cu = 0;
+  if (!per_cu) {
+    int nb = 0;
+    if (BCE_SEG_GRID_PER_CU > 0) nb = BCE_SEG_GRID_PER_CU;
+    else if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, consensus_seg_kernel<G, TM>, 64, 0) !=
+                 hipSuccess || nb <= 0)
+      nb = 8;
+    per_cu = nb;
+  }
+  const int64_t cap = (int64_t)cu_count() * per_cu;
   const int grid = (int)(tiles < cap ? tiles : cap);
   hipLaunchKernelGGL((consensus_seg_kernel<G, TM>), dim3(grid), dim3(64), 0, st, a);
   return check_launch("consensus_seg_kernel");

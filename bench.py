@@ -49,6 +49,7 @@ def parse():
     p.add_argument("--len", type=int, default=32)
     p.add_argument("--sources", type=int, default=10_000)
     p.add_argument("--mode", default="exact", choices=["exact", "fast"])
+    p.add_argument("--agents", type=int, default=16384, help="config 5 agents")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample-markets", type=int, default=1_000_000)
     p.add_argument("--no-parity", action="store_true")

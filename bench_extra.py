@@ -1,0 +1,247 @@
+"""Secondary bench lines for BASELINE.json configs 3-5 (``python bench.py --config c3|c4|c5``).
+
+Same contract as the headline: inputs resident in HBM before timing, W untimed warmup
+steps, K timed steps bracketed by barrier + synchronize, max over ranks, one JSON line.
+
+  c3  100M signals ragged CSR (lengths log-uniform on [1, 4096], Zipf(1.1) sources over
+      1e6 ranks), markets sharded over N ranks at equal signal counts (strong scaling:
+      the 100M total is fixed).  Step = one planned consensus pass (all length bins).
+  c4  10M-source reliability table, T replay steps (decayed view + outcome update per
+      step, participation 0.1, correct 0.6).  Sources are owner-sharded; with N > 1 the
+      per-step outcome flags produced by the market shards are combined with one RCCL
+      reduce-scatter (2-bit packed, disjoint contributions).  Step = one replay step.
+  c5  dense A x M re-estimation (default 16384 x 1e6 fp64 = 131 GB), markets sharded by
+      column over N ranks; per iteration pass 1 (consensus), pass 2 (agreement), an
+      all-reduce of the per-agent counts, the weight update.  Step = one iteration.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+HBM_PEAK_GBS = 8000.0
+
+
+def _timed(step, args, world, stream, barrier, max_over):
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        step()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    barrier(world)
+    torch.cuda.synchronize()
+    per = float(np.mean([a.elapsed_time(b) for a, b in ev])) / 1e3
+    return max_over(wall, world), per
+
+
+def run_extra(args, world, rank):
+    from bench import barrier, max_over_ranks, sum_over_ranks  # noqa: E402
+
+    fn = {"c3": _c3, "c4": _c4, "c5": _c5}[args.config]
+    return fn(args, world, rank, barrier, max_over_ranks, sum_over_ranks)
+
+
+# ---------------------------------------------------------------------------------------
+def _c3(args, world, rank, barrier, max_over, sum_over):
+    from bayesian_engine import batch
+    from bayesian_engine.sharding import shard_markets
+
+    total = 100_000_000
+    S = 1_000_000
+    rng = np.random.default_rng(3)
+    lens = np.floor(np.exp(rng.uniform(0, np.log(4097), size=total // 400))).astype(np.int64)
+    cs = np.cumsum(lens)
+    M = int(np.searchsorted(cs, total) + 1)
+    lens = lens[:M]
+    lens[-1] -= int(cs[M - 1] - total)
+    offsets = np.zeros(M + 1, np.int64)
+    offsets[1:] = np.cumsum(lens)
+    m0, m1 = shard_markets(offsets, world, rank)
+    off = offsets[m0:m1 + 1] - offsets[m0]
+    n = int(off[-1])
+    r2 = np.random.default_rng(1000 + m0)
+    perm = np.random.default_rng(33).permutation(S).astype(np.int32)
+    sid = perm[np.minimum(r2.zipf(1.1, size=n), S) - 1]
+    prob = r2.random(n)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    rt = np.random.default_rng(34)
+    rel, conf = rt.uniform(0.1, 1.0, S), rt.random(S)
+    present = (rt.random(S) < 0.9).astype(np.uint8)
+    table = batch.SourceTable.from_arrays(T(np.where(present == 1, rel, 0.5)), T(np.where(present == 1, conf, 0.25)),
+                                          T(present))
+    d_off, d_sid, d_prob = T(off), T(sid), T(prob)
+    plan = batch.Plan.build(off, dev)
+    res = batch._alloc(len(off) - 1, n, dev, True, True)
+
+    def step():
+        batch.consensus(d_off, d_sid, d_prob, table, plan=plan, mode=args.mode, out=res)
+
+    wall, per = _timed(step, args, world, torch.cuda.current_stream(dev), barrier, max_over)
+    Mloc = len(off) - 1
+    sum_u = int(res.n_unique.sum().item())
+    touched = int(np.unique(sid).size)
+    bytes_step = 12 * n + 8 * (Mloc + 1) + 32 * Mloc + 20 * sum_u + 17 * touched
+    achieved = bytes_step / per / 1e9
+    sig = sum_over(float(n * args.steps), world)
+    return {
+        "metric": "signals aggregated/sec (node), 100M-signal ragged CSR (config 3)",
+        "value": sig / wall, "unit": "signals/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic (SURVEY.md d3: log-uniform lengths, Zipf 1.1)",
+        "config": {"workload": f"c3: {M} markets, {total} signals total, Zipf over {S} sources, mode={args.mode}",
+                   "markets_this_rank": Mloc, "signals_this_rank": n, "unique_per_market_mean": sum_u / max(Mloc, 1),
+                   "bins": plan.bin_start.tolist(), "parallelism": f"markets sharded over {world} rank(s), no collective"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "consensus (all bins, one step)",
+                     "bytes_per_launch": bytes_step, "avg_launch_ms": per * 1e3},
+        "cpu_baseline": None,
+    }
+
+
+# ---------------------------------------------------------------------------------------
+def _c4(args, world, rank, barrier, max_over, sum_over):
+    from bayesian_engine import batch
+
+    S_total = 10_000_000
+    S = S_total // world + (1 if rank < S_total % world else 0)   # this rank's owned sources
+    S -= S % 2
+    dev = torch.device("cuda", torch.cuda.current_device())
+    g = torch.Generator(device=dev)
+    g.manual_seed(4 + rank)
+    now0 = 1_772_323_200_000_000  # 2026-03-01T00:00:00Z in microseconds
+    day = 86_400_000_000
+    rel = torch.rand(S, generator=g, device=dev, dtype=torch.float64)
+    conf = torch.rand(S, generator=g, device=dev, dtype=torch.float64)
+    t_us = now0 - (torch.rand(S, generator=g, device=dev, dtype=torch.float64) * 90 * day).to(torch.int64)
+    present = torch.ones(S, dtype=torch.uint8, device=dev)
+    view = torch.empty(S, dtype=torch.float64, device=dev)
+    POOL = 16
+    nbytes = (S + 3) // 4
+
+    def flags_for(k_seed, who):
+        gg = torch.Generator(device=dev)
+        gg.manual_seed(k_seed)
+        part = torch.rand(S_total if world > 1 else S, generator=gg, device=dev) < 0.1
+        corr = torch.rand(part.numel(), generator=gg, device=dev) < 0.6
+        if world > 1:  # contribution of this rank's market shard: disjoint by source
+            part &= (torch.arange(part.numel(), device=dev) % world) == who
+        f = part.to(torch.uint8) | (corr.to(torch.uint8) << 1)
+        pad = (-f.numel()) % 4
+        f = torch.cat([f, torch.zeros(pad, dtype=torch.uint8, device=dev)]).view(-1, 4)
+        return (f[:, 0] | (f[:, 1] << 2) | (f[:, 2] << 4) | (f[:, 3] << 6)).contiguous()
+
+    pool = [flags_for(1000 + k, rank) for k in range(POOL)]
+    recv = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    state = {"k": 0}
+
+    def step():
+        k = state["k"]
+        fl = pool[k % POOL]
+        if world > 1:
+            # owner shard = contiguous block of the packed vector (sources permuted so each
+            # rank owns one block); disjoint 2-bit contributions -> SUM == OR
+            chunks = fl[: nbytes * world].view(world, nbytes)
+            dist.reduce_scatter_tensor(recv, chunks.contiguous().view(-1), op=dist.ReduceOp.SUM)
+            f2 = recv
+        else:
+            f2 = fl
+        batch.replay_step(rel, conf, t_us, present, f2, now0 + k * day, view)
+        state["k"] = k + 1
+
+    wall, per = _timed(step, args, world, torch.cuda.current_stream(dev), barrier, max_over)
+    p = 0.1
+    bps = 24 + 0.25 + 8 + p * (8 + 24 + 1)
+    achieved = bps * S / per / 1e9
+    total_ss = sum_over(float(S * args.steps), world)
+    return {
+        "metric": "source-steps/sec (node), 10M-source decay + outcome replay (config 4)",
+        "value": total_ss / wall, "unit": "source-steps/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (SURVEY.md d4: participation 0.1, correct 0.6, 16-step flag pool)",
+        "config": {"workload": f"c4: {S_total} sources, replay_step per step", "sources_this_rank": S,
+                   "parallelism": f"sources owner-sharded over {world} rank(s); flags reduce-scatter per step"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "replay_step_kernel",
+                     "bytes_per_launch": bps * S, "avg_launch_ms": per * 1e3},
+        "cpu_baseline": None,
+    }
+
+
+# ---------------------------------------------------------------------------------------
+def _c5(args, world, rank, barrier, max_over, sum_over):
+    from bayesian_engine import _native as N
+
+    A = getattr(args, "agents", 16384) or 16384
+    M_total = args.markets if args.markets != 1_000_000 else 1_000_000
+    Mloc = M_total // world + (1 if rank < M_total % world else 0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    truth = torch.rand(Mloc, generator=g, device=dev) < 0.5
+    P = torch.empty((A, Mloc), dtype=torch.float64, device=dev)
+    CH = 256
+    for a0 in range(0, A, CH):
+        a1 = min(A, a0 + CH)
+        u = torch.rand((3, a1 - a0, Mloc), generator=g, device=dev, dtype=torch.float64)
+        P[a0:a1] = u.median(dim=0).values  # median of 3 uniforms ~ Beta(2, 2)
+        del u
+    oracle = torch.nonzero(torch.rand(A, generator=g, device=dev) < 0.1).flatten().tolist()
+    for a in oracle:
+        u = torch.rand((6, Mloc), generator=g, device=dev, dtype=torch.float64).sort(dim=0).values
+        P[a] = torch.where(truth, u[4], u[1])  # Beta(5,2) / Beta(2,5) order statistics
+    L = N.require_gpu()
+    w = torch.full((A,), 0.5, dtype=torch.float64, device=dev)
+    cons = torch.empty(Mloc, dtype=torch.float64, device=dev)
+    nul = torch.empty(max(Mloc, 1), dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(A + 1, dtype=torch.int64, device=dev)  # agreement[A] | resolved
+    st = N.stream(dev)
+    ld = P.stride(0)
+    ev_k = []
+
+    def step():
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        N.check(L.bce_reestimate_consensus(N.ptr(P), A, Mloc, ld, N.ptr(w), N.ptr(cons), N.ptr(nul), st), "c5 p1")
+        cnt.zero_()
+        N.check(L.bce_reestimate_agreement(N.ptr(P), A, Mloc, ld, N.ptr(cons), N.ptr(nul), N.ptr(cnt[:A]),
+                                           N.ptr(cnt[A:]), st), "c5 p2")
+        e1.record()
+        ev_k.append((e0, e1))
+        if world > 1:
+            dist.all_reduce(cnt, op=dist.ReduceOp.SUM)  # per-agent counts over market shards (e4)
+        N.check(L.bce_reestimate_weights(A, N.ptr(cnt[:A]), N.ptr(cnt[A:]), N.ptr(w), st), "c5 w")
+
+    wall, per = _timed(step, args, world, torch.cuda.current_stream(dev), barrier, max_over)
+    kern = float(np.mean([a.elapsed_time(b) for a, b in ev_k[-args.steps:]])) / 1e3
+    bytes_iter = 16 * A * Mloc + 16 * A + 18 * Mloc
+    achieved = bytes_iter / kern / 1e9
+    cells = sum_over(float(A * Mloc * args.steps), world)
+    return {
+        "metric": "agent-market cells re-estimated/sec (node), dense consensus<->reliability (config 5)",
+        "value": cells / wall, "unit": "cells/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (SURVEY.md d5: Beta(2,2) via order statistics, 10% oracle agents)",
+        "config": {"workload": f"c5: {A} agents x {M_total} markets fp64, 1 iteration per step",
+                   "markets_this_rank": Mloc,
+                   "parallelism": f"markets sharded by column over {world} rank(s); per-agent counts all-reduced"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "reestimate_consensus + reestimate_agreement (one iteration)",
+                     "bytes_per_launch": bytes_iter, "avg_launch_ms": kern * 1e3,
+                     "mfma": "not used: GEMV at ~0.25 flop/B; exact agent-order sums on the VALU"},
+        "cpu_baseline": None,
+    }

@@ -1,0 +1,414 @@
+"""GPU parity of the drop-in modules against the reference's golden vectors.
+
+Every fixture under tests/golden/ was produced by the reference itself
+(tests/golden/gen_golden.py).  Consensus, validation, outcome updates, tie-break and
+agreement statistics are compared with Python ``==`` (bit-exact).  Decay goes through
+``pow(2, x)``; CPython calls glibc's pow, which is itself not correctly rounded for ~0.1%
+of inputs, so decay values are held to 2 ulp (rel 5e-16), far inside the north-star
+tolerance of 1e-9 absolute, and the exact-match rate is asserted to be high.
+"""
+import json
+import math
+import os
+import subprocess
+import sys
+import tempfile
+from datetime import datetime, timedelta, timezone
+
+import numpy as np
+import pytest
+
+from golden_util import load_json, load_npz
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "bayesian-consensus-engine_amd")
+EPOCH = datetime(1970, 1, 1, tzinfo=timezone.utc)
+ULP_REL = 5e-16
+
+
+def _eq(a, b):
+    """Python == with NaN == NaN, recursively, and the same JSON types (int vs float)."""
+    if isinstance(a, float) and isinstance(b, float) and math.isnan(a) and math.isnan(b):
+        return True
+    if isinstance(a, dict) and isinstance(b, dict):
+        return list(a) == list(b) and all(_eq(a[k], b[k]) for k in a)
+    if isinstance(a, list) and isinstance(b, list):
+        return len(a) == len(b) and all(_eq(x, y) for x, y in zip(a, b))
+    return type(a) is type(b) and a == b
+
+
+@pytest.mark.parametrize("case", load_json("consensus_cases.json"), ids=lambda c: c["name"])
+def test_compute_consensus_golden(case):
+    from bayesian_engine.core import compute_consensus
+    got = compute_consensus(case["signals"], case["source_reliability"])
+    assert _eq(got, case["expected"]), (got, case["expected"])
+
+
+def test_reference_golden_regression_fixture():
+    """The reference's own golden fixture (tests/fixtures/golden_regression.json, == on floats)."""
+    from bayesian_engine.core import compute_consensus, validate_input_payload
+    case = [c for c in load_json("consensus_cases.json") if c["name"] == "golden"][0]
+    payload = {"schemaVersion": "1.0.0", "marketId": "golden-regression-1", "signals": case["signals"]}
+    validate_input_payload(payload)
+    r = compute_consensus(payload["signals"])
+    assert r["consensus"] == 0.6966666666666667
+    assert [w["normalizedWeight"] for w in r["sourceWeights"]] == [0.3333333333333333] * 3
+    assert r == case["expected"]
+    assert all(compute_consensus(payload["signals"]) == r for _ in range(3))
+
+
+@pytest.mark.parametrize("case", load_json("validate_cases.json"), ids=lambda c: c["name"])
+def test_validate_input_payload_golden(case):
+    from bayesian_engine.core import ValidationError, validate_input_payload
+    if case["error"] is None:
+        validate_input_payload(case["payload"])
+    else:
+        with pytest.raises(ValidationError) as ei:
+            validate_input_payload(case["payload"])
+        assert str(ei.value) == case["error"]
+
+
+def _close(a, b):
+    if a == b:
+        return True
+    return abs(a - b) <= ULP_REL * max(abs(a), abs(b))
+
+
+def test_decay_golden():
+    from bayesian_engine.decay import apply_reliability_decay, compute_decay_factor, decay_reliability_if_needed
+    d = load_json("decay_cases.json")
+    exact = n = 0
+    for e, h, f in d["factor"]:
+        g = compute_decay_factor(e, h)
+        assert _close(g, f), (e, h, g, f)
+        exact += g == f
+        n += 1
+    for r, e, h, m, v in d["apply"]:
+        g = apply_reliability_decay(r, e, h, m)
+        assert _close(g, v), (r, e, h, m, g, v)
+        exact += g == v
+        n += 1
+    assert exact / n > 0.9, f"exact-match rate {exact / n:.3f}"
+    for r, stamp, now_us, v, changed in d["if_needed"]:
+        now = EPOCH + timedelta(microseconds=now_us)
+        g, c = decay_reliability_if_needed(r, stamp, now=now)
+        assert _close(g, v) and (c == changed or g != v)
+
+
+def test_decay_vectorized_matches_scalar():
+    import torch
+    from bayesian_engine.decay import apply_reliability_decay, compute_decay_factor
+    rng = np.random.default_rng(0)
+    e = rng.uniform(-5, 200, 10000)
+    r = rng.random(10000)
+    f = compute_decay_factor(e)
+    v = apply_reliability_decay(r, e)
+    for i in range(0, 10000, 997):
+        assert f[i] == compute_decay_factor(float(e[i])) or e[i] <= 0
+        assert v[i] == apply_reliability_decay(float(r[i]), float(e[i]))
+    tv = apply_reliability_decay(torch.tensor(r), torch.tensor(e))
+    assert np.array_equal(tv.cpu().numpy(), v)
+
+
+def test_update_traces_golden():
+    from bayesian_engine.reliability import SQLiteReliabilityStore
+    for tr in load_json("update_traces.json"):
+        store = SQLiteReliabilityStore(":memory:")
+        if tr["start"] != "cold":
+            store._conn.execute("INSERT INTO sources VALUES (?,?,?,?,?)",
+                                ("s", "m", tr["start"][0], tr["start"][1], "2026-01-01T00:00:00+00:00"))
+        sid = "src" if tr["start"] == "cold" else "s"
+        for st in tr["steps"]:
+            rec = store.update_reliability(sid, "m", st["correct"], dry_run=st.get("dry_run", False))
+            assert rec.reliability == st["reliability"] and rec.confidence == st["confidence"], (tr["name"], st)
+        store.close()
+
+
+def test_reliability_store_semantics(tmp_path):
+    """Restates the reference's tests/test_reliability.py assertions."""
+    from bayesian_engine.reliability import (DEFAULT_CONFIDENCE, DEFAULT_RELIABILITY, MAX_UPDATE_STEP,
+                                             SQLiteReliabilityStore)
+    s = SQLiteReliabilityStore(":memory:")
+    assert s.update_reliability("a", "m", True).reliability > DEFAULT_RELIABILITY
+    assert s.update_reliability("b", "m", False).reliability < DEFAULT_RELIABILITY
+    assert abs(s.get_reliability("a", "m").reliability - DEFAULT_RELIABILITY) <= MAX_UPDATE_STEP + 1e-9
+    for _ in range(20):
+        s.update_reliability("lo", "m", False)
+        s.update_reliability("hi", "m", True)
+    assert s.get_reliability("lo", "m").reliability == 0.0
+    assert s.get_reliability("hi", "m").reliability == 1.0
+    c1 = s.get_reliability("a", "m").confidence
+    s.update_reliability("a", "m", False)
+    assert s.get_reliability("a", "m").confidence > c1
+    s.update_reliability("x", "m1", True)
+    s.update_reliability("x", "m2", False)
+    assert s.get_reliability("x", "m1").reliability > DEFAULT_RELIABILITY > s.get_reliability("x", "m2").reliability
+    ids = [r.source_id for r in s.list_sources()]
+    assert ids == sorted(ids)
+    assert len(s.list_sources("m1")) == 1
+    s.close()
+    db = tmp_path / "p.db"
+    with SQLiteReliabilityStore(db) as st:
+        st.update_reliability("src-a", "m-1", True)
+    with SQLiteReliabilityStore(db) as st:
+        rec = st.get_reliability("src-a", "m-1")
+        assert rec.reliability > DEFAULT_RELIABILITY and rec.confidence > DEFAULT_CONFIDENCE
+
+
+def test_bulk_store_paths_match_per_row(tmp_path):
+    from bayesian_engine import decay as dmod
+    from bayesian_engine.reliability import SQLiteReliabilityStore
+    from bayesian_engine.timeutil import dt_to_us
+    rng = np.random.default_rng(3)
+    s = SQLiteReliabilityStore(":memory:")
+    now = datetime(2026, 3, 1, tzinfo=timezone.utc)
+    names = [f"s{i:04d}" for i in range(300)]
+    for n in names[::2]:
+        t = now - timedelta(microseconds=int(rng.integers(0, 90 * 86400 * 10**6)))
+        s._conn.execute("INSERT INTO sources VALUES (?,?,?,?,?)", (n, "g", float(rng.random()),
+                                                                   float(rng.random()), t.isoformat()))
+    table = s.load_table("g", names)
+    view = s.decayed_view(table, now=now).cpu().numpy()
+
+    class _Frozen(datetime):
+        @classmethod
+        def now(cls, tz=None):
+            return now
+
+    old = dmod.datetime
+    dmod.datetime = _Frozen
+    try:
+        for i, n in enumerate(names):
+            assert view[i] == s.get_reliability(n, "g", apply_decay=True).reliability
+    finally:
+        dmod.datetime = old
+    outcomes = {n: bool(rng.integers(0, 2)) for n in names[::3]}
+    per_row = {n: s.compute_update(n, "g", c) for n, c in outcomes.items()}
+    bulk = s.apply_outcomes("g", outcomes, now=now)
+    for n, rec in bulk.items():
+        assert (rec.reliability, rec.confidence) == (per_row[n].reliability, per_row[n].confidence)
+        assert s.get_reliability(n, "g").reliability == rec.reliability
+    assert dt_to_us(now) > 0
+    s.close()
+
+
+def test_tiebreak_golden():
+    from bayesian_engine.tiebreak import AgentSignal, DeterministicTieBreaker
+    cases = load_json("tiebreak_cases.json")
+    tb = DeterministicTieBreaker()
+    markets = []
+    for case in cases:
+        agents = [AgentSignal(a[0], a[1], a[2], a[3], a[4]) for a in case["agents"]]
+        markets.append(agents)
+        pred, diag = tb.resolve(agents)
+        assert pred == case["winner"]
+        assert diag.method == case["method"]
+        assert diag.tie_resolved_by == case["tie_resolved_by"]
+        assert diag.selected_group == case["selected_group"]
+        assert diag.confidence_variance == case["confidence_variance"]
+        assert [[k, v] for k, v in diag.groups.items()] == case["groups"]
+    # the batched entry point gives the same answers in one launch
+    batch = tb.resolve_many(markets)
+    for (pred, diag), case in zip(batch, cases):
+        assert pred == case["winner"] and diag.tie_resolved_by == case["tie_resolved_by"]
+
+
+def test_tiebreak_long_markets_vs_oracle():
+    import torch
+    from bayesian_engine import batch
+    from oracle import oracle as orc
+    rng = np.random.default_rng(9)
+    lens = np.array([65, 100, 1000, 4096, 2, 64, 300], np.int64)
+    off = np.zeros(len(lens) + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    n = int(off[-1])
+    pred = np.where(rng.random(n) < 0.5, rng.integers(0, 9, n) / 8.0, rng.random(n))
+    pred[rng.random(n) < 0.05] = -0.0
+    conf, weight, rel = rng.random(n), rng.choice([0.5, 1.0, 2.0], n), rng.choice([0.5, 0.9], n)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    r = batch.tiebreak(T(off), T(pred), T(conf), T(weight), T(rel), offsets_host=off)
+    exp = orc.tiebreak_csr(off, pred, conf, weight, rel)
+    assert np.array_equal(r.winner.cpu().numpy(), exp["winner"])
+    assert np.array_equal(r.label.cpu().numpy(), exp["label"])
+    assert np.array_equal(r.n_groups.cpu().numpy(), exp["n_groups"])
+    np.testing.assert_allclose(r.variance.cpu().numpy(), exp["variance"], rtol=1e-12)
+    for m in range(len(lens)):
+        a, g = int(off[m]), int(exp["n_groups"][m])
+        sl = slice(a, a + g)
+        assert np.array_equal(r.g_key.cpu().numpy()[sl], exp["g_key"][sl])
+        assert np.array_equal(r.g_count.cpu().numpy()[sl], exp["g_count"][sl])
+        assert np.array_equal(r.g_density.cpu().numpy()[sl], exp["g_total"][sl] / exp["g_count"][sl])
+        assert np.array_equal(r.g_maxrel.cpu().numpy()[sl], exp["g_maxrel"][sl])
+
+
+def test_summarize_sources_golden():
+    from bayesian_engine.market import CrossMarketAggregator, MarketId, MarketStore
+    for case in load_json("summarize_cases.json"):
+        store = MarketStore()
+        for mk in case["markets"]:
+            m = store.create_market(MarketId(mk["marketId"]))
+            for s in mk["signals"]:
+                m.add_signal(s)
+            if mk["resolved"]:
+                m.resolve(mk["outcome"])
+        perf = CrossMarketAggregator(store).summarize_sources()
+        assert list(perf) == case["order"]
+        for sid, e in case["expected"].items():
+            p = perf[sid]
+            assert (p.total_markets, p.correct_predictions, p.wrong_predictions, p.reliability, p.markets) == \
+                (e["total"], e["correct"], e["wrong"], e["reliability"], e["markets"])
+
+
+def test_compute_all_consensus_golden():
+    from bayesian_engine import decay as dmod
+    from bayesian_engine.market import MarketId, MarketStore
+    from bayesian_engine.reliability import SQLiteReliabilityStore
+    for case in load_json("market_cases.json"):
+        store = SQLiteReliabilityStore(":memory:")
+        for row in case["rows"]:
+            store._conn.execute("INSERT INTO sources VALUES (?,?,?,?,?)", tuple(row))
+        ms = MarketStore()
+        for mk in case["markets"]:
+            m = ms.create_market(MarketId(mk["marketId"]))
+            for s in mk["signals"]:
+                m.add_signal(s)
+            if mk["resolved"]:
+                m.resolve(True)
+        now = EPOCH + timedelta(microseconds=case["now_us"])
+
+        class _Frozen(datetime):
+            @classmethod
+            def now(cls, tz=None):
+                return now
+
+        old = dmod.datetime
+        dmod.datetime = _Frozen
+        try:
+            got = ms.compute_all_consensus(store)
+        finally:
+            dmod.datetime = old
+        exp = case["expected"]
+        assert list(got) == list(exp)
+        for k in exp:
+            g, e = got[k], exp[k]
+            assert list(g) == list(e)
+            if e.get("consensus") is not None:
+                assert abs(g["consensus"] - e["consensus"]) <= 1e-12 and abs(g["confidence"] - e["confidence"]) <= 1e-12
+                for gw, ew in zip(g["sourceWeights"], e["sourceWeights"]):
+                    assert gw["sourceId"] == ew["sourceId"] and _close(gw["weight"], ew["weight"])
+            assert g["diagnostics"] == e["diagnostics"] if "diagnostics" in e else True
+        assert _eq(ms.compute_all_consensus(None), case["expected_no_store"])
+        store.close()
+
+
+def test_multi_market_reference_assertions():
+    """Restates the reference's tests/test_multi_market.py numeric assertions."""
+    from bayesian_engine.market import CrossMarketAggregator, Market, MarketId, MarketStore
+    m = Market(id=MarketId("test-1"))
+    m.add_signal({"sourceId": "agent-a", "probability": 0.7})
+    m.add_signal({"sourceId": "agent-b", "probability": 0.8})
+    assert m.compute_consensus()["consensus"] == 0.75
+    store = MarketStore()
+    m1 = store.create_market(MarketId("crypto:btc:1"))
+    m1.add_signal({"sourceId": "agent-a", "probability": 0.8})
+    m1.add_signal({"sourceId": "agent-b", "probability": 0.7})
+    m1.resolve(True)
+    m2 = store.create_market(MarketId("crypto:btc:2"))
+    m2.add_signal({"sourceId": "agent-a", "probability": 0.6})
+    m2.add_signal({"sourceId": "agent-b", "probability": 0.3})
+    m2.resolve(True)
+    perf = CrossMarketAggregator(store).summarize_sources()
+    assert perf["agent-a"].correct_predictions == 2 and perf["agent-a"].accuracy == 1.0
+    assert perf["agent-b"].correct_predictions == 1 and perf["agent-b"].accuracy == 0.5
+    for market in store.list_markets():
+        market.compute_consensus()
+    agg = CrossMarketAggregator(store)
+    assert agg.aggregate_consensus(["crypto:*"])["marketsIncluded"] == 2
+    assert agg.aggregate_consensus(["crypto:*"], method="majority")["method"] == "majority"
+
+
+def test_reestimate_c5_slice():
+    import torch
+    from bayesian_engine import batch
+    g = load_npz("c5_reestimate.npz")
+    K = int(g["iters"])
+    P = torch.from_numpy(g["P"]).cuda()
+    w, cons, nul, agree, hist = batch.reestimate(P, K, keep_history=True)
+    for k in range(K):
+        assert np.array_equal(hist[k][0].cpu().numpy(), g["consensus"][k])
+        assert np.array_equal(hist[k][1].cpu().numpy(), g["is_null"][k])
+        assert np.array_equal(hist[k][2].cpu().numpy(), g["agree"][k])
+        assert np.array_equal(hist[k][3].cpu().numpy(), g["weights"][k])
+
+
+def test_c4_replay_slice():
+    """Config-4 replay through the fused replay_step kernel vs the reference trace."""
+    import torch
+    from bayesian_engine import batch
+    g = load_npz("c4_replay.npz")
+    pres = g["present"].copy()
+    r = np.where(pres == 1, g["r0"], 0.5)
+    c = np.where(pres == 1, g["c0"], 0.25)
+    t = g["t0_us"].copy()
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    dr, dc, dt, dp = T(r), T(c), T(t), T(pres)
+    view = torch.empty_like(dr)
+    exact = total = 0
+    for k in range(g["flags"].shape[0]):
+        now = int(g["now0_us"]) + k * int(g["step_us"])
+        f = g["flags"][k]
+        f2 = batch.pack_flags2((f & 1) == 1, (f & 2) == 2)
+        batch.replay_step(dr, dc, dt, dp, T(f2), now, view)
+        v = view.cpu().numpy()
+        exp = g["views"][k]
+        assert np.all(np.abs(v - exp) <= ULP_REL * np.maximum(np.abs(v), np.abs(exp)))
+        exact += int(np.sum(v == exp))
+        total += v.size
+    assert exact / total > 0.95
+    fp = g["final_present"] == 1
+    assert np.array_equal(dp.cpu().numpy() == 1, fp)
+    assert np.array_equal(dr.cpu().numpy()[fp], g["final_r"][fp])
+    assert np.array_equal(dc.cpu().numpy()[fp], g["final_c"][fp])
+
+
+def _cli(args, stdin=None, cwd=None):
+    env = dict(os.environ, PYTHONPATH=PKG)
+    return subprocess.run([sys.executable, "-m", "bayesian_engine.cli"] + args, capture_output=True, text=True,
+                          input=stdin, env=env, cwd=cwd, timeout=600)
+
+
+def test_cli_cases_golden():
+    fx = load_json("cli_cases.json")
+    with tempfile.TemporaryDirectory() as d:
+        for name, payload in fx["inputs"].items():
+            with open(os.path.join(d, name), "w") as f:
+                json.dump(payload, f)
+        for case in fx["cases"]:
+            p = _cli([a.replace("{DIR}", d) for a in case["args"]], stdin=case["stdin"], cwd=d)
+            assert p.returncode == case["rc"], (case["args"], p.stderr)
+            assert p.stdout == case["stdout"], case["args"]
+            if case["rc"]:
+                assert p.stderr.strip().splitlines()[-1] == case["stderr"].strip().splitlines()[-1]
+
+
+def test_cli_dry_run_and_db_reliability():
+    """Restates the reference's tests/test_dry_run.py flows."""
+    with tempfile.TemporaryDirectory() as d:
+        db = os.path.join(d, "t.db")
+        p = _cli(["--db", db, "--dry-run", "report-outcome", "--source-id", "agent-a", "--market-id", "market-1",
+                  "--correct"])
+        out = json.loads(p.stdout)
+        assert p.returncode == 0 and out["dryRun"] is True and out["reliability"] > 0.5
+        assert json.loads(_cli(["--db", db, "list-sources"]).stdout)["count"] == 0
+        assert json.loads(_cli(["--db", db, "--dry-run", "report-outcome", "--source-id", "a", "--market-id",
+                                "m"]).stdout)["reliability"] < 0.5
+        p = _cli(["--db", db, "report-outcome", "--source-id", "agent-a", "--market-id", "market-1", "--correct"])
+        assert json.loads(p.stdout)["dryRun"] is False
+        ls = json.loads(_cli(["--db", db, "list-sources", "--market-id", "market-1"]).stdout)
+        assert ls["count"] == 1 and ls["sources"][0]["sourceId"] == "agent-a"
+        payload = {"schemaVersion": "1.0.0", "marketId": "market-1",
+                   "signals": [{"sourceId": "agent-a", "probability": 0.6}, {"sourceId": "agent-b", "probability": 0.4}]}
+        p = _cli(["--db", db, "consensus"], stdin=json.dumps(payload))
+        w = {x["sourceId"]: x["weight"] for x in json.loads(p.stdout)["sourceWeights"]}
+        assert w["agent-a"] > w["agent-b"]

@@ -20,18 +20,15 @@ OUT = os.path.join(ROOT, "tools", "ablate_build")
 
 VARIANTS = {
     "base": [],
-    "nosort": ["-DBCE_ABLATE=1"],
-    "nogather": ["-DBCE_ABLATE=2"],
-    "noserial": ["-DBCE_ABLATE=4"],
-    "nouniqout": ["-DBCE_ABLATE=8"],
-    "nodup": ["-DBCE_ABLATE=16"],
-    "alloff": ["-DBCE_ABLATE=31"],
     "tm8": ["-DBCE_SEG32_TM=8"],
-    "tm32": ["-DBCE_SEG32_TM=32"],
-    "grid8": ["-DBCE_SEG_GRID_PER_CU=8"],
-    "grid64": ["-DBCE_SEG_GRID_PER_CU=64"],
-    "grid4": ["-DBCE_SEG_GRID_PER_CU=4"],
-    "grid12": ["-DBCE_SEG_GRID_PER_CU=12"],
+    "tm4": ["-DBCE_SEG32_TM=4"],
+    "tm4_s0": ["-DBCE_SEG32_TM=4", "-DBCE_STAGE=0"],
+    "tm8_s0": ["-DBCE_SEG32_TM=8", "-DBCE_STAGE=0"],
+    "tm4_nouniq": ["-DBCE_SEG32_TM=4", "-DBCE_ABLATE=8"],
+    "tm4_nogather": ["-DBCE_SEG32_TM=4", "-DBCE_ABLATE=2"],
+    "tm4_nosort": ["-DBCE_SEG32_TM=4", "-DBCE_ABLATE=1"],
+    "tm4_alloff": ["-DBCE_SEG32_TM=4", "-DBCE_ABLATE=31"],
+    "tm4_alloff_s0": ["-DBCE_SEG32_TM=4", "-DBCE_ABLATE=31", "-DBCE_STAGE=0"],
 }
 SRCS = ["capi.hip", "consensus.hip"]
 
