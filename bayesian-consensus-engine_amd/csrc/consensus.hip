@@ -33,7 +33,16 @@
 #define BCE_ABLATE 0
 #endif
 #ifndef BCE_SEG32_TM
-#define BCE_SEG32_TM 16
+#define BCE_SEG32_TM 8
+#endif
+#ifndef BCE_LPM_LOAD
+#define BCE_LPM_LOAD 0  // 0: per-market LDS-DMA rows; 2: direct per-lane loads + payload sort
+#endif
+#ifndef BCE_LPM_SYNC
+#define BCE_LPM_SYNC 1
+#endif
+#ifndef BCE_USE_LPM
+#define BCE_USE_LPM 1  // lane-per-market kernel for n <= 32 (else the cooperative one)
 #endif
 #ifndef BCE_SEG_GRID_PER_CU
 #define BCE_SEG_GRID_PER_CU 0  // 0 = exactly the resident occupancy (persistent grid)
@@ -340,6 +349,279 @@ void consensus_seg_kernel(ConsArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
+// short markets, lane per market: consensus_lpm_kernel<G>  (n <= G, G in {8, 16, 32})
+// ------------------------------------------------------------------------------------
+// Batcher odd-even merge sort network for N (power of two) keys, generated at compile
+// time; with full unrolling every key index is a constant, so the keys live in VGPRs.
+template <int N>
+struct OemNet {
+  static constexpr int count() {
+    int c = 0;
+    for (int p = 1; p < N; p <<= 1)
+      for (int k = p; k >= 1; k >>= 1)
+        for (int j = k % p; j + k < N; j += 2 * k)
+          for (int i = 0; i < k && i + j + k < N; ++i)
+            if ((i + j) / (2 * p) == (i + j + k) / (2 * p)) ++c;
+    return c;
+  }
+  static constexpr int C = count();
+  struct Pairs {
+    int a[C > 0 ? C : 1];
+    int b[C > 0 ? C : 1];
+  };
+  static constexpr Pairs make() {
+    Pairs r{};
+    int c = 0;
+    for (int p = 1; p < N; p <<= 1)
+      for (int k = p; k >= 1; k >>= 1)
+        for (int j = k % p; j + k < N; j += 2 * k)
+          for (int i = 0; i < k && i + j + k < N; ++i)
+            if ((i + j) / (2 * p) == (i + j + k) / (2 * p)) {
+              r.a[c] = i + j;
+              r.b[c] = i + j + k;
+              ++c;
+            }
+    return r;
+  }
+};
+
+template <int N>
+__device__ __forceinline__ void oem_sort(unsigned (&key)[N]) {
+  constexpr auto P = OemNet<N>::make();
+#pragma unroll
+  for (int c = 0; c < OemNet<N>::C; ++c) {
+    const unsigned x = key[P.a[c]], y = key[P.b[c]];
+    key[P.a[c]] = x < y ? x : y;
+    key[P.b[c]] = x < y ? y : x;
+  }
+}
+
+// Same network carrying a payload (the probability) with each key.
+template <int N>
+__device__ __forceinline__ void oem_sort_kv(unsigned (&key)[N], double (&val)[N]) {
+  constexpr auto P = OemNet<N>::make();
+#pragma unroll
+  for (int c = 0; c < OemNet<N>::C; ++c) {
+    const unsigned x = key[P.a[c]], y = key[P.b[c]];
+    const double vx = val[P.a[c]], vy = val[P.b[c]];
+    const bool sw = y < x;
+    key[P.a[c]] = sw ? y : x;
+    key[P.b[c]] = sw ? x : y;
+    val[P.a[c]] = sw ? vy : vx;
+    val[P.b[c]] = sw ? vx : vy;
+  }
+}
+
+// LDS ordering inside a single-wave workgroup: the wave's LDS instructions execute in
+// order, so a compiler barrier + lgkmcnt drain is all a cross-lane hand-off needs.
+__device__ __forceinline__ void wave_sync() {
+#if BCE_LPM_SYNC
+  __syncthreads();
+#else
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+}
+
+__device__ __forceinline__ void dma4(const void* g, void* lds) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds, 4, 0, 0);
+}
+
+template <int G>
+__global__ __launch_bounds__(64) void consensus_lpm_kernel(ConsArgs a) {
+  static_assert(G == 8 || G == 16 || G == 32, "lane-per-market widths");
+  constexpr int LOGG = (G == 8) ? 3 : (G == 16) ? 4 : 5;
+  constexpr int SST = G + 1;       // sid / usid row stride (dwords): conflict-free b32 reads
+  constexpr int PST = 2 * G + 2;   // prob / weight row stride (dwords, even -> 8-B aligned)
+  constexpr int RING = 8;          // gathers issued this many sorted positions ahead
+  constexpr int MPI = kWave / G;   // markets per copy-out iteration
+
+  __shared__ uint32_t sS[kWave * SST];  // sid rows; after the walk: usid rows
+  __shared__ uint32_t sP[kWave * PST];  // prob rows; after the sorted read: weight rows
+  __shared__ int64_t sOff[kWave];
+  __shared__ int32_t sU[kWave];
+  __shared__ double sTot[kWave];
+
+  const int lane = lane_id();
+  const int64_t n_tiles = (a.n_list + kWave - 1) / kWave;
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    // ---- this lane's market ---------------------------------------------------------
+    const int64_t li = tile * kWave + lane;
+    int32_t mk = -1;
+    int64_t off = 0;
+    int n = 0;
+    if (li < a.n_list) {
+      mk = a.list ? a.list[li] : (int32_t)li;
+      off = a.offsets[mk];
+      n = (int)(a.offsets[mk + 1] - off);
+    }
+
+    unsigned key[G];
+    double sp[G];
+    int err = -1;
+    if constexpr (BCE_LPM_LOAD == 2) {
+      // ---- direct per-lane loads: the lane's row of sids / probabilities -------------
+      const bool aligned = ballot((off & 3) != 0) == 0;
+      if (aligned) {
+#pragma unroll
+        for (int c = 0; c < G / 4; ++c) {
+          int4 v = make_int4(0, 0, 0, 0);
+          if (4 * c < n) v = *reinterpret_cast<const int4*>(a.sid + off + 4 * c);
+          key[4 * c] = (unsigned)v.x; key[4 * c + 1] = (unsigned)v.y;
+          key[4 * c + 2] = (unsigned)v.z; key[4 * c + 3] = (unsigned)v.w;
+        }
+#pragma unroll
+        for (int c = 0; c < G / 2; ++c) {
+          double2 v = make_double2(0.0, 0.0);
+          if (2 * c < n) v = *reinterpret_cast<const double2*>(a.prob + off + 2 * c);
+          sp[2 * c] = v.x; sp[2 * c + 1] = v.y;
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < G; ++t) {
+          key[t] = (t < n) ? (unsigned)a.sid[off + t] : 0u;
+          sp[t] = (t < n) ? a.prob[off + t] : 0.0;
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < G; ++t) {
+        const bool v = t < n;
+        key[t] = v ? ((key[t] << LOGG) | (unsigned)t) : kSent32;
+        if (v && err < 0 && (sp[t] < 0.0 || sp[t] > 1.0)) err = t;  // core.py:59-60
+      }
+      if constexpr (!(BCE_ABLATE & 1)) oem_sort_kv<G>(key, sp);
+    } else {
+      // ---- rows -> LDS by LDS-DMA: one dword per lane, market by market --------------
+      for (int q = 0; q < kWave; ++q) {
+        const int nq = __builtin_amdgcn_readlane(n, q);
+        if (nq == 0) continue;
+        const int64_t oq = ((int64_t)__builtin_amdgcn_readlane((int)(off >> 32), q) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((int)off, q);
+        if (lane < nq) dma4(a.sid + oq + lane, sS + q * SST);
+        if (lane < 2 * nq) dma4(reinterpret_cast<const uint32_t*>(a.prob + oq) + lane, sP + q * PST);
+        if (2 * nq > kWave && lane < 2 * nq - kWave)
+          dma4(reinterpret_cast<const uint32_t*>(a.prob + oq) + kWave + lane, sP + q * PST + kWave);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      wave_sync();
+      const uint32_t* rowS = sS + lane * SST;
+      const double* rowP = reinterpret_cast<const double*>(sP + lane * PST);
+      // keys (sid, slot) and the validation scan in input order
+#pragma unroll
+      for (int t = 0; t < G; ++t) {
+        const bool v = t < n;
+        key[t] = v ? ((rowS[t] << LOGG) | (unsigned)t) : kSent32;
+        const double p = rowP[t];
+        if (v && err < 0 && (p < 0.0 || p > 1.0)) err = t;  // core.py:59-60 (NaN passes)
+      }
+      if constexpr (!(BCE_ABLATE & 1)) oem_sort<G>(key);
+      // probabilities in sorted order (registers); the rows become output staging
+#pragma unroll
+      for (int t = 0; t < G; ++t) sp[t] = rowP[key[t] & (G - 1)];
+      wave_sync();
+    }
+
+    // ---- walk in sorted order: runs summed in input order (core.py:116), then the
+    //      reference's left-to-right totals over unique sources (core.py:107-144) -----
+    uint32_t* outS = sS + lane * SST;                         // usid of unique j
+    double* outW = reinterpret_cast<double*>(sP + lane * PST);  // weight of unique j
+    double2 rc[RING];
+    uint32_t pw[RING];
+#pragma unroll
+    for (int t = 0; t < RING && t < G; ++t) {
+      const bool kv = key[t] != kSent32;
+      const int sid = (int)(key[t] >> LOGG);
+      const bool fst = kv && (t == 0 || sid != (int)(key[t - 1 > 0 ? t - 1 : 0] >> LOGG));
+      if (!(BCE_ABLATE & 2) && fst) {
+        rc[t] = a.relconf[sid];
+        pw[t] = a.pbits[sid >> 5];
+      } else {
+        rc[t] = make_double2(0.5, 0.25);
+        pw[t] = 0xffffffffu;
+      }
+    }
+    double total = 0.0, ws = 0.0, cs = 0.0;
+    double psum = 0.0;
+    int cnt = 0, j = 0, psid = 0;
+    double2 prc = make_double2(0.0, 0.0);
+    uint32_t ppw = 0;
+    auto finalize = [&]() {
+      double avg = psum;
+      if (ballot(cnt > 1)) {  // duplicates: avg = sum / len (core.py:116), rare
+        if (cnt > 1) avg = psum / (double)cnt;
+      }
+      const double w = prc.x, c = prc.y;
+      total += w;          // core.py:120
+      ws += avg * w;       // core.py:135-137
+      cs += c * w;         // core.py:141-143
+      const bool cold = ((ppw >> (psid & 31)) & 1u) == 0;  // core.py:167-170
+      outS[j] = (uint32_t)psid | (cold ? 0x80000000u : 0u);
+      outW[j] = w;
+      ++j;
+    };
+#pragma unroll
+    for (int t = 0; t < G; ++t) {
+      const bool kv = key[t] != kSent32;
+      const int sid = (int)(key[t] >> LOGG);
+      const bool fst = kv && (t == 0 || sid != (int)(key[t > 0 ? t - 1 : 0] >> LOGG));
+      if (fst) {
+        if (cnt > 0) finalize();
+        psid = sid;
+        prc = rc[t % RING];
+        ppw = pw[t % RING];
+        psum = 0.0 + sp[t];  // builtin sum() starts from int 0
+        cnt = 1;
+      } else if (kv) {
+        psum += sp[t];
+        ++cnt;
+      }
+      if (t + RING < G) {  // refill the ring slot just consumed
+        const int tt = t + RING;
+        const bool kv2 = key[tt] != kSent32;
+        const int sid2 = (int)(key[tt] >> LOGG);
+        const bool fst2 = kv2 && sid2 != (int)(key[tt - 1] >> LOGG);
+        if (!(BCE_ABLATE & 2) && fst2) {
+          rc[tt % RING] = a.relconf[sid2];
+          pw[tt % RING] = a.pbits[sid2 >> 5];
+        }
+      }
+    }
+    if (cnt > 0) finalize();
+
+    // ---- per-market results (lane = market: coalesced) ------------------------------
+    if (mk >= 0) {
+      const bool null_ = (total == 0.0);  // core.py:131-133
+      a.consensus[mk] = null_ ? 0.0 : ws / total;
+      a.confidence[mk] = null_ ? 0.0 : cs / total;
+      a.total_weight[mk] = total;
+      a.n_unique[mk] = j;
+      if (a.err_idx) a.err_idx[mk] = err;
+    }
+    sOff[lane] = off;
+    sU[lane] = (mk >= 0) ? j : 0;
+    sTot[lane] = total;
+    wave_sync();
+
+    // ---- per-unique outputs: MPI markets per iteration, lane = slot (coalesced) ------
+    if ((a.usid || a.weight || a.nweight) && !(BCE_ABLATE & 8)) {
+      const int slot = lane & (G - 1);
+#pragma unroll 4
+      for (int it = 0; it < G; ++it) {
+        const int q = it * MPI + lane / G;
+        if (slot < sU[q]) {
+          const int64_t p = sOff[q] + slot;
+          const double w = reinterpret_cast<const double*>(sP + q * PST)[slot];
+          const double tot = sTot[q];
+          if (a.usid) a.usid[p] = (int32_t)sS[q * SST + slot];
+          if (a.weight) a.weight[p] = w;
+          if (a.nweight) a.nweight[p] = (tot > 0.0) ? w / tot : 0.0;  // core.py:151
+        }
+      }
+    }
+    wave_sync();
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // long markets: workgroup per market
 // ------------------------------------------------------------------------------------
 constexpr int kLongThreads = 256;
@@ -575,10 +857,35 @@ int launch_seg(const ConsArgs& a, hipStream_t st) {
   return check_launch("consensus_seg_kernel");
 }
 
+template <int G>
+int launch_lpm(const ConsArgs& a, hipStream_t st) {
+  const int64_t tiles = (a.n_list + kWave - 1) / kWave;
+  if (tiles == 0) return BCE_OK;
+  static int per_cu = 0;
+  if (!per_cu) {
+    int nb = 0;
+    if (BCE_SEG_GRID_PER_CU > 0) nb = BCE_SEG_GRID_PER_CU;
+    else if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, consensus_lpm_kernel<G>, 64, 0) !=
+                 hipSuccess || nb <= 0)
+      nb = 4;
+    per_cu = nb;
+  }
+  const int64_t cap = (int64_t)cu_count() * per_cu;
+  const int grid = (int)(tiles < cap ? tiles : cap);
+  hipLaunchKernelGGL((consensus_lpm_kernel<G>), dim3(grid), dim3(64), 0, st, a);
+  return check_launch("consensus_lpm_kernel");
+}
+
 int launch_seg_for_len(int max_len, const ConsArgs& a, hipStream_t st) {
-  if (max_len <= 8) return launch_seg<8, 64>(a, st);
-  if (max_len <= 16) return launch_seg<16, 32>(a, st);
-  if (max_len <= 32) return launch_seg<32, BCE_SEG32_TM>(a, st);
+  if (BCE_USE_LPM) {
+    if (max_len <= 8) return launch_lpm<8>(a, st);
+    if (max_len <= 16) return launch_lpm<16>(a, st);
+    if (max_len <= 32) return launch_lpm<32>(a, st);
+  } else {
+    if (max_len <= 8) return launch_seg<8, 64>(a, st);
+    if (max_len <= 16) return launch_seg<16, 32>(a, st);
+    if (max_len <= 32) return launch_seg<32, BCE_SEG32_TM>(a, st);
+  }
   return launch_seg<64, 8>(a, st);
 }
 

@@ -19,16 +19,12 @@ CSRC = os.path.join(ROOT, "bayesian-consensus-engine_amd", "csrc")
 OUT = os.path.join(ROOT, "tools", "ablate_build")
 
 VARIANTS = {
-    "base": [],
-    "tm8": ["-DBCE_SEG32_TM=8"],
-    "tm4": ["-DBCE_SEG32_TM=4"],
-    "tm4_s0": ["-DBCE_SEG32_TM=4", "-DBCE_STAGE=0"],
-    "tm8_s0": ["-DBCE_SEG32_TM=8", "-DBCE_STAGE=0"],
-    "tm4_nouniq": ["-DBCE_SEG32_TM=4", "-DBCE_ABLATE=8"],
-    "tm4_nogather": ["-DBCE_SEG32_TM=4", "-DBCE_ABLATE=2"],
-    "tm4_nosort": ["-DBCE_SEG32_TM=4", "-DBCE_ABLATE=1"],
-    "tm4_alloff": ["-DBCE_SEG32_TM=4", "-DBCE_ABLATE=31"],
-    "tm4_alloff_s0": ["-DBCE_SEG32_TM=4", "-DBCE_ABLATE=31", "-DBCE_STAGE=0"],
+    "lpm": [],
+    "coop_tm8": ["-DBCE_USE_LPM=0"],
+    "lpm_noout": ["-DBCE_ABLATE=8"],
+    "lpm_nogather": ["-DBCE_ABLATE=2"],
+    "lpm_nosort": ["-DBCE_ABLATE=1"],
+    "lpm_all": ["-DBCE_ABLATE=11"],
 }
 SRCS = ["capi.hip", "consensus.hip"]
 
