@@ -23,6 +23,9 @@
 //                         tree (BCE_MODE_FAST).
 //
 // FP contraction is off for the whole file: every mul/add rounds like CPython.
+#include <stdio.h>
+#include <stdlib.h>
+
 #include "bce_device.hpp"
 #include "bce_internal.hpp"
 
@@ -49,6 +52,30 @@
 #endif
 #ifndef BCE_SEG_WPE
 #define BCE_SEG_WPE 1  // __launch_bounds__ min waves per SIMD for the segment kernel
+#endif
+#ifndef BCE_FLAT
+#define BCE_FLAT 3  // contiguous tiles, list == NULL, n <= 32: 3 = pipe, 2 = stream, 1 = flat, 0 = lpm
+#endif
+#ifndef BCE_FLAT_TM
+#define BCE_FLAT_TM 64
+#endif
+#ifndef BCE_PIPE_DBG
+#define BCE_PIPE_DBG 0
+#endif
+#ifndef BCE_STREAM_WPB
+#define BCE_STREAM_WPB 5
+#endif
+#ifndef BCE_STREAM_CH
+#define BCE_STREAM_CH 4
+#endif
+#ifndef BCE_FLAT_RING
+#define BCE_FLAT_RING 8  // relconf gathers in flight per lane
+#endif
+#ifndef BCE_FLAT_WPE
+#define BCE_FLAT_WPE 1  // min waves per SIMD (register budget) for the flat kernel
+#endif
+#ifndef BCE_FLAT_WPB
+#define BCE_FLAT_WPB 2
 #endif
 #ifndef BCE_STAGE
 #define BCE_STAGE 1  // LDS-staged 16-B input loads for contiguous tiles
@@ -422,6 +449,11 @@ __device__ __forceinline__ void wave_sync() {
 #endif
 }
 
+// Cross-lane LDS hand-off inside ONE wave (waves of a workgroup run independently): the
+// wave's LDS instructions execute in order, so draining lgkmcnt behind a compiler
+// barrier orders every earlier ds_write before every later ds_read / LDS-DMA.
+__device__ __forceinline__ void wave_sync_lds() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
 __device__ __forceinline__ void dma4(const void* g, void* lds) {
   __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds, 4, 0, 0);
 }
@@ -618,6 +650,999 @@ __global__ __launch_bounds__(64) void consensus_lpm_kernel(ConsArgs a) {
       }
     }
     wave_sync();
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// contiguous short markets, lane per market: consensus_flat_kernel<G, TM, WPB>
+// ------------------------------------------------------------------------------------
+// The headline path (list == NULL, every n <= G).  WPB independent waves per workgroup
+// share only the present bitmask; each wave owns a tile of TM consecutive markets whose
+// signals form ONE contiguous range [B, E):
+//   1. B, E by scalar loads; the range is streamed into the wave's LDS image with 16-B
+//      LDS-DMA (global_load_lds_dwordx4): ceil(TM*G*12 / 1 KiB) wave-instructions, no
+//      per-market loop, no VGPR staging.
+//   2. lane = market: its sids -> 32-bit keys (sid << log2 G | slot), Batcher odd-even
+//      merge network in VGPRs.
+//   3. walk in sorted order (branch-free): probability of the sorted slot from LDS,
+//      duplicate runs summed in input order (core.py:115-116), one 16-B relconf gather
+//      per position (ring RING ahead), and the reference's left-to-right totals over
+//      unique sources (core.py:120, 135-143) gated by "last of its run".  The range
+//      check of core.py:59-60 is the minimum failing slot.  Per unique j the packed
+//      (sid | slot << 25) goes to the (dead) sid image at j and the weight over the
+//      (consumed) probability cell of that slot.
+//   4. per-market scalars (lane = market, coalesced); per-unique outputs with G/2 lanes
+//      per market, two slots per lane: 8-B usid pairs and 16-B weight/nweight pairs.
+constexpr int kPackSlot = 25;  // packed = sid | slot << 25 (sid < 2^25)
+// global (not constant) address space: selected against the relconf argument, a constant
+// pointer would turn the gathers into flat loads (vmcnt + lgkmcnt, out of order)
+__device__ double2 kColdRow[1] = {{0.5, 0.25}};  // DEFAULT_RELIABILITY / _CONFIDENCE
+
+template <int G, int TM, int WPB>
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(BCE_FLAT_WPE, 8)))
+void consensus_flat_kernel(ConsArgs a) {
+  static_assert(G == 8 || G == 16 || G == 32, "flat widths");
+  static_assert(TM == 32 || TM == 64, "markets per wave tile");
+  constexpr int LOGG = (G == 8) ? 3 : (G == 16) ? 4 : 5;
+  constexpr int TS = TM * G;           // max signals per tile
+  constexpr int SW = TS + 8 + G;       // sid image (dwords): alignment slack, row overrun, sink
+  constexpr int PW = TS + 4 + G;       // prob image (doubles)
+  constexpr int RING = BCE_FLAT_RING;
+  constexpr int P = G / 2;             // lanes per market in the copy-out (2 slots each)
+  constexpr int MPI = kWave / P;       // markets per copy-out iteration
+
+  __shared__ uint32_t sBits[kBitsLds];
+  __shared__ __attribute__((aligned(16))) uint32_t sSid[WPB][SW];
+  __shared__ __attribute__((aligned(16))) double sProb[WPB][PW];
+  __shared__ double sTot[WPB][TM];
+  __shared__ int32_t sU[WPB][TM];
+  __shared__ int32_t sRs[WPB][TM];
+
+  const int lane = lane_id();
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int nwords = (a.n_sources + 31) >> 5;
+  const bool bits_in_lds = nwords <= kBitsLds;
+  if (bits_in_lds)
+    for (int i = threadIdx.x; i < nwords; i += 64 * WPB) sBits[i] = a.pbits[i];
+  __syncthreads();  // the only workgroup barrier: waves are independent from here on
+
+  uint32_t* const iS = sSid[w];
+  double* const iP = sProb[w];
+  const int64_t M = a.n_list;
+  const int64_t n_tiles = (M + TM - 1) / TM;
+  for (int64_t tile = (int64_t)blockIdx.x * WPB + w; tile < n_tiles; tile += (int64_t)gridDim.x * WPB) {
+    const int64_t m0 = tile * TM;
+    const int64_t m1 = (m0 + TM < M) ? m0 + TM : M;
+    const int64_t B = a.offsets[m0];   // wave-uniform: scalar loads
+    const int64_t E = a.offsets[m1];
+    const int64_t Bs = B & ~3ll, Bp = B & ~1ll;
+
+    // ---- this lane's market ------------------------------------------------------------
+    const int64_t mk = m0 + lane;
+    const bool has = lane < TM && mk < M;
+    int64_t off = B;
+    int n = 0;
+    if (has) {
+      off = a.offsets[mk];
+      n = (int)(a.offsets[mk + 1] - off);
+    }
+
+    // ---- 1. stream [B, E) into the LDS image (16-B LDS-DMA, full chunks in bounds) -------
+    {
+      const int64_t Nf4 = a.n_signals & ~3ll;                  // last full 4-sid chunk end
+      const int64_t es = (E < Nf4) ? ((E + 3) & ~3ll) : Nf4;   // DMA end (sids)
+      const int nci = (int)((es - Bs) >> 2);                   // 16-B chunks
+      for (int i = 0; i * kWave < nci; ++i) {
+        const int c = i * kWave + lane;
+        if (c < nci)
+          __builtin_amdgcn_global_load_lds(a.sid + Bs + 4 * c,
+                                           (__attribute__((address_space(3))) void*)(iS + i * 256), 16, 0, 0);
+      }
+      const int64_t Nf2 = a.n_signals & ~1ll;
+      const int64_t ep = (E < Nf2) ? ((E + 1) & ~1ll) : Nf2;
+      const int ncp = (int)((ep - Bp) >> 1);
+      for (int i = 0; i * kWave < ncp; ++i) {
+        const int c = i * kWave + lane;
+        if (c < ncp)
+          __builtin_amdgcn_global_load_lds(a.prob + Bp + 2 * c,
+                                           (__attribute__((address_space(3))) void*)(iP + i * 128), 16, 0, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // tail of the arrays that does not fill a 16-B chunk (last tile only)
+      if (E > es && lane < (int)(E - es)) iS[es - Bs + lane] = (uint32_t)a.sid[es + lane];
+      if (E > ep && lane < (int)(E - ep)) iP[ep - Bp + lane] = a.prob[ep + lane];
+      wave_sync_lds();
+    }
+
+    // ---- 2. keys + sort ------------------------------------------------------------------
+    const int rs = (int)(off - B);            // row start relative to B
+    const int rsi = rs + (int)(B - Bs);       // ... in the sid image
+    const int rsp = rs + (int)(B - Bp);       // ... in the prob image
+    unsigned key[G];
+    if (ballot(has && (rsi & 3) != 0) == 0) {
+#pragma unroll
+      for (int c = 0; c < G / 4; ++c) {
+        const uint4 v = *reinterpret_cast<const uint4*>(iS + rsi + 4 * c);
+        key[4 * c] = v.x; key[4 * c + 1] = v.y; key[4 * c + 2] = v.z; key[4 * c + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < G; ++t) key[t] = iS[rsi + t];
+    }
+#pragma unroll
+    for (int t = 0; t < G; ++t) key[t] = (t < n) ? ((key[t] << LOGG) | (unsigned)t) : kSent32;
+    if constexpr (!(BCE_ABLATE & 1)) oem_sort<G>(key);
+    // run structure as bit masks in one VGPR each (bit t: position t is the first / last
+    // position of its sid run); valid positions are exactly t < n after the sort
+    unsigned fb = 0, lb = 0;
+#pragma unroll
+    for (int t = 0; t < G; ++t) {
+      const unsigned s = key[t] >> LOGG;
+      const bool kv = key[t] != kSent32;
+      const bool f = kv && (t == 0 || s != (key[t > 0 ? t - 1 : 0] >> LOGG));
+      const bool l = kv && (t == G - 1 || s != (key[t < G - 1 ? t + 1 : t] >> LOGG));
+      fb |= (f ? 1u : 0u) << t;
+      lb |= (l ? 1u : 0u) << t;
+    }
+    unsigned vb = (n >= 32) ? 0xFFFFFFFFu : ((1u << n) - 1u);  // valid positions
+    // opaque to the optimiser: otherwise it folds the bit tests back into the per-position
+    // compare masks and keeps ~3*G of them alive in SGPRs across the walk (spills)
+    asm volatile("" : "+v"(fb), "+v"(lb), "+v"(vb));
+    // ---- 3. walk: every input of every position in registers before the ordered sums -----
+    wave_sync_lds();  // every lane has read its sids: rows may be rewritten
+    double sp[G];
+#pragma unroll
+    for (int t = 0; t < G; ++t) sp[t] = iP[rsp + (int)(key[t] & (G - 1))];  // sentinel: slot G-1, in the image
+    // gathers: index clamped into the table (sentinels and out-of-range sids never fault;
+    // their values are never used), no per-position branch
+    const unsigned smax = (unsigned)(a.n_sources > 0 ? a.n_sources - 1 : 0);
+    const bool have_tab = a.n_sources > 0;
+    constexpr int NG = (G < RING) ? G : RING;  // gathers in flight
+    double2 ring[NG];
+#pragma unroll
+    for (int t = 0; t < NG; ++t) {
+      const unsigned ix = min(key[t] >> LOGG, smax);
+      ring[t] = (!(BCE_ABLATE & 2) && have_tab) ? a.relconf[ix] : make_double2(0.5, 0.25);
+    }
+    const int dumS = SW - 1, dumP = PW - 1;  // write sinks for invalid positions
+    double total = 0.0, ws = 0.0, cs = 0.0, psum = 0.0;
+    int cnt = 0, j = 0, err = G;
+#pragma unroll
+    for (int t = 0; t < G; ++t) {
+      const bool kv = (vb >> t) & 1u;
+      const unsigned sid = key[t] >> LOGG;
+      const int slot = (int)(key[t] & (G - 1));
+      const bool fst = (fb >> t) & 1u;
+      const bool lst = (lb >> t) & 1u;
+      const double p = sp[t];
+      const double2 rc = ring[t % NG];
+      if (t + NG < G) {
+        const unsigned ix = min(key[t + NG < G ? t + NG : t] >> LOGG, smax);
+        if (!(BCE_ABLATE & 2) && have_tab) ring[t % NG] = a.relconf[ix];
+      }
+      if (kv && (p < 0.0 || p > 1.0)) err = (slot < err) ? slot : err;  // core.py:59-60
+      psum = (fst ? 0.0 : psum) + p;   // builtin sum() from int 0 (core.py:116)
+      cnt = fst ? 1 : cnt + 1;
+      double avg = psum;
+      if (ballot(lst && cnt > 1)) {     // duplicates: sum / len (core.py:116), rare
+        if (lst && cnt > 1) avg = psum / (double)cnt;
+      }
+      const double wt = rc.x, cf = rc.y;
+      // accumulate only at the last position of a run; +0.0 leaves every chain bit-exact
+      // (the chains start at +0.0 and can never become -0.0)
+      total += lst ? wt : 0.0;          // core.py:120
+      ws += lst ? avg * wt : 0.0;       // core.py:135-137
+      cs += lst ? cf * wt : 0.0;        // core.py:141-143
+      // j <= t: the row cell is dead; the slot's probability is already in registers
+      iS[kv ? rsi + j : dumS] = sid | ((unsigned)slot << kPackSlot);
+      iP[kv ? rsp + slot : dumP] = wt;
+      j += lst ? 1 : 0;
+      // pin the chains here: left alone the compiler sinks every add to the end of the
+      // walk and keeps all per-position operands and masks alive
+      asm volatile("" : "+v"(total), "+v"(ws), "+v"(cs), "+v"(psum), "+v"(j), "+v"(cnt), "+v"(err));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+
+    // ---- 4a. per-market results --------------------------------------------------------
+    if (has) {
+      const bool null_ = (total == 0.0);  // core.py:131-133
+      a.consensus[mk] = null_ ? 0.0 : ws / total;
+      a.confidence[mk] = null_ ? 0.0 : cs / total;
+      a.total_weight[mk] = total;
+      a.n_unique[mk] = j;
+      if (a.err_idx) a.err_idx[mk] = (err < G) ? err : -1;
+    }
+    if (lane < TM) {
+      sTot[w][lane] = total;
+      sU[w][lane] = has ? j : 0;
+      sRs[w][lane] = rs;
+    }
+    wave_sync_lds();
+
+    // ---- 4b. per-unique outputs ---------------------------------------------------------
+    if ((a.usid || a.weight || a.nweight) && !(BCE_ABLATE & 8)) {
+      const int dB = (int)(B - Bs), dP = (int)(B - Bp);
+      const bool vec_ok = (((uintptr_t)a.usid & 7) | ((uintptr_t)a.weight & 15) | ((uintptr_t)a.nweight & 15)) == 0;
+      if (vec_ok && ballot(has && (off & 1) != 0) == 0 && (B & 1) == 0) {
+        // even offsets: slot pairs are 8-B (usid) / 16-B (weights) aligned
+        const int k2 = 2 * (lane % P);
+#pragma unroll 1
+        for (int it = 0; it < TM / MPI; ++it) {
+          const int q = it * MPI + lane / P;
+          const int u = sU[w][q];
+          if (k2 < u) {
+            const int r = sRs[w][q];
+            const double tot = sTot[w][q];
+            const int64_t pos = B + r + k2;
+            const bool two = k2 + 1 < u;
+            const unsigned pk0 = iS[dB + r + k2];
+            const unsigned pk1 = two ? iS[dB + r + k2 + 1] : 0u;
+            const unsigned s0 = pk0 & ((1u << kPackSlot) - 1), s1 = pk1 & ((1u << kPackSlot) - 1);
+            const double w0 = iP[dP + r + (int)(pk0 >> kPackSlot)];
+            const double w1 = iP[dP + r + (int)(pk1 >> kPackSlot)];
+            const bool p0 = bits_in_lds ? is_present(sBits, (int)s0) : is_present(a.pbits, (int)s0);
+            const bool p1 = two && (bits_in_lds ? is_present(sBits, (int)s1) : is_present(a.pbits, (int)s1));
+            const unsigned u0 = s0 | (p0 ? 0u : 0x80000000u);  // core.py:167-170
+            const unsigned u1 = s1 | (p1 ? 0u : 0x80000000u);
+            const double n0 = (tot > 0.0) ? w0 / tot : 0.0;    // core.py:151
+            const double n1 = (tot > 0.0) ? w1 / tot : 0.0;
+            if (two) {
+              if (a.usid) *reinterpret_cast<uint2*>(a.usid + pos) = make_uint2(u0, u1);
+              if (a.weight) *reinterpret_cast<double2*>(a.weight + pos) = make_double2(w0, w1);
+              if (a.nweight) *reinterpret_cast<double2*>(a.nweight + pos) = make_double2(n0, n1);
+            } else {
+              if (a.usid) a.usid[pos] = (int32_t)u0;
+              if (a.weight) a.weight[pos] = w0;
+              if (a.nweight) a.nweight[pos] = n0;
+            }
+          }
+        }
+      } else {
+        const int slot = lane % G;
+#pragma unroll 1
+        for (int it = 0; it < TM / (kWave / G); ++it) {
+          const int q = it * (kWave / G) + lane / G;
+          if (slot < sU[w][q]) {
+            const int r = sRs[w][q];
+            const double tot = sTot[w][q];
+            const unsigned pk = iS[dB + r + slot];
+            const unsigned s = pk & ((1u << kPackSlot) - 1);
+            const double wt = iP[dP + r + (int)(pk >> kPackSlot)];
+            const bool pr = bits_in_lds ? is_present(sBits, (int)s) : is_present(a.pbits, (int)s);
+            const int64_t pos = B + r + slot;
+            if (a.usid) a.usid[pos] = (int32_t)(s | (pr ? 0u : 0x80000000u));
+            if (a.weight) a.weight[pos] = wt;
+            if (a.nweight) a.nweight[pos] = (tot > 0.0) ? wt / tot : 0.0;
+          }
+        }
+      }
+    }
+    wave_sync_lds();  // the next tile's DMA overwrites the images
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// consensus_stream_kernel<G, TM, WPB>: the flat kernel with the next tile in flight
+// ------------------------------------------------------------------------------------
+// Same arithmetic as consensus_flat_kernel; the schedule hides the memory latency that
+// bounds the flat kernel at ~5 waves per CU:
+//   * every wave batch-loads the [B, E) bounds of its next 64 tiles once (one vector
+//     load pair), so no per-tile scalar load sits on the critical path;
+//   * the per-market offsets travel with the tile (3 dword LDS-DMA instructions);
+//   * keys and the sorted-slot probabilities are read out of the input image into
+//     registers right after the sort, so the image is dead before the walk's last
+//     relconf gather is issued -- the NEXT tile's LDS-DMA is issued right there.  (VMEM
+//     counters retire in order: a DMA issued before a gather would make that gather's
+//     wait cover the DMA; issued after the last gather it overlaps the rest of the walk
+//     and the copy-out instead.)
+//   * weights stay in registers by sorted position; the per-unique outputs leave through
+//     a small staging area in chunks of CH positions (lane = market writes, lane =
+//     (market, position) stores at offsets[m] + j).
+// Waits the compiler's wait-count pass can see (an asm s_waitcnt is opaque to it, so it
+// would keep treating the previous tile's stores as pending and fall back to vmcnt(0)
+// for every later load).  gfx9 encoding: vmcnt[3:0] expcnt[6:4] lgkmcnt[11:8] vmcnt[15:14].
+__device__ __forceinline__ void wait_vm0() {
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void wait_lgkm0() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  asm volatile("" ::: "memory");
+}
+
+// LDS-DMA issued from inline asm.  The compiler's wait-count pass treats every LDS
+// access after a *builtin* LDS-DMA as a possible alias and drains vmcnt(0) in front of
+// it, which would make the copy-out of tile k wait for the DMA of tile k+1.  The stream
+// kernel orders its images itself (one explicit vmcnt(0) before the image is read; the
+// staging rows are never DMA targets), so the DMA is hidden from that pass.
+__device__ __forceinline__ void dma_b128(const void* g, const void* lds) {
+  const uint32_t l = (uint32_t)(uintptr_t)lds;
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(l), "v"(g) : "memory", "m0");
+}
+__device__ __forceinline__ void dma_b32(const void* g, const void* lds) {
+  const uint32_t l = (uint32_t)(uintptr_t)lds;
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off" ::"s"(l), "v"(g) : "memory", "m0");
+}
+
+template <int G, int TM, int WPB, int CH>
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(BCE_FLAT_WPE, 8)))
+void consensus_stream_kernel(ConsArgs a) {
+  static_assert(G == 8 || G == 16 || G == 32, "stream widths");
+  static_assert(TM == 64, "one market per lane");
+  static_assert(G % CH == 0 && (CH == 2 || CH == 4 || CH == 8), "chunk");
+  constexpr int LOGG = (G == 8) ? 3 : (G == 16) ? 4 : 5;
+  constexpr int TS = TM * G;             // max signals per tile
+  constexpr int SW = TS + 8 + G;         // sid image (dwords): alignment slack + row overrun
+  constexpr int PW = TS + 4 + G;         // prob image (doubles)
+  constexpr int OW = 2 * (TM + 1) + 2;   // offsets block (dwords)
+  constexpr int NG = (G < BCE_FLAT_RING) ? G : BCE_FLAT_RING;  // relconf gathers in flight
+  constexpr int SR = CH + 1;             // staging row stride (16-B entries): conflict-free
+  constexpr int QPR = kWave / CH;        // markets per copy-out round
+  constexpr int NSI = (TS + 8 + 4 * kWave - 1) / (4 * kWave);  // max sid DMA instructions per tile
+  constexpr int NPI = (TS + 4 + 2 * kWave - 1) / (2 * kWave);  // max prob DMA instructions
+
+  __shared__ uint32_t sBits[kBitsLds];
+  __shared__ __attribute__((aligned(16))) uint32_t sSid[WPB][SW];
+  __shared__ __attribute__((aligned(16))) double sProb[WPB][PW];
+  __shared__ __attribute__((aligned(16))) uint32_t sOffs[WPB][OW];
+  __shared__ __attribute__((aligned(16))) uint4 sStage[WPB][TM * SR];
+  __shared__ double sTot[WPB][TM];
+  __shared__ int64_t sMkOff[WPB][TM];
+
+  const int lane = lane_id();
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int nwords = (a.n_sources + 31) >> 5;  // <= kBitsLds (checked by the launcher)
+  for (int i = threadIdx.x; i < nwords; i += 64 * WPB) sBits[i] = a.pbits[i];
+  __syncthreads();  // the only workgroup barrier: waves are independent from here on
+
+  uint32_t* const iS = sSid[w];
+  double* const iP = sProb[w];
+  uint32_t* const iO = sOffs[w];
+  uint4* const stg = sStage[w];
+  const int64_t M = a.n_list;
+  const int64_t n_tiles = (M + TM - 1) / TM;
+  const int64_t t0 = (int64_t)blockIdx.x * WPB + w;
+  const int64_t tstride = (int64_t)gridDim.x * WPB;
+  if (t0 >= n_tiles) return;
+  const unsigned smax = (unsigned)(a.n_sources > 0 ? a.n_sources - 1 : 0);
+  // relconf gathers are unconditional (a branch around a load forces a vmcnt(0) at its
+  // join); with no sources the table is a single cold-start row
+  const double2* const tab = (a.n_sources > 0) ? a.relconf : kColdRow;
+  const int64_t Nf4 = a.n_signals & ~3ll, Nf2 = a.n_signals & ~1ll;
+
+  // bounds of this wave's tiles t0 + i*tstride, i in [base, base + 64): lane i holds them
+  int64_t tbB = 0, tbE = 0;
+  auto load_bounds = [&](int64_t base) {
+    const int64_t tl = t0 + (base + lane) * tstride;
+    if (tl < n_tiles) {
+      const int64_t m0 = tl * TM;
+      tbB = a.offsets[m0];
+      tbE = a.offsets[(m0 + TM < M) ? m0 + TM : M];
+    }
+  };
+  auto bound = [&](int64_t v, int i) -> int64_t {
+    return ((int64_t)__builtin_amdgcn_readlane((int)(v >> 32), i) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)v, i);
+  };
+  // issue the LDS-DMA of one tile into this wave's image (sid, prob, offsets block)
+  auto issue_dma = [&](int64_t tile, int64_t B, int64_t E) {
+    int lane = lane_id();
+    asm volatile("" : "+v"(lane));
+    const int64_t Bs = B & ~3ll, Bp = B & ~1ll;
+    const int64_t es = (E < Nf4) ? ((E + 3) & ~3ll) : Nf4;
+    const int nci = (int)((es - Bs) >> 2);
+#pragma unroll
+    for (int i = 0; i < NSI; ++i) {
+      const int c = i * kWave + lane;
+      if (c < nci)
+        dma_b128(a.sid + Bs + 4 * c, iS + i * 256);
+    }
+    const int64_t ep = (E < Nf2) ? ((E + 1) & ~1ll) : Nf2;
+    const int ncp = (int)((ep - Bp) >> 1);
+#pragma unroll
+    for (int i = 0; i < NPI; ++i) {
+      const int c = i * kWave + lane;
+      if (c < ncp)
+        dma_b128(a.prob + Bp + 2 * c, iP + i * 128);
+    }
+    const int64_t m0 = tile * TM;
+    const int64_t m1 = (m0 + TM < M) ? m0 + TM : M;
+    const int ndw = (int)(2 * (m1 - m0 + 1));  // dwords of offsets[m0 .. m1]
+    const uint32_t* og = reinterpret_cast<const uint32_t*>(a.offsets + m0);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int d = i * kWave + lane;
+      if (d < ndw)
+        dma_b32(og + d, iO + i * 64);
+    }
+  };
+
+  load_bounds(0);
+  int64_t B = bound(tbB, 0), E = bound(tbE, 0);
+  issue_dma(t0, B, E);
+
+  int64_t it = 0;
+  for (int64_t tile = t0; tile < n_tiles; tile += tstride, ++it) {
+    // lane-derived addresses are recomputed per tile (opaque lane id): hoisted out of the
+    // loop they overflow the register budget and spill to scratch, and a scratch reload
+    // after the next tile's DMA would wait for that DMA
+    int lane = lane_id();
+    asm volatile("" : "+v"(lane));
+    const int64_t m0 = tile * TM;
+    const int64_t Bs = B & ~3ll, Bp = B & ~1ll;
+    const int64_t es = (E < Nf4) ? ((E + 3) & ~3ll) : Nf4;
+    const int64_t ep = (E < Nf2) ? ((E + 1) & ~1ll) : Nf2;
+    wait_vm0();
+    if (E > es && lane < (int)(E - es)) iS[es - Bs + lane] = (uint32_t)a.sid[es + lane];
+    if (E > ep && lane < (int)(E - ep)) iP[ep - Bp + lane] = a.prob[ep + lane];
+    wave_sync_lds();
+
+    // ---- this lane's market (offsets block from the image) ------------------------------
+    const int64_t mk = m0 + lane;
+    const bool has = mk < M;
+    int64_t off = B;
+    int n = 0;
+    if (has) {
+      off = ((int64_t)iO[2 * lane + 1] << 32) | iO[2 * lane];
+      n = (int)((((int64_t)iO[2 * lane + 3] << 32) | iO[2 * lane + 2]) - off);
+    }
+    const int rs = (int)(off - B);
+    const int rsi = rs + (int)(B - Bs);
+    const int rsp = rs + (int)(B - Bp);
+
+    // ---- keys + sort ------------------------------------------------------------------------
+    unsigned key[G];
+    if (ballot(has && (rsi & 3) != 0) == 0) {
+#pragma unroll
+      for (int c = 0; c < G / 4; ++c) {
+        const uint4 v = *reinterpret_cast<const uint4*>(iS + rsi + 4 * c);
+        key[4 * c] = v.x; key[4 * c + 1] = v.y; key[4 * c + 2] = v.z; key[4 * c + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < G; ++t) key[t] = iS[rsi + t];
+    }
+#pragma unroll
+    for (int t = 0; t < G; ++t) key[t] = (t < n) ? ((key[t] << LOGG) | (unsigned)t) : kSent32;
+    if constexpr (!(BCE_ABLATE & 1)) oem_sort<G>(key);
+    // built high position first with shift-or: (f ? 1 << t : 0) would put one literal
+    // mask per position in a VGPR of its own
+    unsigned fb = 0, lb = 0;
+#pragma unroll
+    for (int t = G - 1; t >= 0; --t) {
+      const unsigned s = key[t] >> LOGG;
+      const bool kv = key[t] != kSent32;
+      const bool f = kv && (t == 0 || s != (key[t > 0 ? t - 1 : 0] >> LOGG));
+      const bool l = kv && (t == G - 1 || s != (key[t < G - 1 ? t + 1 : t] >> LOGG));
+      fb = (fb << 1) | (f ? 1u : 0u);
+      lb = (lb << 1) | (l ? 1u : 0u);
+    }
+    unsigned vb = (n >= 32) ? 0xFFFFFFFFu : ((1u << n) - 1u);
+    // opaque to the optimiser: otherwise it folds the bit tests back into per-position
+    // compare masks and keeps ~3*G of them alive in SGPRs across the walk (spills)
+    asm volatile("" : "+v"(fb), "+v"(lb), "+v"(vb));
+    double wr[G];  // probabilities of the sorted slots; become the weights in the walk
+#pragma unroll
+    for (int t = 0; t < G; ++t) wr[t] = iP[rsp + (int)(key[t] & (G - 1))];  // sentinel: slot G-1, in the image
+    double2 ring[NG];
+#pragma unroll
+    for (int t = 0; t < NG; ++t) {
+      const unsigned ix = min(key[t] >> LOGG, smax);
+      if constexpr (!(BCE_ABLATE & 2)) ring[t] = tab[ix];
+      else ring[t] = make_double2(0.5, 0.25 + ix);
+    }
+    // the next tile: bounds from the batch, its DMA once every read of this image is done
+    const int64_t ntile = tile + tstride;
+    int64_t Bn = 0, En = 0;
+    if (ntile < n_tiles) {
+      if (((it + 1) & 63) == 0) {  // refresh the bounds batch (every 64 tiles)
+        wait_lgkm0();
+        load_bounds(it + 1);
+      }
+      Bn = bound(tbB, (int)((it + 1) & 63));
+      En = bound(tbE, (int)((it + 1) & 63));
+    }
+    auto next_dma = [&]() {
+      if (ntile < n_tiles) {
+        wait_lgkm0();  // keys / wr reads have landed
+        issue_dma(ntile, Bn, En);
+      }
+    };
+
+    // ---- walk (core.py:107-144 in sorted-source order) ---------------------------------------
+    double total = 0.0, ws = 0.0, cs = 0.0, psum = 0.0;
+    int cnt = 0, err = G;
+#pragma unroll
+    for (int t = 0; t < G; ++t) {
+      // bit tests as v_bfe with inline constants (a literal mask per position gets
+      // hoisted into a VGPR of its own: 3*G registers)
+      const bool kv = __builtin_amdgcn_ubfe(vb, t, 1) != 0u;
+      const int slot = (int)(key[t] & (G - 1));
+      const bool fst = __builtin_amdgcn_ubfe(fb, t, 1) != 0u;
+      const bool lst = __builtin_amdgcn_ubfe(lb, t, 1) != 0u;
+      const double p = wr[t];
+      const double2 rc = ring[t % NG];
+      if (t + NG < G) {
+        const unsigned ix = min(key[t + NG < G ? t + NG : t] >> LOGG, smax);
+        if constexpr (!(BCE_ABLATE & 2)) ring[t % NG] = tab[ix];
+      }
+      if (kv && (p < 0.0 || p > 1.0)) err = (slot < err) ? slot : err;  // core.py:59-60
+      psum = (fst ? 0.0 : psum) + p;   // builtin sum() from int 0 (core.py:116)
+      cnt = fst ? 1 : cnt + 1;
+      double avg = psum;
+      if (ballot(lst && cnt > 1)) {     // duplicates: sum / len (core.py:116), rare
+        if (lst && cnt > 1) avg = psum / (double)cnt;
+      }
+      const double wt = rc.x, cf = rc.y;
+      // accumulate only at the last position of a run; +0.0 leaves every chain bit-exact
+      // (the chains start at +0.0 and can never become -0.0)
+      total += lst ? wt : 0.0;          // core.py:120
+      ws += lst ? avg * wt : 0.0;       // core.py:135-137
+      cs += lst ? cf * wt : 0.0;        // core.py:141-143
+      wr[t] = wt;
+      // pin the chains here: left alone the compiler sinks every add to the end of the
+      // walk and keeps all per-position operands and masks alive
+      asm volatile("" : "+v"(total), "+v"(ws), "+v"(cs), "+v"(psum), "+v"(cnt), "+v"(err));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // every gather of this tile has been consumed: the next tile's DMA now overlaps the
+    // per-market stores and the copy-out without any later wait covering it
+    next_dma();
+    const int u = __builtin_popcount(lb);
+
+    // ---- per-market results ---------------------------------------------------------------
+    if (has) {
+      const bool null_ = (total == 0.0);  // core.py:131-133
+      a.consensus[mk] = null_ ? 0.0 : ws / total;
+      a.confidence[mk] = null_ ? 0.0 : cs / total;
+      a.total_weight[mk] = total;
+      a.n_unique[mk] = u;
+      if (a.err_idx) a.err_idx[mk] = (err < G) ? err : -1;
+    }
+
+    // ---- per-unique outputs: CH sorted positions per chunk through the staging rows -----
+    if ((a.usid || a.weight || a.nweight) && !(BCE_ABLATE & 8)) {
+      sTot[w][lane] = total;
+      sMkOff[w][lane] = off;
+#pragma unroll
+      for (int c = 0; c < G / CH; ++c) {
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+          const int t = c * CH + i;
+          const unsigned sid = key[t] >> LOGG;
+          const bool lst = __builtin_amdgcn_ubfe(lb, t, 1) != 0u;
+          const int j = lst ? __builtin_popcount(__builtin_amdgcn_ubfe(lb, 0, t)) : -1;
+          const unsigned ps = min(sid, smax);
+          const bool pr = is_present(sBits, (int)ps);  // host: S <= 32 * kBitsLds
+          const unsigned us = sid | (pr ? 0u : 0x80000000u);  // core.py:167-170
+          const uint2 wb = *reinterpret_cast<const uint2*>(&wr[t]);
+          stg[lane * SR + i] = make_uint4(us, (unsigned)j, wb.x, wb.y);
+        }
+        wave_sync_lds();
+#pragma unroll
+        for (int r = 0; r < CH; ++r) {
+          const int q = r * QPR + lane / CH;
+          const int i = lane % CH;
+          const uint4 e = stg[q * SR + i];
+          const int j = (int)e.y;
+          if (j >= 0) {
+            const int64_t pos = sMkOff[w][q] + j;
+            const double tot = sTot[w][q];
+            const double wt = __hiloint2double((int)e.w, (int)e.z);
+            if (a.usid) a.usid[pos] = (int32_t)e.x;
+            if (a.weight) a.weight[pos] = wt;
+            if (a.nweight) a.nweight[pos] = (tot > 0.0) ? wt / tot : 0.0;  // core.py:151
+          }
+        }
+        wave_sync_lds();
+      }
+    }
+    B = Bn;
+    E = En;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// consensus_pipe_kernel<G, C, R>: one loader wave + C compute waves per workgroup
+// ------------------------------------------------------------------------------------
+// The headline schedule.  Per workgroup (one per CU) an LDS ring of R tile slots:
+//   loader wave   streams tile after tile into free slots with LDS-DMA, a FIXED number
+//                 of 16-B wave-instructions per tile (lanes past the tile's range re-read
+//                 its first chunk into the slot's slack), so `s_waitcnt vmcnt(NDMA)`
+//                 publishes tile i-1 while tile i is still in flight (two tiles deep);
+//   compute waves grab tiles in sequence (LDS counter), wait for the slot's ready flag,
+//                 and run the flat kernel's arithmetic on it: keys + odd-even merge sort
+//                 in VGPRs, the walk with 16 relconf gathers in flight and the sorted-slot
+//                 probabilities read from the slot just ahead of use, per-unique results
+//                 staged in place (packed sid|slot over the dead sid row, the weight over
+//                 the consumed probability cell), coalesced copy-out with 16-B pairs, then
+//                 release the slot.
+// A compute wave never issues an LDS-DMA, so none of its waits covers one; the loader
+// never touches registers the compute waves need.  Flags live in LDS (one workgroup).
+// Progress: the loader only waits for the release of sequence i-R, which a compute wave
+// is processing or has released (sequences are grabbed in order and R > C).
+constexpr int kSpinCap = 1 << 22;  // ~0.1-0.3 s of s_sleep polling per wait
+
+// Acquire-load of an LDS flag, broadcast to a wave-uniform (SGPR) value: every spin and
+// branch on a flag is then scalar control flow (a per-lane view of the same word makes
+// the compiler build divergent loop exits around it).
+__device__ __forceinline__ int ldsflag(int* f) {
+  const int v = __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  return __builtin_amdgcn_readfirstlane(v);
+}
+
+template <int G>
+struct PipeCfg {
+  static constexpr int C = 4;   // compute waves
+  static constexpr int R = 5;   // slots
+};
+
+template <int G>
+__global__ __launch_bounds__(64 * (PipeCfg<G>::C + 1))
+void consensus_pipe_kernel(ConsArgs a) {
+  static_assert(G == 8 || G == 16 || G == 32, "pipe widths");
+  constexpr int C = PipeCfg<G>::C, R = PipeCfg<G>::R;
+  constexpr int TM = kWave;
+  constexpr int LOGG = (G == 8) ? 3 : (G == 16) ? 4 : 5;
+  constexpr int TS = TM * G;
+  constexpr int NSI = (TS + 8 + 4 * kWave - 1) / (4 * kWave);  // sid DMA instructions per tile
+  constexpr int NPI = (TS + 4 + 2 * kWave - 1) / (2 * kWave);  // prob DMA instructions
+  constexpr int NOI = 3;                                       // offsets block (dwords)
+  constexpr int NDMA = NSI + NPI + NOI;
+  static_assert(NDMA < 64, "vmcnt field");
+  constexpr int SW = NSI * 256;  // sid image dwords (every DMA lane lands inside)
+  constexpr int PW = NPI * 128;  // prob image doubles
+  constexpr int OW = NOI * 64;   // offsets block dwords
+  static_assert(SW >= TS + 8 + G && PW >= TS + 4 + G && OW >= 2 * (TM + 1), "slot sizes");
+  constexpr int RING = 16;
+  constexpr int NG = (G < RING) ? G : RING;
+  constexpr int PA = 4;          // probabilities read this many positions ahead
+  constexpr int P2 = G / 2;      // copy-out lanes per market (two slots per lane)
+  constexpr int MPI = kWave / P2;
+
+  __shared__ uint32_t sBits[kBitsLds];
+  __shared__ __attribute__((aligned(16))) uint32_t sSid[R][SW];
+  __shared__ __attribute__((aligned(16))) double sProb[R][PW];
+  __shared__ __attribute__((aligned(16))) uint32_t sOffs[R][OW];
+  __shared__ int64_t sTile[R];
+  __shared__ int sReady[R];  // sequence + 1 once the slot holds it
+  __shared__ int sFree[R];   // sequence + 1 once the slot's tile has been released
+  __shared__ int sNext;
+  __shared__ double sTot[C][TM];
+  __shared__ int32_t sU[C][TM];
+  __shared__ int32_t sRs[C][TM];
+
+  const int lane = lane_id();
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int nwords = (a.n_sources + 31) >> 5;  // <= kBitsLds (launcher)
+  for (int i = threadIdx.x; i < nwords; i += 64 * (C + 1)) sBits[i] = a.pbits[i];
+  if (threadIdx.x < R) {
+    sReady[threadIdx.x] = 0;
+    sFree[threadIdx.x] = 0;
+  }
+  if (threadIdx.x == 0) sNext = 0;
+  __syncthreads();  // the only workgroup barrier
+
+  const int64_t M = a.n_list;
+  const int64_t n_tiles = (M + TM - 1) / TM;
+
+  if (w == 0) {
+    // ================================ loader ==========================================
+    const int64_t Nf4 = a.n_signals & ~3ll, Nf2 = a.n_signals & ~1ll;
+    const int64_t clamp_s = (Nf4 - 4 > 0) ? Nf4 - 4 : 0;  // host: n_signals >= 4
+    const int64_t clamp_p = (Nf2 - 2 > 0) ? Nf2 - 2 : 0;
+    int64_t tbB = 0, tbE = 0;
+    auto load_bounds = [&](int64_t base) {
+      const int64_t t = (int64_t)blockIdx.x + (base + lane) * gridDim.x;
+      if (t < n_tiles) {
+        const int64_t m0 = t * TM;
+        tbB = a.offsets[m0];
+        tbE = a.offsets[(m0 + TM < M) ? m0 + TM : M];
+      }
+    };
+    auto rl = [&](int64_t v, int i) -> int64_t {
+      return ((int64_t)__builtin_amdgcn_readlane((int)(v >> 32), i) << 32) |
+             (uint32_t)__builtin_amdgcn_readlane((int)v, i);
+    };
+    auto publish = [&](int seq, int64_t t) {
+      const int s = seq % R;
+#if BCE_PIPE_DBG
+      if (lane == 0 && blockIdx.x == 0) printf("[L] publish seq %d tile %ld slot %d\n", seq, (long)t, s);
+#endif
+      // every lane stores the same words: no lane-0-only region inside the loop (the
+      // structurizer splits loops around such regions and breaks wave-uniform state)
+      sTile[s] = t;
+      __hip_atomic_store(&sReady[s], seq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    const int64_t my_tiles = (n_tiles > (int64_t)blockIdx.x) ? (n_tiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+    int pending = -1;  // sequence whose DMA is in flight and not yet published
+    int64_t pend_t = -1;
+    for (int64_t i = 0; i < my_tiles + C; ++i) {
+      const int s = (int)(i % R);
+#if BCE_PIPE_DBG
+      if (lane == 0 && blockIdx.x == 0) printf("[L] i %ld / %ld\n", (long)i, (long)(my_tiles + C));
+#endif
+      // wait for the release of sequence i - R (publish what is in flight first)
+      if (i >= R) {
+        const int need = (int)(i - R) + 1;
+        if (ldsflag(&sFree[s]) < need) {
+          if (pending >= 0) {
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+            publish(pending, pend_t);
+            pending = -1;
+          }
+          int spins = 0;
+          while (ldsflag(&sFree[s]) < need) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > kSpinCap) return;  // never expected; bounded so a bug cannot hang the GPU
+          }
+        }
+      }
+      if (i >= my_tiles) {  // end markers: one per compute wave
+        if (pending >= 0) {
+          __builtin_amdgcn_s_waitcnt(0x0F70);
+          publish(pending, pend_t);
+          pending = -1;
+        }
+        publish((int)i, -1);
+        continue;
+      }
+      if ((i & 63) == 0) {
+        load_bounds(i);
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // (drains in-flight DMA too; once per 64 tiles)
+        if (pending >= 0) {
+          publish(pending, pend_t);
+          pending = -1;
+        }
+      }
+      const int64_t t = (int64_t)blockIdx.x + i * gridDim.x;
+      const int64_t B = rl(tbB, (int)(i & 63)), E = rl(tbE, (int)(i & 63));
+      const int64_t m0 = t * TM, m1 = (m0 + TM < M) ? m0 + TM : M;
+      const int64_t Bs = B & ~3ll, Bp = B & ~1ll;
+      const int64_t es = (E < Nf4) ? ((E + 3) & ~3ll) : Nf4;
+      const int64_t ep = (E < Nf2) ? ((E + 1) & ~1ll) : Nf2;
+      const int nci = (int)((es - Bs) >> 2), ncp = (int)((ep - Bp) >> 1);
+      const int ndw = (int)(2 * (m1 - m0 + 1));
+      const int64_t fs = (Bs < clamp_s) ? Bs : clamp_s, fp = (Bp < clamp_p) ? Bp : clamp_p;
+#pragma unroll
+      for (int k = 0; k < NSI; ++k) {
+        const int c = k * kWave + lane;
+        dma_b128(a.sid + ((c < nci) ? Bs + 4 * c : fs), &sSid[s][k * 256]);
+      }
+#pragma unroll
+      for (int k = 0; k < NPI; ++k) {
+        const int c = k * kWave + lane;
+        dma_b128(a.prob + ((c < ncp) ? Bp + 2 * c : fp), &sProb[s][k * 128]);
+      }
+      const uint32_t* og = reinterpret_cast<const uint32_t*>(a.offsets + m0);
+#pragma unroll
+      for (int k = 0; k < NOI; ++k) {
+        const int d = k * kWave + lane;
+        dma_b32(og + ((d < ndw) ? d : 0), &sOffs[s][k * 64]);
+      }
+      if (pending >= 0) {  // the previous tile has landed once only this one is in flight
+        __builtin_amdgcn_s_waitcnt((NDMA & 15) | (7 << 4) | (15 << 8) | ((NDMA >> 4) << 14));
+        publish(pending, pend_t);
+      }
+      pending = (int)i;
+      pend_t = t;
+    }
+    if (pending >= 0) {
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+      publish(pending, pend_t);
+    }
+    return;
+  }
+
+  // ================================ compute waves =====================================
+  const int cw = w - 1;
+  const unsigned smax = (unsigned)(a.n_sources > 0 ? a.n_sources - 1 : 0);
+  const double2* const tab = (a.n_sources > 0) ? a.relconf : kColdRow;
+  const int64_t Nf4 = a.n_signals & ~3ll, Nf2 = a.n_signals & ~1ll;
+  for (;;) {
+    // every lane takes a ticket (one aggregated ds_add of 64 per wave): the wave's
+    // sequence number is its first ticket / 64
+    const int tk = __hip_atomic_fetch_add(&sNext, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const int seq = __builtin_amdgcn_readfirstlane(tk) >> 6;
+    const int s = seq % R;
+#if BCE_PIPE_DBG
+    if (lane == 0 && blockIdx.x == 0) printf("[C%d] grab seq %d\n", w, seq);
+#endif
+    int spins = 0;
+    while (ldsflag(&sReady[s]) != seq + 1) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > kSpinCap) return;  // never expected; bounded so a bug cannot hang the GPU
+    }
+    const int64_t tile0 = sTile[s];
+    const int64_t tile = ((int64_t)__builtin_amdgcn_readfirstlane((int)(tile0 >> 32)) << 32) |
+                         (uint32_t)__builtin_amdgcn_readfirstlane((int)tile0);  // uniform
+#if BCE_PIPE_DBG
+    if (lane == 0 && blockIdx.x == 0) printf("[C%d] seq %d ready, tile %ld\n", w, seq, (long)tile);
+#endif
+    if (tile < 0) {
+      __hip_atomic_store(&sFree[s], seq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      break;
+    }
+    uint32_t* const iS = sSid[s];
+    double* const iP = sProb[s];
+    const uint32_t* const iO = sOffs[s];
+    int ln = lane_id();
+    asm volatile("" : "+v"(ln));  // per-tile addresses (no loop-invariant hoisting)
+    const int64_t m0 = tile * TM;
+    const int64_t B = ((int64_t)iO[1] << 32) | iO[0];
+    const int64_t mlast = ((m0 + TM < M) ? m0 + TM : M) - m0;
+    const int64_t E = ((int64_t)iO[2 * mlast + 1] << 32) | iO[2 * mlast];
+    const int64_t Bs = B & ~3ll, Bp = B & ~1ll;
+    const int64_t es = (E < Nf4) ? ((E + 3) & ~3ll) : Nf4;
+    const int64_t ep = (E < Nf2) ? ((E + 1) & ~1ll) : Nf2;
+    if (E > es && ln < (int)(E - es)) iS[es - Bs + ln] = (uint32_t)a.sid[es + ln];
+    if (E > ep && ln < (int)(E - ep)) iP[ep - Bp + ln] = a.prob[ep + ln];
+    wave_sync_lds();
+
+    const int64_t mk = m0 + ln;
+    const bool has = mk < M;
+    int64_t off = B;
+    int n = 0;
+    if (has) {
+      off = ((int64_t)iO[2 * ln + 1] << 32) | iO[2 * ln];
+      n = (int)((((int64_t)iO[2 * ln + 3] << 32) | iO[2 * ln + 2]) - off);
+    }
+    const int rs = (int)(off - B);
+    const int rsi = rs + (int)(B - Bs);
+    const int rsp = rs + (int)(B - Bp);
+
+    // ---- keys + sort ---------------------------------------------------------------------
+    unsigned key[G];
+    if (ballot(has && (rsi & 3) != 0) == 0) {
+#pragma unroll
+      for (int c = 0; c < G / 4; ++c) {
+        const uint4 v = *reinterpret_cast<const uint4*>(iS + rsi + 4 * c);
+        key[4 * c] = v.x; key[4 * c + 1] = v.y; key[4 * c + 2] = v.z; key[4 * c + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < G; ++t) key[t] = iS[rsi + t];
+    }
+#pragma unroll
+    for (int t = 0; t < G; ++t) key[t] = (t < n) ? ((key[t] << LOGG) | (unsigned)t) : kSent32;
+    if constexpr (!(BCE_ABLATE & 1)) oem_sort<G>(key);
+    unsigned fb = 0, lb = 0;
+#pragma unroll
+    for (int t = G - 1; t >= 0; --t) {
+      const unsigned sd = key[t] >> LOGG;
+      const bool kv = key[t] != kSent32;
+      const bool f = kv && (t == 0 || sd != (key[t > 0 ? t - 1 : 0] >> LOGG));
+      const bool l = kv && (t == G - 1 || sd != (key[t < G - 1 ? t + 1 : t] >> LOGG));
+      fb = (fb << 1) | (f ? 1u : 0u);
+      lb = (lb << 1) | (l ? 1u : 0u);
+    }
+    unsigned vb = (n >= 32) ? 0xFFFFFFFFu : ((1u << n) - 1u);
+    asm volatile("" : "+v"(fb), "+v"(lb), "+v"(vb));
+    wave_sync_lds();  // every lane has its sids: rows become usid staging
+
+    double2 ring[NG];
+#pragma unroll
+    for (int t = 0; t < NG; ++t) {
+      const unsigned ix = min(key[t] >> LOGG, smax);
+      if constexpr (!(BCE_ABLATE & 2)) ring[t] = tab[ix];
+      else ring[t] = make_double2(0.5, 0.25 + ix);
+    }
+    double pq[PA];
+#pragma unroll
+    for (int t = 0; t < PA; ++t) pq[t] = iP[rsp + (int)(key[t] & (G - 1))];
+
+    // ---- walk (core.py:107-144 in sorted-source order) ----------------------------------
+    double total = 0.0, ws = 0.0, cs = 0.0, psum = 0.0;
+    int cnt = 0, err = G, j = 0;
+#pragma unroll
+    for (int t = 0; t < G; ++t) {
+      const bool kv = __builtin_amdgcn_ubfe(vb, t, 1) != 0u;
+      const unsigned sid = key[t] >> LOGG;
+      const int slot = (int)(key[t] & (G - 1));
+      const bool fst = __builtin_amdgcn_ubfe(fb, t, 1) != 0u;
+      const bool lst = __builtin_amdgcn_ubfe(lb, t, 1) != 0u;
+      const double p = pq[t % PA];
+      if (t + PA < G) pq[t % PA] = iP[rsp + (int)(key[t + PA < G ? t + PA : t] & (G - 1))];
+      const double2 rc = ring[t % NG];
+      if (t + NG < G) {
+        const unsigned ix = min(key[t + NG < G ? t + NG : t] >> LOGG, smax);
+        if constexpr (!(BCE_ABLATE & 2)) ring[t % NG] = tab[ix];
+      }
+      if (kv && (p < 0.0 || p > 1.0)) err = (slot < err) ? slot : err;  // core.py:59-60
+      psum = (fst ? 0.0 : psum) + p;   // builtin sum() from int 0 (core.py:116)
+      cnt = fst ? 1 : cnt + 1;
+      double avg = psum;
+      if (ballot(lst && cnt > 1)) {     // duplicates: sum / len (core.py:116), rare
+        if (lst && cnt > 1) avg = psum / (double)cnt;
+      }
+      const double wt = rc.x, cf = rc.y;
+      total += lst ? wt : 0.0;          // core.py:120
+      ws += lst ? avg * wt : 0.0;       // core.py:135-137
+      cs += lst ? cf * wt : 0.0;        // core.py:141-143
+      if (kv) {  // j <= t: the row cell is dead; the slot's probability has been read
+        iS[rsi + j] = sid | ((unsigned)slot << kPackSlot);
+        iP[rsp + slot] = wt;
+      }
+      j += lst ? 1 : 0;
+      asm volatile("" : "+v"(total), "+v"(ws), "+v"(cs), "+v"(psum), "+v"(cnt), "+v"(err), "+v"(j));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+
+    // ---- per-market results --------------------------------------------------------------
+    if (has) {
+      const bool null_ = (total == 0.0);  // core.py:131-133
+      a.consensus[mk] = null_ ? 0.0 : ws / total;
+      a.confidence[mk] = null_ ? 0.0 : cs / total;
+      a.total_weight[mk] = total;
+      a.n_unique[mk] = j;
+      if (a.err_idx) a.err_idx[mk] = (err < G) ? err : -1;
+    }
+    sTot[cw][ln] = total;
+    sU[cw][ln] = has ? j : 0;
+    sRs[cw][ln] = rs;
+    wave_sync_lds();
+
+    // ---- per-unique outputs from the in-place staging ------------------------------------
+    if ((a.usid || a.weight || a.nweight) && !(BCE_ABLATE & 8)) {
+      const int dB = (int)(B - Bs), dP = (int)(B - Bp);
+      const bool vec_ok = (((uintptr_t)a.usid & 7) | ((uintptr_t)a.weight & 15) | ((uintptr_t)a.nweight & 15)) == 0;
+      if (vec_ok && ballot(has && (off & 1) != 0) == 0 && (B & 1) == 0) {
+        const int k2 = 2 * (ln % P2);
+#pragma unroll 2
+        for (int it = 0; it < TM / MPI; ++it) {
+          const int q = it * MPI + ln / P2;
+          const int u = sU[cw][q];
+          if (k2 < u) {
+            const int r = sRs[cw][q];
+            const double tot = sTot[cw][q];
+            const int64_t pos = B + r + k2;
+            const bool two = k2 + 1 < u;
+            const uint2 pk = *reinterpret_cast<const uint2*>(iS + dB + r + k2);  // (rs + dB) even
+            const unsigned s0 = pk.x & ((1u << kPackSlot) - 1), s1 = pk.y & ((1u << kPackSlot) - 1);
+            const double w0 = iP[dP + r + (int)(pk.x >> kPackSlot)];
+            const double w1 = two ? iP[dP + r + (int)(pk.y >> kPackSlot)] : 0.0;
+            const bool p0 = is_present(sBits, (int)min(s0, smax));
+            const bool p1 = is_present(sBits, (int)min(s1, smax));
+            const unsigned u0 = s0 | (p0 ? 0u : 0x80000000u);  // core.py:167-170
+            const unsigned u1 = s1 | (p1 ? 0u : 0x80000000u);
+            const double n0 = (tot > 0.0) ? w0 / tot : 0.0;    // core.py:151
+            const double n1 = (tot > 0.0) ? w1 / tot : 0.0;
+            if (two) {
+              if (a.usid) *reinterpret_cast<uint2*>(a.usid + pos) = make_uint2(u0, u1);
+              if (a.weight) *reinterpret_cast<double2*>(a.weight + pos) = make_double2(w0, w1);
+              if (a.nweight) *reinterpret_cast<double2*>(a.nweight + pos) = make_double2(n0, n1);
+            } else {
+              if (a.usid) a.usid[pos] = (int32_t)u0;
+              if (a.weight) a.weight[pos] = w0;
+              if (a.nweight) a.nweight[pos] = n0;
+            }
+          }
+        }
+      } else {
+        const int sl = ln % G;
+#pragma unroll 1
+        for (int it = 0; it < TM / (kWave / G); ++it) {
+          const int q = it * (kWave / G) + ln / G;
+          if (sl < sU[cw][q]) {
+            const int r = sRs[cw][q];
+            const double tot = sTot[cw][q];
+            const unsigned pk = iS[dB + r + sl];
+            const unsigned s0 = pk & ((1u << kPackSlot) - 1);
+            const double wt = iP[dP + r + (int)(pk >> kPackSlot)];
+            const bool pr = is_present(sBits, (int)min(s0, smax));
+            const int64_t pos = B + r + sl;
+            if (a.usid) a.usid[pos] = (int32_t)(s0 | (pr ? 0u : 0x80000000u));
+            if (a.weight) a.weight[pos] = wt;
+            if (a.nweight) a.nweight[pos] = (tot > 0.0) ? wt / tot : 0.0;
+          }
+        }
+      }
+    }
+    wave_sync_lds();  // every read of the slot has returned
+#if BCE_PIPE_DBG
+    if (lane == 0 && blockIdx.x == 0) printf("[C%d] seq %d done\n", w, seq);
+#endif
+    __hip_atomic_store(&sFree[s], seq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
 }
 
@@ -876,7 +1901,90 @@ int launch_lpm(const ConsArgs& a, hipStream_t st) {
   return check_launch("consensus_lpm_kernel");
 }
 
+template <int G>
+int launch_pipe(const ConsArgs& a, hipStream_t st) {
+  constexpr int TM = 64;
+  const int64_t tiles = (a.n_list + TM - 1) / TM;
+  if (tiles == 0) return BCE_OK;
+  static int per_cu = 0;
+  if (!per_cu) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, consensus_pipe_kernel<G>, 64 * (PipeCfg<G>::C + 1), 0) !=
+            hipSuccess || nb <= 0)
+      nb = 1;
+    per_cu = nb;
+    if (getenv("BCE_DEBUG_LAUNCH"))
+      fprintf(stderr, "[bce] consensus_pipe_kernel<%d>: %d blocks/CU x %d CUs\n", G, nb, cu_count());
+  }
+  const int64_t cap = (int64_t)cu_count() * per_cu;
+  const int grid = (int)(tiles < cap ? tiles : cap);
+  hipLaunchKernelGGL((consensus_pipe_kernel<G>), dim3(grid), dim3(64 * (PipeCfg<G>::C + 1)), 0, st, a);
+  return check_launch("consensus_pipe_kernel");
+}
+
+template <int G>
+int launch_stream(const ConsArgs& a, hipStream_t st) {
+  constexpr int TM = 64, WPB = BCE_STREAM_WPB, CH = (G < BCE_STREAM_CH) ? G : BCE_STREAM_CH;
+  const int64_t tiles = (a.n_list + TM - 1) / TM;
+  if (tiles == 0) return BCE_OK;
+  static int per_cu = 0;
+  if (!per_cu) {
+    int nb = 0;
+    if (BCE_SEG_GRID_PER_CU > 0) nb = BCE_SEG_GRID_PER_CU;
+    else if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, consensus_stream_kernel<G, TM, WPB, CH>, 64 * WPB, 0) !=
+                 hipSuccess || nb <= 0)
+      nb = 1;
+    per_cu = nb;
+    if (getenv("BCE_DEBUG_LAUNCH"))
+      fprintf(stderr, "[bce] consensus_stream_kernel<%d,%d,%d,%d>: %d blocks/CU x %d CUs\n", G, TM, WPB, CH, nb,
+              cu_count());
+  }
+  const int64_t blocks = (tiles + WPB - 1) / WPB;
+  const int64_t cap = (int64_t)cu_count() * per_cu;
+  const int grid = (int)(blocks < cap ? blocks : cap);
+  hipLaunchKernelGGL((consensus_stream_kernel<G, TM, WPB, CH>), dim3(grid), dim3(64 * WPB), 0, st, a);
+  return check_launch("consensus_stream_kernel");
+}
+
+template <int G>
+int launch_flat(const ConsArgs& a, hipStream_t st) {
+  constexpr int TM = BCE_FLAT_TM, WPB = BCE_FLAT_WPB;
+  const int64_t tiles = (a.n_list + TM - 1) / TM;
+  if (tiles == 0) return BCE_OK;
+  static int per_cu = 0;
+  if (!per_cu) {
+    int nb = 0;
+    if (BCE_SEG_GRID_PER_CU > 0) nb = BCE_SEG_GRID_PER_CU;
+    else if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, consensus_flat_kernel<G, TM, WPB>, 64 * WPB, 0) !=
+                 hipSuccess || nb <= 0)
+      nb = 2;
+    per_cu = nb;
+    if (getenv("BCE_DEBUG_LAUNCH"))
+      fprintf(stderr, "[bce] consensus_flat_kernel<%d,%d,%d>: %d blocks/CU x %d CUs\n", G, TM, WPB, nb, cu_count());
+  }
+  const int64_t blocks = (tiles + WPB - 1) / WPB;
+  const int64_t cap = (int64_t)cu_count() * per_cu;
+  const int grid = (int)(blocks < cap ? blocks : cap);
+  hipLaunchKernelGGL((consensus_flat_kernel<G, TM, WPB>), dim3(grid), dim3(64 * WPB), 0, st, a);
+  return check_launch("consensus_flat_kernel");
+}
+
 int launch_seg_for_len(int max_len, const ConsArgs& a, hipStream_t st) {
+  if (BCE_FLAT == 3 && a.list == nullptr && max_len <= 32 && a.n_sources <= 32 * kBitsLds && a.n_signals >= 4) {
+    if (max_len <= 8) return launch_pipe<8>(a, st);
+    if (max_len <= 16) return launch_pipe<16>(a, st);
+    return launch_pipe<32>(a, st);
+  }
+  if (BCE_FLAT == 2 && a.list == nullptr && max_len <= 32 && a.n_sources <= 32 * kBitsLds) {
+    if (max_len <= 8) return launch_stream<8>(a, st);
+    if (max_len <= 16) return launch_stream<16>(a, st);
+    return launch_stream<32>(a, st);
+  }
+  if (BCE_FLAT && a.list == nullptr && max_len <= 32 && a.n_sources <= (1 << kPackSlot)) {
+    if (max_len <= 8) return launch_flat<8>(a, st);
+    if (max_len <= 16) return launch_flat<16>(a, st);
+    return launch_flat<32>(a, st);
+  }
   if (BCE_USE_LPM) {
     if (max_len <= 8) return launch_lpm<8>(a, st);
     if (max_len <= 16) return launch_lpm<16>(a, st);

@@ -118,3 +118,59 @@ def test_single_market_cases(case):
     g = dict(offsets=offsets, sid=sid, prob=prob, rel=rel, conf=conf, present=present)
     exp = orc.consensus_csr(offsets, sid, prob, rel, conf, present)
     _compare(_run(g), exp, offsets)
+
+
+def _compare_vec(out, exp, offsets):
+    """Vectorised bit-exact comparison (large M): per-unique slots j < n_unique only."""
+    for k in ("n_unique", "err_idx"):
+        assert np.array_equal(out[k], exp[k]), k
+    for k in ("consensus", "confidence", "total_weight"):
+        assert np.array_equal(out[k], exp[k], equal_nan=True), k
+    M = len(offsets) - 1
+    u = exp["n_unique"].astype(np.int64)
+    pos = np.repeat(offsets[:-1], u) + (np.arange(int(u.sum())) - np.repeat(np.cumsum(u) - u, u))
+    for k in ("usid", "weight", "nweight"):
+        assert np.array_equal(out[k][pos], exp[k][pos], equal_nan=True), k
+    assert M == len(u)
+
+
+def test_stream_kernel_many_tiles_per_wave():
+    """> 64 tiles per wave: exercises the streamed kernel's bounds-batch refresh."""
+    rng = np.random.default_rng(11)
+    M, S = 6_000_000, 1000
+    lens = rng.integers(0, 3, M)
+    off = np.zeros(M + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    n = int(off[-1])
+    sid = rng.integers(0, S, n).astype(np.int32)
+    prob = rng.random(n)
+    rel, conf = rng.uniform(0, 1, S), rng.random(S)
+    present = (rng.random(S) < 0.8).astype(np.uint8)
+    g = dict(offsets=off, sid=sid, prob=prob, rel=rel, conf=conf, present=present)
+    exp = orc.consensus_csr(off, sid, prob, rel, conf, present)
+    _compare_vec(_run(g, max_len=2), exp, off)
+
+
+@pytest.mark.parametrize("maxlen,S,M,seed", [(32, 10000, 20000, 1), (32, 7, 3000, 2), (16, 500, 9000, 3),
+                                             (8, 20000, 5000, 4), (31, 100, 4000, 5), (3, 3, 7000, 6)])
+def test_short_ragged_unaligned(maxlen, S, M, seed):
+    """Ragged lengths 0..maxlen (odd offsets, empty markets, duplicates) on the contiguous
+    short-market path, with an offset view (offsets[0] != 0) like a shard."""
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, maxlen + 1, M)
+    lens[rng.random(M) < 0.05] = 0
+    base = 13
+    off = np.zeros(M + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    off += base
+    n = int(off[-1])
+    sid = rng.integers(0, S, n).astype(np.int32)
+    prob = rng.random(n)
+    prob[rng.random(n) < 0.02] = -0.5
+    prob[rng.random(n) < 0.01] = np.nan
+    rel, conf = rng.uniform(-0.2, 1, S), rng.random(S)
+    rel[rng.random(S) < 0.05] = 0.0
+    present = (rng.random(S) < 0.7).astype(np.uint8)
+    g = dict(offsets=off, sid=sid, prob=prob, rel=rel, conf=conf, present=present)
+    exp = orc.consensus_csr(off, sid, prob, rel, conf, present)
+    _compare_vec(_run(g, max_len=maxlen), exp, off)

@@ -19,14 +19,16 @@ CSRC = os.path.join(ROOT, "bayesian-consensus-engine_amd", "csrc")
 OUT = os.path.join(ROOT, "tools", "ablate_build")
 
 VARIANTS = {
-    "lpm": [],
-    "coop_tm8": ["-DBCE_USE_LPM=0"],
-    "lpm_noout": ["-DBCE_ABLATE=8"],
-    "lpm_nogather": ["-DBCE_ABLATE=2"],
-    "lpm_nosort": ["-DBCE_ABLATE=1"],
-    "lpm_all": ["-DBCE_ABLATE=11"],
+    "pipe": [],
+    "stream": ["-DBCE_FLAT=2"],
+    "flat_wpb1": ["-DBCE_FLAT=1", "-DBCE_FLAT_WPB=1"],
+    "lpm": ["-DBCE_FLAT=0"],
+    "pipe_noout": ["-DBCE_ABLATE=8"],
+    "pipe_nogather": ["-DBCE_ABLATE=2"],
+    "pipe_nosort": ["-DBCE_ABLATE=1"],
+    "pipe_all": ["-DBCE_ABLATE=11"],
 }
-SRCS = ["capi.hip", "consensus.hip"]
+SRCS = ["capi.hip", "consensus.hip", "elementwise.hip", "tiebreak.hip", "stats.hip"]
 
 
 def build(names):
