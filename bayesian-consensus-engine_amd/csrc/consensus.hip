@@ -24,6 +24,7 @@
 //
 // FP contraction is off for the whole file: every mul/add rounds like CPython.
 #include <stdio.h>
+#include <type_traits>
 #include <stdlib.h>
 
 #include "bce_device.hpp"
@@ -1261,6 +1262,15 @@ void consensus_stream_kernel(ConsArgs a) {
 // never touches registers the compute waves need.  Flags live in LDS (one workgroup).
 // Progress: the loader only waits for the release of sequence i-R, which a compute wave
 // is processing or has released (sequences are grabbed in order and R > C).
+#ifndef BCE_PIPE_PROF
+#define BCE_PIPE_PROF 0
+#endif
+#ifndef BCE_PIPE_RING
+#define BCE_PIPE_RING 16  // relconf gathers in flight per compute lane
+#endif
+#if BCE_PIPE_PROF
+__device__ unsigned long long g_pipe_prof[8];  // s_memtime cycles per compute-wave phase (debug build)
+#endif
 constexpr int kSpinCap = 1 << 22;  // ~0.1-0.3 s of s_sleep polling per wait
 
 // Acquire-load of an LDS flag, broadcast to a wave-uniform (SGPR) value: every spin and
@@ -1271,30 +1281,50 @@ __device__ __forceinline__ int ldsflag(int* f) {
   return __builtin_amdgcn_readfirstlane(v);
 }
 
+#ifndef BCE_PIPE_C32
+#define BCE_PIPE_C32 4  // compute waves at G = 32
+#endif
+#ifndef BCE_PIPE_R32
+#define BCE_PIPE_R32 6  // slots at G = 32 (LDS: ~25 KB each)
+#endif
+// Slots R >= C + 2: with one spare slot the ring is load-latency bound (a released slot
+// must be refilled within tile_time / C); two spares keep two tiles in flight.
+#ifndef BCE_PIPE_L
+#define BCE_PIPE_L 1  // loader waves (each keeps its own tiles in flight; 2 measured slower: TA contention)
+#endif
 template <int G>
 struct PipeCfg {
-  static constexpr int C = 4;   // compute waves
-  static constexpr int R = 5;   // slots
+  static constexpr int L = BCE_PIPE_L;
+  static constexpr int C = (G == 32) ? BCE_PIPE_C32 : 6;
+  static constexpr int R = (G == 32) ? BCE_PIPE_R32 : C + 3;
 };
 
 template <int G>
-__global__ __launch_bounds__(64 * (PipeCfg<G>::C + 1))
+__global__ __launch_bounds__(64 * (PipeCfg<G>::C + PipeCfg<G>::L))
 void consensus_pipe_kernel(ConsArgs a) {
   static_assert(G == 8 || G == 16 || G == 32, "pipe widths");
-  constexpr int C = PipeCfg<G>::C, R = PipeCfg<G>::R;
+  constexpr int C = PipeCfg<G>::C, R = PipeCfg<G>::R, NL = PipeCfg<G>::L;
   constexpr int TM = kWave;
   constexpr int LOGG = (G == 8) ? 3 : (G == 16) ? 4 : 5;
   constexpr int TS = TM * G;
-  constexpr int NSI = (TS + 8 + 4 * kWave - 1) / (4 * kWave);  // sid DMA instructions per tile
-  constexpr int NPI = (TS + 4 + 2 * kWave - 1) / (2 * kWave);  // prob DMA instructions
-  constexpr int NOI = 3;                                       // offsets block (dwords)
+  // Fixed DMA shape per tile: body instructions cover chunks [64k, 64k + 64) of the
+  // tile's range, one tail instruction covers its LAST 64 chunks [n - 64, n) (the same
+  // bytes again where they overlap), so the image is only as long as the largest range
+  // and the wave-instruction count never depends on the data.
+  constexpr int SCH = (TS + 6) / 4 + 1;   // max 16-B sid chunks of a tile (misaligned start)
+  constexpr int PCH = (TS + 2) / 2 + 1;   // max 16-B prob chunks
+  constexpr int OCH = 2 * (TM + 1);       // offsets block dwords
+  constexpr int NSI = SCH / kWave + 1;    // body + tail
+  constexpr int NPI = PCH / kWave + 1;
+  constexpr int NOI = OCH / kWave + 1;
   constexpr int NDMA = NSI + NPI + NOI;
   static_assert(NDMA < 64, "vmcnt field");
-  constexpr int SW = NSI * 256;  // sid image dwords (every DMA lane lands inside)
-  constexpr int PW = NPI * 128;  // prob image doubles
-  constexpr int OW = NOI * 64;   // offsets block dwords
-  static_assert(SW >= TS + 8 + G && PW >= TS + 4 + G && OW >= 2 * (TM + 1), "slot sizes");
-  constexpr int RING = 16;
+  constexpr int SW = (4 * SCH > TS + 4 + G) ? 4 * SCH : TS + 4 + G;  // sid image dwords (row overrun)
+  constexpr int PW = (2 * PCH > TS + 4 + G) ? 2 * PCH : TS + 4 + G;  // prob image doubles
+  constexpr int OW = OCH + 2;
+  static_assert(4 * kWave * (NSI - 1) <= SW && 2 * kWave * (NPI - 1) <= PW && kWave * (NOI - 1) <= OW,
+                "every body-instruction lane lands inside its image");
+  constexpr int RING = BCE_PIPE_RING;
   constexpr int NG = (G < RING) ? G : RING;
   constexpr int PA = 4;          // probabilities read this many positions ahead
   constexpr int P2 = G / 2;      // copy-out lanes per market (two slots per lane)
@@ -1308,14 +1338,13 @@ void consensus_pipe_kernel(ConsArgs a) {
   __shared__ int sReady[R];  // sequence + 1 once the slot holds it
   __shared__ int sFree[R];   // sequence + 1 once the slot's tile has been released
   __shared__ int sNext;
-  __shared__ double sTot[C][TM];
-  __shared__ int32_t sU[C][TM];
-  __shared__ int32_t sRs[C][TM];
+  __shared__ uint32_t sBad[R][TS / 32 + 2];  // bit i: prob of tile position i outside [0, 1]
+  __shared__ uint4 sInfo[C][TM];  // per market: {rs, u | n << 8 | rot << 16, total (lo, hi)}
 
   const int lane = lane_id();
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int nwords = (a.n_sources + 31) >> 5;  // <= kBitsLds (launcher)
-  for (int i = threadIdx.x; i < nwords; i += 64 * (C + 1)) sBits[i] = a.pbits[i];
+  for (int i = threadIdx.x; i < nwords; i += 64 * (C + NL)) sBits[i] = a.pbits[i];
   if (threadIdx.x < R) {
     sReady[threadIdx.x] = 0;
     sFree[threadIdx.x] = 0;
@@ -1326,14 +1355,15 @@ void consensus_pipe_kernel(ConsArgs a) {
   const int64_t M = a.n_list;
   const int64_t n_tiles = (M + TM - 1) / TM;
 
-  if (w == 0) {
-    // ================================ loader ==========================================
+  if (w < NL) {
+    // ================================ loaders =========================================
+    // loader w owns sequences i = w, w + NL, ... (slot i % R); k counts its own tiles
     const int64_t Nf4 = a.n_signals & ~3ll, Nf2 = a.n_signals & ~1ll;
     const int64_t clamp_s = (Nf4 - 4 > 0) ? Nf4 - 4 : 0;  // host: n_signals >= 4
     const int64_t clamp_p = (Nf2 - 2 > 0) ? Nf2 - 2 : 0;
     int64_t tbB = 0, tbE = 0;
-    auto load_bounds = [&](int64_t base) {
-      const int64_t t = (int64_t)blockIdx.x + (base + lane) * gridDim.x;
+    auto load_bounds = [&](int64_t kbase) {
+      const int64_t t = (int64_t)blockIdx.x + (w + (kbase + lane) * NL) * gridDim.x;
       if (t < n_tiles) {
         const int64_t m0 = t * TM;
         tbB = a.offsets[m0];
@@ -1343,6 +1373,27 @@ void consensus_pipe_kernel(ConsArgs a) {
     auto rl = [&](int64_t v, int i) -> int64_t {
       return ((int64_t)__builtin_amdgcn_readlane((int)(v >> 32), i) << 32) |
              (uint32_t)__builtin_amdgcn_readlane((int)v, i);
+    };
+    // validation (core.py:59-60) for the compute waves: the tail of the arrays that no
+    // 16-B chunk covers is loaded here, then every position's range check becomes one bit
+    // of sBad (ballot per 64 positions, contiguous conflict-free reads); NaN passes
+    auto finish = [&](int s, int64_t B, int64_t E) {
+      const int64_t Bs = B & ~3ll, Bp = B & ~1ll;
+      const int64_t es = (E < Nf4) ? ((E + 3) & ~3ll) : Nf4;
+      const int64_t ep = (E < Nf2) ? ((E + 1) & ~1ll) : Nf2;
+      if (E > es && lane < (int)(E - es)) sSid[s][es - Bs + lane] = (uint32_t)a.sid[es + lane];
+      if (E > ep && lane < (int)(E - ep)) sProb[s][ep - Bp + lane] = a.prob[ep + lane];
+      wave_sync_lds();
+      const int nb = (int)(E - B), d = (int)(B - Bp);
+#pragma unroll 4
+      for (int k = 0; k < TS / kWave; ++k) {
+        const int i = k * kWave + lane;
+        const double p = sProb[s][d + ((i < nb) ? i : 0)];
+        const unsigned long long m = ballot(i < nb && (p < 0.0 || p > 1.0));
+        sBad[s][2 * k] = (uint32_t)m;
+        sBad[s][2 * k + 1] = (uint32_t)(m >> 32);
+      }
+      wave_sync_lds();
     };
     auto publish = [&](int seq, int64_t t) {
       const int s = seq % R;
@@ -1356,8 +1407,8 @@ void consensus_pipe_kernel(ConsArgs a) {
     };
     const int64_t my_tiles = (n_tiles > (int64_t)blockIdx.x) ? (n_tiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
     int pending = -1;  // sequence whose DMA is in flight and not yet published
-    int64_t pend_t = -1;
-    for (int64_t i = 0; i < my_tiles + C; ++i) {
+    int64_t pend_t = -1, pend_B = 0, pend_E = 0;
+    for (int64_t i = w, k = 0; i < my_tiles + C; i += NL, ++k) {
       const int s = (int)(i % R);
 #if BCE_PIPE_DBG
       if (lane == 0 && blockIdx.x == 0) printf("[L] i %ld / %ld\n", (long)i, (long)(my_tiles + C));
@@ -1368,6 +1419,7 @@ void consensus_pipe_kernel(ConsArgs a) {
         if (ldsflag(&sFree[s]) < need) {
           if (pending >= 0) {
             __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+            finish(pending % R, pend_B, pend_E);
             publish(pending, pend_t);
             pending = -1;
           }
@@ -1381,22 +1433,24 @@ void consensus_pipe_kernel(ConsArgs a) {
       if (i >= my_tiles) {  // end markers: one per compute wave
         if (pending >= 0) {
           __builtin_amdgcn_s_waitcnt(0x0F70);
-          publish(pending, pend_t);
+          finish(pending % R, pend_B, pend_E);
+            publish(pending, pend_t);
           pending = -1;
         }
         publish((int)i, -1);
         continue;
       }
-      if ((i & 63) == 0) {
-        load_bounds(i);
+      if ((k & 63) == 0) {
+        load_bounds(k);
         __builtin_amdgcn_s_waitcnt(0x0F70);  // (drains in-flight DMA too; once per 64 tiles)
         if (pending >= 0) {
-          publish(pending, pend_t);
+          finish(pending % R, pend_B, pend_E);
+            publish(pending, pend_t);
           pending = -1;
         }
       }
       const int64_t t = (int64_t)blockIdx.x + i * gridDim.x;
-      const int64_t B = rl(tbB, (int)(i & 63)), E = rl(tbE, (int)(i & 63));
+      const int64_t B = rl(tbB, (int)(k & 63)), E = rl(tbE, (int)(k & 63));
       const int64_t m0 = t * TM, m1 = (m0 + TM < M) ? m0 + TM : M;
       const int64_t Bs = B & ~3ll, Bp = B & ~1ll;
       const int64_t es = (E < Nf4) ? ((E + 3) & ~3ll) : Nf4;
@@ -1404,38 +1458,70 @@ void consensus_pipe_kernel(ConsArgs a) {
       const int nci = (int)((es - Bs) >> 2), ncp = (int)((ep - Bp) >> 1);
       const int ndw = (int)(2 * (m1 - m0 + 1));
       const int64_t fs = (Bs < clamp_s) ? Bs : clamp_s, fp = (Bp < clamp_p) ? Bp : clamp_p;
+      // body instruction k covers chunks [64k, 64k + 64) (lanes past the range re-read the
+      // first chunk into slack the range never reaches); once the range is exhausted a body
+      // instruction repeats instruction 0 (same bytes to the same places); the tail
+      // instruction covers the range's last 64 chunks (from 0 if it is shorter)
 #pragma unroll
-      for (int k = 0; k < NSI; ++k) {
-        const int c = k * kWave + lane;
-        dma_b128(a.sid + ((c < nci) ? Bs + 4 * c : fs), &sSid[s][k * 256]);
+      for (int k = 0; k < NSI - 1; ++k) {
+        const int kk = (k * kWave < nci) ? k : 0;
+        const int c = kk * kWave + lane;
+        dma_b128(a.sid + ((c < nci) ? Bs + 4 * c : fs), &sSid[s][kk * 256]);
+      }
+      {
+        const int tb = (nci > kWave) ? nci - kWave : 0;
+        const int c = tb + lane;
+        dma_b128(a.sid + ((c < nci) ? Bs + 4 * c : fs), &sSid[s][tb * 4]);
       }
 #pragma unroll
-      for (int k = 0; k < NPI; ++k) {
-        const int c = k * kWave + lane;
-        dma_b128(a.prob + ((c < ncp) ? Bp + 2 * c : fp), &sProb[s][k * 128]);
+      for (int k = 0; k < NPI - 1; ++k) {
+        const int kk = (k * kWave < ncp) ? k : 0;
+        const int c = kk * kWave + lane;
+        dma_b128(a.prob + ((c < ncp) ? Bp + 2 * c : fp), &sProb[s][kk * 128]);
+      }
+      {
+        const int tb = (ncp > kWave) ? ncp - kWave : 0;
+        const int c = tb + lane;
+        dma_b128(a.prob + ((c < ncp) ? Bp + 2 * c : fp), &sProb[s][tb * 2]);
       }
       const uint32_t* og = reinterpret_cast<const uint32_t*>(a.offsets + m0);
 #pragma unroll
-      for (int k = 0; k < NOI; ++k) {
-        const int d = k * kWave + lane;
-        dma_b32(og + ((d < ndw) ? d : 0), &sOffs[s][k * 64]);
+      for (int k = 0; k < NOI - 1; ++k) {
+        const int kk = (k * kWave < ndw) ? k : 0;
+        const int d = kk * kWave + lane;
+        dma_b32(og + ((d < ndw) ? d : 0), &sOffs[s][kk * 64]);
+      }
+      {
+        const int tb = (ndw > kWave) ? ndw - kWave : 0;
+        const int d = tb + lane;
+        dma_b32(og + ((d < ndw) ? d : 0), &sOffs[s][tb]);
       }
       if (pending >= 0) {  // the previous tile has landed once only this one is in flight
         __builtin_amdgcn_s_waitcnt((NDMA & 15) | (7 << 4) | (15 << 8) | ((NDMA >> 4) << 14));
-        publish(pending, pend_t);
+        finish(pending % R, pend_B, pend_E);
+            publish(pending, pend_t);
       }
       pending = (int)i;
       pend_t = t;
+      pend_B = B;
+      pend_E = E;
     }
     if (pending >= 0) {
       __builtin_amdgcn_s_waitcnt(0x0F70);
-      publish(pending, pend_t);
+      finish(pending % R, pend_B, pend_E);
+            publish(pending, pend_t);
     }
     return;
   }
 
   // ================================ compute waves =====================================
-  const int cw = w - 1;
+  const int cw = w - NL;
+#if BCE_PIPE_PROF
+  unsigned long long pr_t = __builtin_amdgcn_s_memtime(), pr[6] = {0, 0, 0, 0, 0, 0};
+#define PROF_MARK(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); pr[k] += t_ - pr_t; pr_t = t_; } while (0)
+#else
+#define PROF_MARK(k) do {} while (0)
+#endif
   const unsigned smax = (unsigned)(a.n_sources > 0 ? a.n_sources - 1 : 0);
   const double2* const tab = (a.n_sources > 0) ? a.relconf : kColdRow;
   const int64_t Nf4 = a.n_signals & ~3ll, Nf2 = a.n_signals & ~1ll;
@@ -1453,6 +1539,7 @@ void consensus_pipe_kernel(ConsArgs a) {
       __builtin_amdgcn_s_sleep(1);
       if (++spins > kSpinCap) return;  // never expected; bounded so a bug cannot hang the GPU
     }
+    PROF_MARK(0);  // waiting for a loaded slot
     const int64_t tile0 = sTile[s];
     const int64_t tile = ((int64_t)__builtin_amdgcn_readfirstlane((int)(tile0 >> 32)) << 32) |
                          (uint32_t)__builtin_amdgcn_readfirstlane((int)tile0);  // uniform
@@ -1461,6 +1548,11 @@ void consensus_pipe_kernel(ConsArgs a) {
 #endif
     if (tile < 0) {
       __hip_atomic_store(&sFree[s], seq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#if BCE_PIPE_PROF
+      if (lane_id() == 0)
+        for (int k = 0; k < 5; ++k) atomicAdd(&g_pipe_prof[k], pr[k]);
+      if (lane_id() == 0) atomicAdd(&g_pipe_prof[5], 1ull);
+#endif
       break;
     }
     uint32_t* const iS = sSid[s];
@@ -1475,10 +1567,8 @@ void consensus_pipe_kernel(ConsArgs a) {
     const int64_t Bs = B & ~3ll, Bp = B & ~1ll;
     const int64_t es = (E < Nf4) ? ((E + 3) & ~3ll) : Nf4;
     const int64_t ep = (E < Nf2) ? ((E + 1) & ~1ll) : Nf2;
-    if (E > es && ln < (int)(E - es)) iS[es - Bs + ln] = (uint32_t)a.sid[es + ln];
-    if (E > ep && ln < (int)(E - ep)) iP[ep - Bp + ln] = a.prob[ep + ln];
-    wave_sync_lds();
-
+    (void)es;
+    (void)ep;
     const int64_t mk = m0 + ln;
     const bool has = mk < M;
     int64_t off = B;
@@ -1506,20 +1596,18 @@ void consensus_pipe_kernel(ConsArgs a) {
 #pragma unroll
     for (int t = 0; t < G; ++t) key[t] = (t < n) ? ((key[t] << LOGG) | (unsigned)t) : kSent32;
     if constexpr (!(BCE_ABLATE & 1)) oem_sort<G>(key);
-    unsigned fb = 0, lb = 0;
+    // run boundaries: bit t of nq = (sid_t != sid_t+1); sentinels sort last and never
+    // equal a sid, so lst = nq | top bit, fst = nq << 1 | 1, both masked to t < n
+    unsigned nq = 0;
 #pragma unroll
-    for (int t = G - 1; t >= 0; --t) {
-      const unsigned sd = key[t] >> LOGG;
-      const bool kv = key[t] != kSent32;
-      const bool f = kv && (t == 0 || sd != (key[t > 0 ? t - 1 : 0] >> LOGG));
-      const bool l = kv && (t == G - 1 || sd != (key[t < G - 1 ? t + 1 : t] >> LOGG));
-      fb = (fb << 1) | (f ? 1u : 0u);
-      lb = (lb << 1) | (l ? 1u : 0u);
-    }
+    for (int t = G - 2; t >= 0; --t) nq = (nq << 1) | (((key[t] ^ key[t + 1]) >> LOGG) != 0u ? 1u : 0u);
     unsigned vb = (n >= 32) ? 0xFFFFFFFFu : ((1u << n) - 1u);
+    unsigned lb = (nq | (1u << (G - 1))) & vb;
+    unsigned fb = ((nq << 1) | 1u) & vb;
     asm volatile("" : "+v"(fb), "+v"(lb), "+v"(vb));
     wave_sync_lds();  // every lane has its sids: rows become usid staging
 
+    PROF_MARK(1);  // keys + sort
     double2 ring[NG];
 #pragma unroll
     for (int t = 0; t < NG; ++t) {
@@ -1533,14 +1621,20 @@ void consensus_pipe_kernel(ConsArgs a) {
 
     // ---- walk (core.py:107-144 in sorted-source order) ----------------------------------
     double total = 0.0, ws = 0.0, cs = 0.0, psum = 0.0;
-    int cnt = 0, err = G, j = 0;
+    int cnt = 0, j = 0;
+    // single positions: valid, first AND last of their run -- on random ids ~97 % of all
+    // positions, and at ~83 % of positions every lane of the wave is single
+    unsigned sb = fb & lb & vb;
+    asm volatile("" : "+v"(sb));
+    // unique j is staged at row cell (j + lane) mod n: rows of equal length sit at a
+    // stride of n dwords, so cell j alone would put every lane on one bank (32-way);
+    // rotating by the lane spreads them (cells < n only: neighbours' rows untouched)
+    const int rotn = (n > 0) ? ln % n : 0;
+    auto rot = [&](int jj) { const int x = jj + rotn; return (x >= n) ? x - n : x; };
 #pragma unroll
     for (int t = 0; t < G; ++t) {
-      const bool kv = __builtin_amdgcn_ubfe(vb, t, 1) != 0u;
       const unsigned sid = key[t] >> LOGG;
       const int slot = (int)(key[t] & (G - 1));
-      const bool fst = __builtin_amdgcn_ubfe(fb, t, 1) != 0u;
-      const bool lst = __builtin_amdgcn_ubfe(lb, t, 1) != 0u;
       const double p = pq[t % PA];
       if (t + PA < G) pq[t % PA] = iP[rsp + (int)(key[t + PA < G ? t + PA : t] & (G - 1))];
       const double2 rc = ring[t % NG];
@@ -1548,26 +1642,41 @@ void consensus_pipe_kernel(ConsArgs a) {
         const unsigned ix = min(key[t + NG < G ? t + NG : t] >> LOGG, smax);
         if constexpr (!(BCE_ABLATE & 2)) ring[t % NG] = tab[ix];
       }
-      if (kv && (p < 0.0 || p > 1.0)) err = (slot < err) ? slot : err;  // core.py:59-60
-      psum = (fst ? 0.0 : psum) + p;   // builtin sum() from int 0 (core.py:116)
-      cnt = fst ? 1 : cnt + 1;
-      double avg = psum;
-      if (ballot(lst && cnt > 1)) {     // duplicates: sum / len (core.py:116), rare
-        if (lst && cnt > 1) avg = psum / (double)cnt;
-      }
       const double wt = rc.x, cf = rc.y;
-      total += lst ? wt : 0.0;          // core.py:120
-      ws += lst ? avg * wt : 0.0;       // core.py:135-137
-      cs += lst ? cf * wt : 0.0;        // core.py:141-143
-      if (kv) {  // j <= t: the row cell is dead; the slot's probability has been read
-        iS[rsi + j] = sid | ((unsigned)slot << kPackSlot);
+      const bool kv = __builtin_amdgcn_ubfe(vb, t, 1) != 0u;
+      if (ballot(__builtin_amdgcn_ubfe(sb, t, 1) == 0u) == 0) {
+        // every lane: a source seen once (avg = 0 + p) -- plain left-to-right adds
+        total += wt;                      // core.py:120
+        ws += p * wt;                     // core.py:135-137 (0 + p == p bit for bit,
+        cs += cf * wt;                    //   except -0.0 -> +0.0, which * w changes nothing)
+        iS[rsi + rot(j)] = sid | ((unsigned)slot << kPackSlot);
         iP[rsp + slot] = wt;
+        j += 1;
+      } else {
+        const bool fst = __builtin_amdgcn_ubfe(fb, t, 1) != 0u;
+        const bool lst = __builtin_amdgcn_ubfe(lb, t, 1) != 0u;
+        psum = (fst ? 0.0 : psum) + p;   // builtin sum() from int 0 (core.py:116)
+        cnt = fst ? 1 : cnt + 1;
+        double avg = psum;
+        if (ballot(lst && cnt > 1)) {     // duplicates: sum / len (core.py:116), rare
+          if (lst && cnt > 1) avg = psum / (double)cnt;
+        }
+        // accumulate only at the last position of a run; +0.0 leaves every chain
+        // bit-exact (the chains start at +0.0 and can never become -0.0)
+        total += lst ? wt : 0.0;          // core.py:120
+        ws += lst ? avg * wt : 0.0;       // core.py:135-137
+        cs += lst ? cf * wt : 0.0;        // core.py:141-143
+        if (kv) {  // j <= t: the row cell is dead; the slot's probability has been read
+          iS[rsi + rot(j)] = sid | ((unsigned)slot << kPackSlot);
+          iP[rsp + slot] = wt;
+        }
+        j += lst ? 1 : 0;
       }
-      j += lst ? 1 : 0;
-      asm volatile("" : "+v"(total), "+v"(ws), "+v"(cs), "+v"(psum), "+v"(cnt), "+v"(err), "+v"(j));
+      asm volatile("" : "+v"(total), "+v"(ws), "+v"(cs), "+v"(psum), "+v"(cnt), "+v"(j));
       __builtin_amdgcn_sched_barrier(0);
     }
 
+    PROF_MARK(2);  // walk
     // ---- per-market results --------------------------------------------------------------
     if (has) {
       const bool null_ = (total == 0.0);  // core.py:131-133
@@ -1575,70 +1684,103 @@ void consensus_pipe_kernel(ConsArgs a) {
       a.confidence[mk] = null_ ? 0.0 : cs / total;
       a.total_weight[mk] = total;
       a.n_unique[mk] = j;
-      if (a.err_idx) a.err_idx[mk] = (err < G) ? err : -1;
+      if (a.err_idx) {  // first bad input index (the loader's range-check bits)
+        const int w0 = rs >> 5, sh = rs & 31;
+        const uint32_t lo = sBad[s][w0], hi = sBad[s][w0 + 1];
+        const uint32_t bits = ((sh ? (hi << (32 - sh)) : 0u) | (lo >> sh)) & vb;
+        a.err_idx[mk] = bits ? (int)__builtin_ctz(bits) : -1;
+      }
     }
-    sTot[cw][ln] = total;
-    sU[cw][ln] = has ? j : 0;
-    sRs[cw][ln] = rs;
+    {
+      const uint2 tb = *reinterpret_cast<const uint2*>(&total);
+      sInfo[cw][ln] = make_uint4((unsigned)rs, (unsigned)(has ? j : 0) | ((unsigned)((n > 0) ? n : 1) << 8) |
+                                                   ((unsigned)rotn << 16), tb.x, tb.y);
+    }
     wave_sync_lds();
 
+    PROF_MARK(3);  // per-market results
     // ---- per-unique outputs from the in-place staging ------------------------------------
-    if ((a.usid || a.weight || a.nweight) && !(BCE_ABLATE & 8)) {
+    // lane = (market q, slot pair k2), batches of CB iterations: the three dependent LDS
+    // round trips (info -> packed usid -> weight cell / present bit) are issued for the
+    // whole batch before any result is used, and no load sits under a branch.
+    if (!(BCE_ABLATE & 8)) {
       const int dB = (int)(B - Bs), dP = (int)(B - Bp);
-      const bool vec_ok = (((uintptr_t)a.usid & 7) | ((uintptr_t)a.weight & 15) | ((uintptr_t)a.nweight & 15)) == 0;
-      if (vec_ok && ballot(has && (off & 1) != 0) == 0 && (B & 1) == 0) {
-        const int k2 = 2 * (ln % P2);
-#pragma unroll 2
-        for (int it = 0; it < TM / MPI; ++it) {
-          const int q = it * MPI + ln / P2;
-          const int u = sU[cw][q];
-          if (k2 < u) {
-            const int r = sRs[cw][q];
-            const double tot = sTot[cw][q];
-            const int64_t pos = B + r + k2;
-            const bool two = k2 + 1 < u;
-            const uint2 pk = *reinterpret_cast<const uint2*>(iS + dB + r + k2);  // (rs + dB) even
-            const unsigned s0 = pk.x & ((1u << kPackSlot) - 1), s1 = pk.y & ((1u << kPackSlot) - 1);
-            const double w0 = iP[dP + r + (int)(pk.x >> kPackSlot)];
-            const double w1 = two ? iP[dP + r + (int)(pk.y >> kPackSlot)] : 0.0;
-            const bool p0 = is_present(sBits, (int)min(s0, smax));
-            const bool p1 = is_present(sBits, (int)min(s1, smax));
-            const unsigned u0 = s0 | (p0 ? 0u : 0x80000000u);  // core.py:167-170
-            const unsigned u1 = s1 | (p1 ? 0u : 0x80000000u);
-            const double n0 = (tot > 0.0) ? w0 / tot : 0.0;    // core.py:151
-            const double n1 = (tot > 0.0) ? w1 / tot : 0.0;
-            if (two) {
-              if (a.usid) *reinterpret_cast<uint2*>(a.usid + pos) = make_uint2(u0, u1);
-              if (a.weight) *reinterpret_cast<double2*>(a.weight + pos) = make_double2(w0, w1);
-              if (a.nweight) *reinterpret_cast<double2*>(a.nweight + pos) = make_double2(n0, n1);
-            } else {
-              if (a.usid) a.usid[pos] = (int32_t)u0;
-              if (a.weight) a.weight[pos] = w0;
-              if (a.nweight) a.nweight[pos] = n0;
+      auto copy_out = [&](auto npl) {
+        constexpr int NPL = decltype(npl)::value;  // 2: slot pairs (16-B stores), 1: single slots
+        constexpr int LPM = G / NPL;               // lanes per market
+        constexpr int MPX = kWave / LPM;           // markets per iteration
+        constexpr int NIT = TM / MPX;
+        constexpr int CB = (NIT < 4) ? NIT : 4;
+        const int k2 = NPL * (ln % LPM), g = ln / LPM;
+#pragma unroll 1
+        for (int i0 = 0; i0 < NIT; i0 += CB) {
+          uint4 inf[CB];
+#pragma unroll
+          for (int b = 0; b < CB; ++b) inf[b] = sInfo[cw][(i0 + b) * MPX + g];
+          int r[CB], c0[CB], c1[CB];
+          bool v0[CB], v1[CB];
+#pragma unroll
+          for (int b = 0; b < CB; ++b) {
+            r[b] = (int)inf[b].x;
+            const int u = (int)(inf[b].y & 255u), nq = (int)((inf[b].y >> 8) & 255u), rq = (int)(inf[b].y >> 16);
+            v0[b] = k2 < u;
+            v1[b] = NPL == 2 && k2 + 1 < u;
+            int x0 = k2 + rq;
+            x0 -= (x0 >= nq) ? nq : 0;
+            int x1 = x0 + 1;
+            x1 -= (x1 >= nq) ? nq : 0;
+            c0[b] = v0[b] ? x0 : 0;
+            c1[b] = v1[b] ? x1 : 0;
+          }
+          unsigned pk0[CB], pk1[CB];
+#pragma unroll
+          for (int b = 0; b < CB; ++b) {
+            pk0[b] = iS[dB + r[b] + c0[b]];
+            pk1[b] = (NPL == 2) ? iS[dB + r[b] + c1[b]] : 0u;
+          }
+          double w0[CB], w1[CB];
+          unsigned u0[CB], u1[CB], bw0[CB], bw1[CB];
+#pragma unroll
+          for (int b = 0; b < CB; ++b) {
+            u0[b] = pk0[b] & ((1u << kPackSlot) - 1);
+            u1[b] = pk1[b] & ((1u << kPackSlot) - 1);
+            w0[b] = iP[dP + r[b] + (int)((pk0[b] >> kPackSlot) & (G - 1))];
+            w1[b] = (NPL == 2) ? iP[dP + r[b] + (int)((pk1[b] >> kPackSlot) & (G - 1))] : 0.0;
+            bw0[b] = sBits[min(u0[b], smax) >> 5];
+            bw1[b] = (NPL == 2) ? sBits[min(u1[b], smax) >> 5] : 0u;
+          }
+          // materialise the batch here: left alone, loads used only under the store
+          // branches are sunk into them and serialise again
+#pragma unroll
+          for (int b = 0; b < CB; ++b) asm volatile("" : "+v"(w0[b]), "+v"(w1[b]), "+v"(bw0[b]), "+v"(bw1[b]));
+#pragma unroll
+          for (int b = 0; b < CB; ++b) {
+            const double tot = __hiloint2double((int)inf[b].w, (int)inf[b].z);
+            const unsigned x0 = u0[b] | ((((bw0[b] >> (min(u0[b], smax) & 31)) & 1u) != 0u) ? 0u : 0x80000000u);
+            const unsigned x1 = u1[b] | ((((bw1[b] >> (min(u1[b], smax) & 31)) & 1u) != 0u) ? 0u : 0x80000000u);
+            const double n0 = (tot > 0.0) ? w0[b] / tot : 0.0;  // core.py:151
+            const double n1 = (tot > 0.0) ? w1[b] / tot : 0.0;  // (cold bit: core.py:167-170)
+            const int64_t pos = B + r[b] + k2;
+            if (v1[b]) {
+              *reinterpret_cast<uint2*>(a.usid + pos) = make_uint2(x0, x1);
+              *reinterpret_cast<double2*>(a.weight + pos) = make_double2(w0[b], w1[b]);
+              *reinterpret_cast<double2*>(a.nweight + pos) = make_double2(n0, n1);
+            } else if (v0[b]) {
+              a.usid[pos] = (int32_t)x0;
+              a.weight[pos] = w0[b];
+              a.nweight[pos] = n0;
             }
           }
         }
-      } else {
-        const int sl = ln % G;
-#pragma unroll 1
-        for (int it = 0; it < TM / (kWave / G); ++it) {
-          const int q = it * (kWave / G) + ln / G;
-          if (sl < sU[cw][q]) {
-            const int r = sRs[cw][q];
-            const double tot = sTot[cw][q];
-            const unsigned pk = iS[dB + r + sl];
-            const unsigned s0 = pk & ((1u << kPackSlot) - 1);
-            const double wt = iP[dP + r + (int)(pk >> kPackSlot)];
-            const bool pr = is_present(sBits, (int)min(s0, smax));
-            const int64_t pos = B + r + sl;
-            if (a.usid) a.usid[pos] = (int32_t)(s0 | (pr ? 0u : 0x80000000u));
-            if (a.weight) a.weight[pos] = wt;
-            if (a.nweight) a.nweight[pos] = (tot > 0.0) ? wt / tot : 0.0;
-          }
-        }
-      }
+      };
+      const bool vec_ok = (((uintptr_t)a.usid & 7) | ((uintptr_t)a.weight & 15) | ((uintptr_t)a.nweight & 15)) == 0;
+      if (vec_ok && ballot(has && (off & 1) != 0) == 0 && (B & 1) == 0)
+        copy_out(std::integral_constant<int, 2>{});
+      else
+        copy_out(std::integral_constant<int, 1>{});
     }
     wave_sync_lds();  // every read of the slot has returned
+    PROF_MARK(4);  // copy-out
 #if BCE_PIPE_DBG
     if (lane == 0 && blockIdx.x == 0) printf("[C%d] seq %d done\n", w, seq);
 #endif
@@ -1909,7 +2051,8 @@ int launch_pipe(const ConsArgs& a, hipStream_t st) {
   static int per_cu = 0;
   if (!per_cu) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, consensus_pipe_kernel<G>, 64 * (PipeCfg<G>::C + 1), 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, consensus_pipe_kernel<G>,
+                                                     64 * (PipeCfg<G>::C + PipeCfg<G>::L), 0) !=
             hipSuccess || nb <= 0)
       nb = 1;
     per_cu = nb;
@@ -1918,7 +2061,8 @@ int launch_pipe(const ConsArgs& a, hipStream_t st) {
   }
   const int64_t cap = (int64_t)cu_count() * per_cu;
   const int grid = (int)(tiles < cap ? tiles : cap);
-  hipLaunchKernelGGL((consensus_pipe_kernel<G>), dim3(grid), dim3(64 * (PipeCfg<G>::C + 1)), 0, st, a);
+  hipLaunchKernelGGL((consensus_pipe_kernel<G>), dim3(grid), dim3(64 * (PipeCfg<G>::C + PipeCfg<G>::L)), 0, st,
+                     a);
   return check_launch("consensus_pipe_kernel");
 }
 
@@ -1970,7 +2114,8 @@ int launch_flat(const ConsArgs& a, hipStream_t st) {
 }
 
 int launch_seg_for_len(int max_len, const ConsArgs& a, hipStream_t st) {
-  if (BCE_FLAT == 3 && a.list == nullptr && max_len <= 32 && a.n_sources <= 32 * kBitsLds && a.n_signals >= 4) {
+  if (BCE_FLAT == 3 && a.list == nullptr && max_len <= 32 && a.n_sources <= 32 * kBitsLds && a.n_signals >= 4 &&
+      a.usid && a.weight && a.nweight) {
     if (max_len <= 8) return launch_pipe<8>(a, st);
     if (max_len <= 16) return launch_pipe<16>(a, st);
     return launch_pipe<32>(a, st);
@@ -2232,6 +2377,15 @@ __global__ __launch_bounds__(256) void validate_kernel(const int64_t* offsets, i
   }
 }
 }  // namespace bce
+
+#if BCE_PIPE_PROF
+extern "C" int bce_pipe_prof_read(unsigned long long* host8) {
+  BCE_HIP(hipMemcpyFromSymbol(host8, HIP_SYMBOL(bce::g_pipe_prof), 8 * sizeof(unsigned long long)));
+  unsigned long long z[8] = {0};
+  BCE_HIP(hipMemcpyToSymbol(HIP_SYMBOL(bce::g_pipe_prof), z, sizeof z));
+  return BCE_OK;
+}
+#endif
 
 extern "C" int bce_validate_csr(const int64_t* offsets, int64_t n_markets, const double* prob,
                                 int32_t* err_idx, void* stream) {

@@ -190,7 +190,7 @@ def bench_c2(args, world, rank):
                    "parallelism": f"markets sharded, {world} independent rank(s), no collective"},
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "consensus_lpm_kernel<32>" if L <= 32 else "consensus_seg_kernel<64,*>",
+                     "kernel": "consensus_pipe_kernel<32>" if L <= 32 else "consensus_seg_kernel<64,*>",
                      "bytes_per_launch": bytes_per_launch, "avg_launch_ms": avg_kernel_s * 1e3},
         "cpu_baseline": None,
     }

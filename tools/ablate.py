@@ -20,13 +20,14 @@ OUT = os.path.join(ROOT, "tools", "ablate_build")
 
 VARIANTS = {
     "pipe": [],
-    "stream": ["-DBCE_FLAT=2"],
-    "flat_wpb1": ["-DBCE_FLAT=1", "-DBCE_FLAT_WPB=1"],
+    "pipe_c5": ["-DBCE_PIPE_C32=5"],
+    "pipe_ring24": ["-DBCE_PIPE_RING=24"],
+    "pipe_c5_ring24": ["-DBCE_PIPE_C32=5", "-DBCE_PIPE_RING=24"],
+    "pipe_r5": ["-DBCE_PIPE_R32=5"],
     "lpm": ["-DBCE_FLAT=0"],
     "pipe_noout": ["-DBCE_ABLATE=8"],
     "pipe_nogather": ["-DBCE_ABLATE=2"],
-    "pipe_nosort": ["-DBCE_ABLATE=1"],
-    "pipe_all": ["-DBCE_ABLATE=11"],
+    "pipe_prof": ["-DBCE_PIPE_PROF=1"],
 }
 SRCS = ["capi.hip", "consensus.hip", "elementwise.hip", "tiebreak.hip", "stats.hip"]
 

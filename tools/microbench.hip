@@ -31,6 +31,45 @@ __global__ __launch_bounds__(64) void gather16(const double2* tab, const int* id
   if (acc == 12345.0) out[0] = acc;
 }
 
+template <int AUX>
+__global__ __launch_bounds__(64) void gather16_aux(const double2* tab, const int* idx, int64_t n_tiles, double* out) {
+  const int lane = threadIdx.x;
+  double acc = 0;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)tab, 0, 10000 * 16, 0x00020000);
+  for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+    const int* ip = idx + (t & 1023) * 2048 + lane * 32;
+    int ids[32];
+#pragma unroll
+    for (int k = 0; k < 32; k += 4) { int4 v = *(const int4*)(ip + k); ids[k] = v.x; ids[k+1] = v.y; ids[k+2] = v.z; ids[k+3] = v.w; }
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      typedef unsigned v4u __attribute__((ext_vector_type(4)));
+      v4u v = __builtin_amdgcn_raw_buffer_load_b128(rs, ids[k] * 16, 0, AUX);
+      double2 d = *reinterpret_cast<double2*>(&v);
+      acc += d.x * d.y;
+    }
+  }
+  if (acc == 12345.0) out[0] = acc;
+}
+
+__global__ __launch_bounds__(64) void gather16_ntl(const double2* tab, const int* idx, int64_t n_tiles, double* out) {
+  const int lane = threadIdx.x;
+  double acc = 0;
+  for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+    const int* ip = idx + (t & 1023) * 2048 + lane * 32;
+    int ids[32];
+#pragma unroll
+    for (int k = 0; k < 32; k += 4) { int4 v = *(const int4*)(ip + k); ids[k] = v.x; ids[k+1] = v.y; ids[k+2] = v.z; ids[k+3] = v.w; }
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const double x = __builtin_nontemporal_load(&tab[ids[k]].x);
+      const double y = __builtin_nontemporal_load(&tab[ids[k]].y);
+      acc += x * y;
+    }
+  }
+  if (acc == 12345.0) out[0] = acc;
+}
+
 __global__ __launch_bounds__(64) void gather8(const double* tab, const int* idx, int64_t n_tiles, double* out) {
   const int lane = threadIdx.x;
   double acc = 0;
@@ -152,30 +191,24 @@ int main() {
     printf("%-28s %8.3f ms  %8.1f GB/s  %7.2f cyc/wave-instr/CU\n", name, s * 1e3, bytes / s / 1e9,
            cyc * cus / instrs);
   };
-  for (int occ : {4, 8, 16}) {
+  for (int occ : {8}) {
     const int grid = cus * occ;
     const int64_t tiles = 200000;
     char nm[64];
     snprintf(nm, 64, "gather16 occ%d", occ);
     timeit(nm, [&] { gather16<<<grid, 64>>>(tab, idx, tiles, dout); }, tiles * 2048.0 * 16, tiles * 32.0);
+    snprintf(nm, 64, "gather16_buf aux0 occ%d", occ);
+    timeit(nm, [&] { gather16_aux<0><<<grid, 64>>>(tab, idx, tiles, dout); }, tiles * 2048.0 * 16, tiles * 32.0);
+    snprintf(nm, 64, "gather16_buf aux1(glc) occ%d", occ);
+    timeit(nm, [&] { gather16_aux<1><<<grid, 64>>>(tab, idx, tiles, dout); }, tiles * 2048.0 * 16, tiles * 32.0);
+    snprintf(nm, 64, "gather16_buf aux2(slc) occ%d", occ);
+    timeit(nm, [&] { gather16_aux<2><<<grid, 64>>>(tab, idx, tiles, dout); }, tiles * 2048.0 * 16, tiles * 32.0);
+    snprintf(nm, 64, "gather16_buf aux3 occ%d", occ);
+    timeit(nm, [&] { gather16_aux<3><<<grid, 64>>>(tab, idx, tiles, dout); }, tiles * 2048.0 * 16, tiles * 32.0);
+    snprintf(nm, 64, "gather16_nt occ%d", occ);
+    timeit(nm, [&] { gather16_ntl<<<grid, 64>>>(tab, idx, tiles, dout); }, tiles * 2048.0 * 16, tiles * 64.0);
     snprintf(nm, 64, "gather8 occ%d", occ);
     timeit(nm, [&] { gather8<<<grid, 64>>>((const double*)tab, idx, tiles, dout); }, tiles * 2048.0 * 8, tiles * 32.0);
-    const int64_t t128 = big / (128 * 64), t256 = big / (256 * 64);
-    snprintf(nm, 64, "coalx4 row128 occ%d", occ);
-    timeit(nm, [&] { coalx4<128><<<grid, 64>>>((const int4*)src, t128, (int*)dout); }, (double)big, t128 * 8.0);
-    snprintf(nm, 64, "transx4 row128 occ%d", occ);
-    timeit(nm, [&] { transx4<128><<<grid, 64>>>((const int4*)src, t128, (int*)dout); }, (double)big, t128 * 8.0);
-    snprintf(nm, 64, "transx4 row256 occ%d", occ);
-    timeit(nm, [&] { transx4<256><<<grid, 64>>>((const int4*)src, t256, (int*)dout); }, (double)big, t256 * 16.0);
-    snprintf(nm, 64, "coaldma row256 occ%d", occ);
-    timeit(nm, [&] { dmax4<256, false><<<grid, 64>>>((const int4*)src, t256, (int*)dout); }, (double)big, t256 * 16.0);
-    snprintf(nm, 64, "transdma row256 occ%d", occ);
-    timeit(nm, [&] { dmax4<256, true><<<grid, 64>>>((const int4*)src, t256, (int*)dout); }, (double)big, t256 * 16.0);
-    const int64_t ts = big / (2048 * 8);
-    snprintf(nm, 64, "st_trans8 occ%d", occ);
-    timeit(nm, [&] { st8<true><<<grid, 64>>>((double*)dst, ts); }, (double)big, ts * 32.0);
-    snprintf(nm, 64, "st_coal8 occ%d", occ);
-    timeit(nm, [&] { st8<false><<<grid, 64>>>((double*)dst, ts); }, (double)big, ts * 32.0);
   }
   return 0;
 }
