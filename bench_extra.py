@@ -72,7 +72,14 @@ def _c3(args, world, rank, barrier, max_over, sum_over):
     n = int(off[-1])
     r2 = np.random.default_rng(1000 + m0)
     perm = np.random.default_rng(33).permutation(S).astype(np.int32)
-    sid = perm[np.minimum(r2.zipf(1.1, size=n), S) - 1]
+    # Zipf(1.1) truncated to S ranks (rejection: redraw values > S; clamping them to rank S
+    # would pile the ~24% tail mass onto one artificial hot source)
+    z = r2.zipf(1.1, size=n)
+    bad = np.nonzero(z > S)[0]
+    while bad.size:
+        z[bad] = r2.zipf(1.1, size=bad.size)
+        bad = bad[z[bad] > S]
+    sid = perm[z - 1]
     prob = r2.random(n)
     dev = torch.device("cuda", torch.cuda.current_device())
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731

@@ -1,0 +1,96 @@
+"""GPU parity for the wide-market kernel (64 < n <= 4096, exact mode) vs the oracle.
+
+consensus_wide_kernel<NW, R> packs (sid, input index) into 32 bits, so these cases sit on
+its edges: every length bin boundary, Zipf-heavy duplicate runs (C3's source law), one
+source for a whole 4096-signal market, the largest table the packed key allows
+(S = 2^20 at P = 4096) and one past it (falls back to the LDS-sort kernel), NaN /
+out-of-range probabilities and non-positive reliabilities.  Bit-exact (==) everywhere.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as orc
+from test_gpu_consensus import _compare_vec, _dev, _run
+
+pytestmark = pytest.mark.gpu
+
+
+def _zipf_case(lens, S, seed, a=1.1, base=0, bad=True):
+    rng = np.random.default_rng(seed)
+    off = np.zeros(len(lens) + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    off += base
+    n = int(off[-1])
+    perm = rng.permutation(S).astype(np.int32)
+    z = rng.zipf(a, n)
+    sid = perm[(z - 1) % S]
+    prob = rng.random(n)
+    if bad:
+        prob[rng.random(n) < 0.001] = 1.5
+        prob[rng.random(n) < 0.001] = np.nan
+    rel = rng.uniform(-0.1, 1.0, S)
+    conf = rng.random(S)
+    present = (rng.random(S) < 0.8).astype(np.uint8)
+    return dict(offsets=off, sid=sid, prob=prob, rel=rel, conf=conf, present=present)
+
+
+def _check(g, **kw):
+    exp = orc.consensus_csr(g["offsets"], g["sid"], g["prob"], g["rel"], g["conf"], g["present"])
+    _compare_vec(_run(g, **kw), exp, g["offsets"])
+
+
+EDGES = [65, 127, 128, 129, 255, 256, 257, 511, 512, 513, 1023, 1024, 1025, 2047, 2048, 2049, 4095, 4096]
+
+
+@pytest.mark.parametrize("S,seed", [(1_000_000, 1), (5000, 2), (40, 3)])
+def test_wide_bins_zipf(S, seed):
+    rng = np.random.default_rng(100 + seed)
+    lens = np.exp(rng.uniform(np.log(65), np.log(4096), 400)).astype(np.int64)
+    lens = np.concatenate([lens, EDGES, [0, 3, 64]])
+    rng.shuffle(lens)
+    _check(_zipf_case(lens, S, seed, base=7))
+
+
+@pytest.mark.parametrize("S", [1, 2])
+def test_wide_single_long_run(S):
+    """All 4096 signals on one or two sources: run sums of thousands of terms."""
+    _check(_zipf_case(np.array([4096, 4000, 3000, 2048, 1500, 700, 300, 100]), S, 5, bad=False))
+
+
+def test_wide_key_limit_and_fallback():
+    """S = 2^20 is the largest table the 32-bit key takes at P = 4096 (top sid at the last
+    index); S = 2^20 + 1 sends the 2049..4096 bin to the LDS-sort kernel."""
+    for S in (1 << 20, (1 << 20) + 1):
+        lens = np.array([4096, 4096, 3000, 2500, 2048, 1000, 200])
+        g = _zipf_case(lens, S, 9, a=1.05)
+        g["sid"][int(g["offsets"][1]) - 1] = S - 1
+        g["sid"][int(g["offsets"][0])] = S - 1
+        _check(g)
+
+
+def test_wide_direct_csr_unplanned():
+    """bce_consensus_csr with max_len in (64, 4096]: every market (short ones too) goes
+    through one wide launch sized by max_len."""
+    from bayesian_engine import _native as N, batch
+    rng = np.random.default_rng(21)
+    lens = rng.integers(0, 3000, 120)
+    lens[:5] = [0, 1, 64, 65, 2999]
+    g = _zipf_case(lens, 20000, 21, base=3)
+    exp = orc.consensus_csr(g["offsets"], g["sid"], g["prob"], g["rel"], g["conf"], g["present"])
+    table = batch.SourceTable.from_arrays(_dev(g["rel"]), _dev(g["conf"]), _dev(g["present"]))
+    M = len(lens)
+    n = int(g["offsets"][-1])
+    off, sid, prob = _dev(g["offsets"]), _dev(g["sid"], np.int32), _dev(g["prob"])
+    res = batch._alloc(M, n, off.device, True, True)
+    L = N.lib()
+    rc = L.bce_consensus_csr(N.ptr(off), M, N.ptr(sid), N.ptr(prob), n, N.ptr(table.relconf), N.ptr(table.bits),
+                             table.n, N.ptr(None), 0, int(lens.max()), N.MODE_EXACT, N.ptr(res.consensus),
+                             N.ptr(res.confidence), N.ptr(res.total_weight), N.ptr(res.n_unique),
+                             N.ptr(res.err_idx), N.ptr(res.usid), N.ptr(res.weight), N.ptr(res.nweight),
+                             N.stream(off.device))
+    assert rc == 0, L.bce_last_error()
+    torch.cuda.synchronize()
+    out = {k: getattr(res, k).cpu().numpy() for k in ("consensus", "confidence", "total_weight", "n_unique",
+                                                      "err_idx", "usid", "weight", "nweight")}
+    _compare_vec(out, exp, g["offsets"])

@@ -19,7 +19,7 @@ table = batch.SourceTable.from_arrays(T(rel), T(conf), T(present))
 d = [T(off), T(sid), T(prob)]
 res = batch._alloc(M, M * L, d[0].device, True, True)
 lib = N.lib()
-buf = (C.c_ulonglong * 8)()
+buf = (C.c_ulonglong * 16)()
 for _ in range(3):
     batch.consensus(*d, table, max_len=L, out=res)
 torch.cuda.synchronize()
