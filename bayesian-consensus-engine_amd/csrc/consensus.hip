@@ -2338,38 +2338,80 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 8)))
           const int jj = (h + i) * NT + t;
           if (jj < u) sP[(jj)] = vw[i];  // slot jj is only read by uniques <= jj
           if (wv == 0) {
-            // 8 terms per batch, two batches in flight, each reloaded right after its adds
-            // (scheduling barriers keep the reloads one batch ahead); masked terms add +0.0,
-            // exact because these chains never hold -0.0
-            constexpr int CB = 8;
+            // Full 16-term steps run in asm: two 8-term batches in fixed registers, each
+            // reloaded right after its adds, so one batch's LDS latency hides under the
+            // other's dependent adds (the compiler would copy loop-carried batch registers
+            // behind an lgkmcnt(0)).  The < 16-term tail is added in C++ with masked
+            // terms adding +0.0 -- exact, because these chains never hold -0.0.
+            __builtin_amdgcn_s_setprio(2);  // the chain is the critical path: win VALU arbitration
             const int ce = (u - (h + i) * NT < NT) ? u - (h + i) * NT : NT;
             const double* src = buf + (lane % 3) * NT;
-            double xa[CB], xb[CB];
-#pragma unroll
-            for (int e = 0; e < CB; ++e) xa[e] = src[e];
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int e = 0; e < CB; ++e) xb[e] = src[CB + e];
-            __builtin_amdgcn_sched_barrier(0);
-            const int nfull = ce & ~(2 * CB - 1);
-            for (int e0 = 0; e0 < nfull; e0 += 2 * CB) {
-#pragma unroll
-              for (int e = 0; e < CB; ++e) acc += xa[e];
-#pragma unroll
-              for (int e = 0; e < CB; ++e) xa[e] = src[e0 + 2 * CB + e];
-              __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-              for (int e = 0; e < CB; ++e) acc += xb[e];
-#pragma unroll
-              for (int e = 0; e < CB; ++e) xb[e] = src[e0 + 3 * CB + e];
-              __builtin_amdgcn_sched_barrier(0);
+            const int nfull = ce & ~15;
+            if (nfull) {
+              unsigned addr = (unsigned)(uintptr_t)src;
+              int steps = nfull >> 4;
+              asm volatile(
+                  "ds_read_b128 v[96:99], %[ad] offset:0\n"
+                  "ds_read_b128 v[100:103], %[ad] offset:16\n"
+                  "ds_read_b128 v[104:107], %[ad] offset:32\n"
+                  "ds_read_b128 v[108:111], %[ad] offset:48\n"
+                  "ds_read_b128 v[112:115], %[ad] offset:64\n"
+                  "ds_read_b128 v[116:119], %[ad] offset:80\n"
+                  "ds_read_b128 v[120:123], %[ad] offset:96\n"
+                  "ds_read_b128 v[124:127], %[ad] offset:112\n"
+                  "1:\n"
+                  "s_waitcnt lgkmcnt(7)\n"
+                  "v_add_f64 %[acc], %[acc], v[96:97]\n"
+                  "v_add_f64 %[acc], %[acc], v[98:99]\n"
+                  "s_waitcnt lgkmcnt(6)\n"
+                  "v_add_f64 %[acc], %[acc], v[100:101]\n"
+                  "v_add_f64 %[acc], %[acc], v[102:103]\n"
+                  "s_waitcnt lgkmcnt(5)\n"
+                  "v_add_f64 %[acc], %[acc], v[104:105]\n"
+                  "v_add_f64 %[acc], %[acc], v[106:107]\n"
+                  "s_waitcnt lgkmcnt(4)\n"
+                  "v_add_f64 %[acc], %[acc], v[108:109]\n"
+                  "v_add_f64 %[acc], %[acc], v[110:111]\n"
+                  "ds_read_b128 v[96:99], %[ad] offset:128\n"
+                  "ds_read_b128 v[100:103], %[ad] offset:144\n"
+                  "ds_read_b128 v[104:107], %[ad] offset:160\n"
+                  "ds_read_b128 v[108:111], %[ad] offset:176\n"
+                  "s_waitcnt lgkmcnt(7)\n"
+                  "v_add_f64 %[acc], %[acc], v[112:113]\n"
+                  "v_add_f64 %[acc], %[acc], v[114:115]\n"
+                  "s_waitcnt lgkmcnt(6)\n"
+                  "v_add_f64 %[acc], %[acc], v[116:117]\n"
+                  "v_add_f64 %[acc], %[acc], v[118:119]\n"
+                  "s_waitcnt lgkmcnt(5)\n"
+                  "v_add_f64 %[acc], %[acc], v[120:121]\n"
+                  "v_add_f64 %[acc], %[acc], v[122:123]\n"
+                  "s_waitcnt lgkmcnt(4)\n"
+                  "v_add_f64 %[acc], %[acc], v[124:125]\n"
+                  "v_add_f64 %[acc], %[acc], v[126:127]\n"
+                  "ds_read_b128 v[112:115], %[ad] offset:192\n"
+                  "ds_read_b128 v[116:119], %[ad] offset:208\n"
+                  "ds_read_b128 v[120:123], %[ad] offset:224\n"
+                  "ds_read_b128 v[124:127], %[ad] offset:240\n"
+                  "v_add_u32 %[ad], 0x80, %[ad]\n"
+                  "s_sub_u32 %[st], %[st], 1\n"
+                  "s_cmp_lg_u32 %[st], 0\n"
+                  "s_cbranch_scc1 1b\n"
+                  "s_waitcnt lgkmcnt(0)\n"
+                  : [acc] "+v"(acc), [ad] "+v"(addr), [st] "+s"(steps)
+                  :
+                  : "memory", "scc", "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104",
+                    "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", "v114", "v115",
+                    "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123", "v124", "v125", "v126",
+                    "v127");
             }
-            if (nfull < ce) {  // tail (< 2*CB terms)
+            if (nfull < ce) {
+              double xt[16];
 #pragma unroll
-              for (int e = 0; e < CB; ++e) acc += (nfull + e < ce) ? xa[e] : 0.0;
+              for (int e = 0; e < 16; ++e) xt[e] = src[nfull + e];
 #pragma unroll
-              for (int e = 0; e < CB; ++e) acc += (nfull + CB + e < ce) ? xb[e] : 0.0;
+              for (int e = 0; e < 16; ++e) acc += (nfull + e < ce) ? xt[e] : 0.0;
             }
+            __builtin_amdgcn_s_setprio(0);
           }
           WPROF(5);
         }
