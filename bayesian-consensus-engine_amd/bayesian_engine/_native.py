@@ -107,12 +107,18 @@ def check(rc: int, what: str = "") -> None:
         raise BCEError(f"{what or 'bce call'} failed (status {rc}): {msg}")
 
 
-def ptr(t) -> C.c_void_p:
-    """Device (or host numpy) pointer of a contiguous buffer; None -> NULL."""
+def ptr(t, row_strided: bool = False) -> C.c_void_p:
+    """Device (or host numpy) pointer of a contiguous buffer; None -> NULL.
+
+    ``row_strided``: a 2-D tensor whose rows are contiguous but may be padded (the
+    callee takes the leading dimension separately)."""
     if t is None:
         return C.c_void_p(0)
     if isinstance(t, torch.Tensor):
-        assert t.is_contiguous(), "tensor must be contiguous"
+        if row_strided:
+            assert t.dim() == 2 and t.stride(1) == 1 and t.stride(0) >= t.shape[1], "rows must be contiguous"
+        else:
+            assert t.is_contiguous(), "tensor must be contiguous"
         return C.c_void_p(t.data_ptr())
     return C.c_void_p(t.ctypes.data)  # numpy (host arrays for planning calls)
 

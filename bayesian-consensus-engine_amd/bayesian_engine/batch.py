@@ -373,11 +373,11 @@ def reestimate(P: torch.Tensor, iters: int, w0: float = 0.5, w: Optional[torch.T
     hist = []
     st = N.stream(dev)
     for _ in range(iters):
-        N.check(L.bce_reestimate_consensus(N.ptr(P), A, M, ld, N.ptr(w), N.ptr(cons), N.ptr(nul), st),
+        N.check(L.bce_reestimate_consensus(N.ptr(P, row_strided=True), A, M, ld, N.ptr(w), N.ptr(cons), N.ptr(nul), st),
                 "bce_reestimate_consensus")
         agree.zero_()
         resolved.zero_()
-        N.check(L.bce_reestimate_agreement(N.ptr(P), A, M, ld, N.ptr(cons), N.ptr(nul), N.ptr(agree),
+        N.check(L.bce_reestimate_agreement(N.ptr(P, row_strided=True), A, M, ld, N.ptr(cons), N.ptr(nul), N.ptr(agree),
                                            N.ptr(resolved), st), "bce_reestimate_agreement")
         N.check(L.bce_reestimate_weights(A, N.ptr(agree), N.ptr(resolved), N.ptr(w), st),
                 "bce_reestimate_weights")

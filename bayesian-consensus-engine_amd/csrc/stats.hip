@@ -7,7 +7,8 @@
 //                          coalesced AND each lane sums in agent order, which is the
 //                          reference's sorted-source order (core.py:130-144): exact.
 //   reestimate_agreement   config 5 pass 2: per-agent count of markets whose binary vote
-//                          matches the consensus vote (market.py:298-304), ballot+popcount.
+//                          matches the consensus vote (market.py:298-304), ballot+popcount
+//                          over (agent tile x market tile) blocks, LDS-collected counts.
 #include "bce_device.hpp"
 #include "bce_internal.hpp"
 
@@ -71,9 +72,13 @@ __global__ __launch_bounds__(256) void reestimate_consensus_kernel(const double*
   null_out[m] = isnull ? 1 : 0;
 }
 
-// Block = 256 markets x AG agents per pass; each wave reduces its 64 markets with a
-// ballot, the block adds 4 popcounts, one int64 atomic per (block, agent).
-constexpr int kAgreeMarketsPerThread = 8;
+// Block = a tile of 256*kAgMT markets x kAgAT agents.  Each thread keeps its markets'
+// consensus votes in registers, streams the tile's agent rows with 4 rows x kAgMT loads
+// in flight (coalesced across lanes), reduces each row's hits with ballots, collects the
+// per-agent counts of the block in LDS and adds them to global memory once per block.
+// (Counting is exact and order-free.)
+constexpr int kAgMT = 8;    // markets per thread
+constexpr int kAgAT = 256;  // agents per block
 
 __global__ __launch_bounds__(256) void reestimate_agreement_kernel(const double* __restrict__ P,
                                                                    int64_t A, int64_t M, int64_t ld,
@@ -81,47 +86,54 @@ __global__ __launch_bounds__(256) void reestimate_agreement_kernel(const double*
                                                                    const uint8_t* __restrict__ nul,
                                                                    long long* __restrict__ agree,
                                                                    long long* __restrict__ resolved) {
+  __shared__ int32_t cntS[kAgAT];
   __shared__ int32_t part[4];
   const int tid = threadIdx.x;
   const int lane = lane_id();
   const int wv = tid >> 6;
-  const int64_t m0 = (int64_t)blockIdx.x * 256 * kAgreeMarketsPerThread;
-  bool cv[kAgreeMarketsPerThread];
-  bool ok[kAgreeMarketsPerThread];
+  const int64_t n_mt = (M + 256 * kAgMT - 1) / (256 * kAgMT);
+  const int64_t mt = blockIdx.x % n_mt;
+  const int64_t a0 = (blockIdx.x / n_mt) * kAgAT;
+  const int64_t a1 = (A < a0 + kAgAT) ? A : a0 + kAgAT;
+  const int64_t m0 = mt * 256 * kAgMT;
+  cntS[tid] = 0;
+  bool cv[kAgMT], ok[kAgMT], in[kAgMT];
   int nres = 0;
 #pragma unroll
-  for (int q = 0; q < kAgreeMarketsPerThread; ++q) {
+  for (int q = 0; q < kAgMT; ++q) {
     const int64_t m = m0 + q * 256 + tid;
-    ok[q] = m < M && nul[m] == 0;
-    cv[q] = ok[q] && cons[m] >= 0.5;
+    in[q] = m < M;
+    ok[q] = in[q] && nul[m] == 0;
+    cv[q] = ok[q] && cons[m] >= 0.5;  // market.py:298-299 with the consensus as outcome
     nres += ok[q] ? 1 : 0;
   }
-  // resolved-market count for this block (same for every agent)
-  {
+  if (a0 == 0) {  // resolved-market count, once per market tile
     int c = nres;
     for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
     if (lane == 0) part[wv] = c;
-    __syncthreads();
-    if (tid == 0) atomicAdd(reinterpret_cast<unsigned long long*>(resolved), (unsigned long long)(part[0] + part[1] + part[2] + part[3]));
-    __syncthreads();
   }
-  for (int64_t a = 0; a < A; ++a) {
-    const double* row = P + a * ld;
-    int cnt = 0;
+  __syncthreads();
+  if (a0 == 0 && tid == 0)
+    atomicAdd(reinterpret_cast<unsigned long long*>(resolved),
+              (unsigned long long)(part[0] + part[1] + part[2] + part[3]));
+  const double* base = P + m0 + tid;
+  for (int64_t a = a0; a < a1; a += 4) {
+    double v[4][kAgMT];
 #pragma unroll
-    for (int q = 0; q < kAgreeMarketsPerThread; ++q) {
-      const int64_t m = m0 + q * 256 + tid;
-      const bool hit = ok[q] && ((row[m] >= 0.5) == cv[q]);
-      cnt += __popcll(ballot(hit));
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int q = 0; q < kAgMT; ++q) v[k][q] = (a + k < a1 && in[q]) ? base[(a + k) * ld + q * 256] : 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      int cnt = 0;
+#pragma unroll
+      for (int q = 0; q < kAgMT; ++q) cnt += __popcll(ballot(ok[q] && ((v[k][q] >= 0.5) == cv[q])));
+      if (lane == 0 && cnt && a + k < a1) atomicAdd(&cntS[a + k - a0], cnt);
     }
-    if (lane == 0) part[wv] = cnt;
-    __syncthreads();
-    if (tid == 0) {
-      const int s = part[0] + part[1] + part[2] + part[3];
-      if (s) atomicAdd(reinterpret_cast<unsigned long long*>(&agree[a]), (unsigned long long)s);
-    }
-    __syncthreads();
   }
+  __syncthreads();
+  if (tid < a1 - a0 && cntS[tid]) atomicAdd(reinterpret_cast<unsigned long long*>(&agree[a0 + tid]),
+                                           (unsigned long long)cntS[tid]);
 }
 
 __global__ void reestimate_weights_kernel(int64_t A, const long long* agree, const long long* resolved,
@@ -174,8 +186,10 @@ extern "C" int bce_reestimate_agreement(const double* P, int64_t A, int64_t M, i
   BCE_REQUIRE(A > 0 && M >= 0 && ld >= M, "reestimate_agreement: bad shape");
   if (M == 0) return BCE_OK;
   BCE_REQUIRE(P && consensus && null_in && agreement && resolved, "reestimate_agreement: NULL");
-  const int64_t per_block = 256 * kAgreeMarketsPerThread;
-  hipLaunchKernelGGL(reestimate_agreement_kernel, dim3((unsigned)((M + per_block - 1) / per_block)),
+  const int64_t n_mt = (M + 256 * kAgMT - 1) / (256 * kAgMT);
+  const int64_t n_at = (A + kAgAT - 1) / kAgAT;
+  BCE_REQUIRE(n_mt * n_at < (1ll << 31), "reestimate_agreement: grid too large");
+  hipLaunchKernelGGL(reestimate_agreement_kernel, dim3((unsigned)(n_mt * n_at)),
                      dim3(256), 0, as_stream(stream), P, A, M, ld, consensus, null_in,
                      reinterpret_cast<long long*>(agreement), reinterpret_cast<long long*>(resolved));
   return check_launch("reestimate_agreement_kernel");

@@ -342,6 +342,27 @@ def test_reestimate_c5_slice():
         assert np.array_equal(hist[k][3].cpu().numpy(), g["weights"][k])
 
 
+@pytest.mark.parametrize("A,M,ld_pad", [(600, 5000, 0), (257, 2049, 3), (5, 700, 1)])
+def test_reestimate_vs_oracle_tiles(A, M, ld_pad):
+    """Several agent tiles (256) and market tiles (2048), ragged edges, padded rows."""
+    import torch
+    from bayesian_engine import batch
+    from oracle import oracle as orc
+    rng = np.random.default_rng(A * 7 + M)
+    P = rng.beta(2, 2, size=(A, M))
+    P[:, rng.random(M) < 0.02] = 0.5
+    K = 2
+    w_exp, c_exp, n_exp, a_exp = orc.reestimate(P, K)
+    full = np.zeros((A, M + ld_pad))
+    full[:, :M] = P
+    Pt = torch.from_numpy(full).cuda()[:, :M]
+    w, cons, nul, agree, _ = batch.reestimate(Pt, K)
+    assert np.array_equal(cons.cpu().numpy(), c_exp[-1])
+    assert np.array_equal(nul.cpu().numpy(), n_exp[-1])
+    assert np.array_equal(agree.cpu().numpy(), a_exp[-1])
+    assert np.array_equal(w.cpu().numpy(), w_exp)
+
+
 def test_c4_replay_slice():
     """Config-4 replay through the fused replay_step kernel vs the reference trace."""
     import torch
