@@ -81,6 +81,9 @@
 #ifndef BCE_WIDE
 #define BCE_WIDE 1  // register-sort kernel for 64 < n <= 4096 (exact mode)
 #endif
+#ifndef BCE_WIDE_HR
+#define BCE_WIDE_HR 4  // wide kernel: rounds of NT uniques computed into registers at once
+#endif
 #ifndef BCE_STAGE
 #define BCE_STAGE 1  // LDS-staged 16-B input loads for contiguous tiles
 #endif
@@ -2255,7 +2258,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 8)))
     // Up to HR rounds of NT uniques are computed into registers at once (all relconf
     // gathers in flight together), then staged round by round through two LDS buffers
     // while wave 0 carries the three left-to-right chains on lanes 0..2.
-    constexpr int HR = (R < 4) ? R : 4;
+    constexpr int HR = (R < BCE_WIDE_HR) ? R : BCE_WIDE_HR;
     double acc = 0.0;  // wave 0: lane 0 = total weight, 1 = sum avg*w, 2 = sum c*w
     const int nr = (u + NT - 1) / NT;
     for (int h = 0; h < nr; h += HR) {

@@ -42,8 +42,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=50)
     p.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
     p.add_argument("--markets", type=int, default=1_000_000)
     p.add_argument("--len", type=int, default=32)
