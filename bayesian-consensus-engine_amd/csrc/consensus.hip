@@ -1364,6 +1364,12 @@ void consensus_pipe_kernel(ConsArgs a) {
   if (w < NL) {
     // ================================ loaders =========================================
     // loader w owns sequences i = w, w + NL, ... (slot i % R); k counts its own tiles
+#if BCE_PIPE_PROF
+    unsigned long long lp_t = __builtin_amdgcn_s_memtime(), lp[4] = {0, 0, 0, 0};
+#define LPROF(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); lp[k] += t_ - lp_t; lp_t = t_; } while (0)
+#else
+#define LPROF(k) do {} while (0)
+#endif
     const int64_t Nf4 = a.n_signals & ~3ll, Nf2 = a.n_signals & ~1ll;
     const int64_t clamp_s = (Nf4 - 4 > 0) ? Nf4 - 4 : 0;  // host: n_signals >= 4
     const int64_t clamp_p = (Nf2 - 2 > 0) ? Nf2 - 2 : 0;
@@ -1436,6 +1442,7 @@ void consensus_pipe_kernel(ConsArgs a) {
           }
         }
       }
+      LPROF(0);  // waiting for a free slot (incl. publishing what was in flight)
       if (i >= my_tiles) {  // end markers: one per compute wave
         if (pending >= 0) {
           __builtin_amdgcn_s_waitcnt(0x0F70);
@@ -1502,10 +1509,13 @@ void consensus_pipe_kernel(ConsArgs a) {
         const int d = tb + lane;
         dma_b32(og + ((d < ndw) ? d : 0), &sOffs[s][tb]);
       }
+      LPROF(1);  // issuing this tile's DMA
       if (pending >= 0) {  // the previous tile has landed once only this one is in flight
         __builtin_amdgcn_s_waitcnt((NDMA & 15) | (7 << 4) | (15 << 8) | ((NDMA >> 4) << 14));
+        LPROF(2);  // waiting for the previous tile to land
         finish(pending % R, pend_B, pend_E);
-            publish(pending, pend_t);
+        publish(pending, pend_t);
+        LPROF(3);  // validation + publish
       }
       pending = (int)i;
       pend_t = t;
@@ -1515,8 +1525,13 @@ void consensus_pipe_kernel(ConsArgs a) {
     if (pending >= 0) {
       __builtin_amdgcn_s_waitcnt(0x0F70);
       finish(pending % R, pend_B, pend_E);
-            publish(pending, pend_t);
+      publish(pending, pend_t);
     }
+#if BCE_PIPE_PROF
+    if (lane == 0)
+      for (int q = 0; q < 4; ++q) atomicAdd(&g_pipe_prof[8 + q], lp[q]);
+#endif
+#undef LPROF
     return;
   }
 

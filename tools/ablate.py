@@ -22,8 +22,7 @@ VARIANTS = {
     "pipe": [],
     "pipe_c5": ["-DBCE_PIPE_C32=5"],
     "pipe_ring24": ["-DBCE_PIPE_RING=24"],
-    "pipe_c5_ring24": ["-DBCE_PIPE_C32=5", "-DBCE_PIPE_RING=24"],
-    "pipe_r5": ["-DBCE_PIPE_R32=5"],
+    "pipe_l2": ["-DBCE_PIPE_L=2"],
     "lpm": ["-DBCE_FLAT=0"],
     "pipe_noout": ["-DBCE_ABLATE=8"],
     "pipe_nogather": ["-DBCE_ABLATE=2"],

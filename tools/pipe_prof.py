@@ -36,3 +36,8 @@ tot = sum(v[:5])
 print(f"compute waves {v[5] // R}  tiles {tiles}")
 for k, nm in enumerate(names):
     print(f"{nm:12s} {v[k] / R / tiles:10.0f} cyc/tile  {100 * v[k] / tot:5.1f} %")
+lnames = ["wait_free_slot", "issue_dma", "wait_landed", "validate_publish"]
+ltot = sum(v[8:12])
+print("loader wave, per tile:")
+for k, nm in enumerate(lnames):
+    print(f"{nm:16s} {v[8 + k] / R / tiles:10.0f} cyc/tile  {100 * v[8 + k] / max(ltot, 1):5.1f} %")
