@@ -962,13 +962,20 @@ __device__ __forceinline__ void wait_lgkm0() {
 // it, which would make the copy-out of tile k wait for the DMA of tile k+1.  The stream
 // kernel orders its images itself (one explicit vmcnt(0) before the image is read; the
 // staging rows are never DMA targets), so the DMA is hidden from that pass.
+// Cache policy of the streamed (read-once) LDS-DMA loads ("nt", "sc1 nt", ... measured no
+// faster than the default on C2: the source table's gathers are not losing lines to them).
+#ifndef BCE_DMA_CP
+#define BCE_DMA_CP ""
+#endif
 __device__ __forceinline__ void dma_b128(const void* g, const void* lds) {
   const uint32_t l = (uint32_t)(uintptr_t)lds;
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(l), "v"(g) : "memory", "m0");
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off " BCE_DMA_CP ::"s"(l), "v"(g)
+               : "memory", "m0");
 }
 __device__ __forceinline__ void dma_b32(const void* g, const void* lds) {
   const uint32_t l = (uint32_t)(uintptr_t)lds;
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off" ::"s"(l), "v"(g) : "memory", "m0");
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off " BCE_DMA_CP ::"s"(l), "v"(g)
+               : "memory", "m0");
 }
 
 template <int G, int TM, int WPB, int CH>
