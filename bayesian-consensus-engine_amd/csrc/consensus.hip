@@ -1302,6 +1302,12 @@ __device__ __forceinline__ int ldsflag(int* f) {
 #endif
 // Slots R >= C + 2: with one spare slot the ring is load-latency bound (a released slot
 // must be refilled within tile_time / C); two spares keep two tiles in flight.
+#ifndef BCE_PIPE_LPRIO
+#define BCE_PIPE_LPRIO 0  // loader wave priority (s_setprio)
+#endif
+#ifndef BCE_PIPE_NTS
+#define BCE_PIPE_NTS 0  // nontemporal per-unique output stores
+#endif
 #ifndef BCE_PIPE_L
 #define BCE_PIPE_L 1  // loader waves (each keeps its own tiles in flight; 2 measured slower: TA contention)
 #endif
@@ -1370,6 +1376,7 @@ void consensus_pipe_kernel(ConsArgs a) {
 
   if (w < NL) {
     // ================================ loaders =========================================
+    if (BCE_PIPE_LPRIO) __builtin_amdgcn_s_setprio(BCE_PIPE_LPRIO);
     // loader w owns sequences i = w, w + NL, ... (slot i % R); k counts its own tiles
 #if BCE_PIPE_PROF
     unsigned long long lp_t = __builtin_amdgcn_s_memtime(), lp[4] = {0, 0, 0, 0};
@@ -1408,7 +1415,7 @@ void consensus_pipe_kernel(ConsArgs a) {
       for (int k = 0; k < TS / kWave; ++k) {
         const int i = k * kWave + lane;
         const double p = sProb[s][d + ((i < nb) ? i : 0)];
-        const unsigned long long m = ballot(i < nb && (p < 0.0 || p > 1.0));
+        const unsigned long long m = (BCE_ABLATE & 32) ? 0ull : ballot(i < nb && (p < 0.0 || p > 1.0));
         sBad[s][2 * k] = (uint32_t)m;
         sBad[s][2 * k + 1] = (uint32_t)(m >> 32);
       }
@@ -1790,9 +1797,18 @@ void consensus_pipe_kernel(ConsArgs a) {
             const double n1 = (tot > 0.0) ? w1[b] / tot : 0.0;  // (cold bit: core.py:167-170)
             const int64_t pos = B + r[b] + k2;
             if (v1[b]) {
+#if BCE_PIPE_NTS
+              // streaming outputs are never re-read by this launch: nontemporal stores
+              typedef unsigned v2u __attribute__((ext_vector_type(2)));
+              typedef double v2d __attribute__((ext_vector_type(2)));
+              __builtin_nontemporal_store((v2u){x0, x1}, reinterpret_cast<v2u*>(a.usid + pos));
+              __builtin_nontemporal_store((v2d){w0[b], w1[b]}, reinterpret_cast<v2d*>(a.weight + pos));
+              __builtin_nontemporal_store((v2d){n0, n1}, reinterpret_cast<v2d*>(a.nweight + pos));
+#else
               *reinterpret_cast<uint2*>(a.usid + pos) = make_uint2(x0, x1);
               *reinterpret_cast<double2*>(a.weight + pos) = make_double2(w0[b], w1[b]);
               *reinterpret_cast<double2*>(a.nweight + pos) = make_double2(n0, n1);
+#endif
             } else if (v0[b]) {
               a.usid[pos] = (int32_t)x0;
               a.weight[pos] = w0[b];

@@ -27,6 +27,11 @@ VARIANTS = {
     "pipe_noout": ["-DBCE_ABLATE=8"],
     "pipe_nogather": ["-DBCE_ABLATE=2"],
     "pipe_prof": ["-DBCE_PIPE_PROF=1"],
+    "pipe_lprio3": ["-DBCE_PIPE_LPRIO=3"],
+    "pipe_lprio1": ["-DBCE_PIPE_LPRIO=1"],
+    "pipe_nts": ["-DBCE_PIPE_NTS=1"],
+    "pipe_nocheck": ["-DBCE_ABLATE=32"],
+    "pipe_nts_lprio3": ["-DBCE_PIPE_NTS=1", "-DBCE_PIPE_LPRIO=3"],
 }
 SRCS = ["capi.hip", "consensus.hip", "elementwise.hip", "tiebreak.hip", "stats.hip"]
 
