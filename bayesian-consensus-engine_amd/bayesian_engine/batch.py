@@ -357,6 +357,90 @@ def agreement_stats(offsets, sid, prob, outcome, n_sources: int, correct=None, t
     return correct, total
 
 
+# ---------------------------------------------------------------------------------------
+# namespaced fallback (reliability_abstraction.py:119-188) and cross-market aggregation
+# ---------------------------------------------------------------------------------------
+@dataclass
+class ScopeTable:
+    """One namespace scope of the store (rows of one market_id key) over a rank space:
+    rel, conf fp64[S], t_us int64[S] (NO_TIMESTAMP = unparseable), has u8[S] = a row with a
+    truthy updated_at exists (the ``if record.updated_at`` test)."""
+
+    rel: torch.Tensor
+    conf: torch.Tensor
+    t_us: torch.Tensor
+    has: torch.Tensor
+
+
+NS_MARKET, NS_DOMAIN, NS_GLOBAL, NS_COLD = 0, 1, 2, 3
+
+
+def namespace_resolve(scopes: Sequence[Optional[ScopeTable]], now_us: int, apply_decay: bool = True,
+                      mark_cold: bool = False, names: Optional[Sequence[str]] = None,
+                      half_life_days: float = DECAY_HALF_LIFE_DAYS, min_rel: float = DECAY_MINIMUM):
+    """Fallback chain market -> domain -> global -> cold start for every source in one launch
+    (bce_namespace_resolve).  ``scopes`` = [market, domain, global], None = not requested.
+    Returns (SourceTable ready for :func:`consensus`, scope u8[S] with NS_* codes)."""
+    L = N.require_gpu()
+    sc = list(scopes) + [None] * (3 - len(scopes))
+    live = [x for x in sc if x is not None]
+    if live:
+        S = live[0].rel.numel()
+        dev = live[0].rel.device
+    else:
+        S = len(names) if names is not None else 0
+        dev = N.device()
+    relconf = torch.empty((max(S, 1), 2), dtype=torch.float64, device=dev)
+    bits = torch.zeros(max((S + 31) // 32, 1), dtype=torch.int32, device=dev)
+    scope = torch.empty(max(S, 1), dtype=torch.uint8, device=dev)
+    args, keep = [], []
+    for x in sc:
+        if x is None:
+            args += [None] * 4
+        else:
+            assert x.rel.numel() == S and x.conf.numel() == S and x.has.numel() == S, "scope sizes differ"
+            arrs = (x.rel.to(torch.float64).contiguous(), x.conf.to(torch.float64).contiguous(),
+                    x.t_us.to(torch.int64).contiguous(), x.has.to(torch.uint8).contiguous())
+            keep.append(arrs)  # alive until the launch is enqueued
+            args += [N.ptr(a) for a in arrs]
+    N.check(L.bce_namespace_resolve(S, *args, int(bool(apply_decay)), int(now_us), float(half_life_days),
+                                    float(min_rel), DEFAULT_RELIABILITY, DEFAULT_CONFIDENCE, int(bool(mark_cold)),
+                                    N.ptr(relconf), N.ptr(bits), N.ptr(scope), N.stream(dev)),
+            "bce_namespace_resolve")
+    table = SourceTable(relconf, bits, list(names) if names is not None else [""] * S)
+    return table, scope[:S]
+
+
+@dataclass
+class AggregateResult:
+    """Per group: weighted_average, median, majority, mean confidence (NaN where no member
+    has a consensus) and the number of members with a consensus."""
+
+    wavg: torch.Tensor
+    median: torch.Tensor
+    majority: torch.Tensor
+    mean_conf: torch.Tensor
+    n_included: torch.Tensor
+
+
+def aggregate(group_offsets: torch.Tensor, members: torch.Tensor, consensus: torch.Tensor,
+              confidence: torch.Tensor, has_consensus: torch.Tensor, median: bool = True) -> AggregateResult:
+    """CrossMarketAggregator.aggregate_consensus (market.py:340-408) for many member groups
+    in one launch (bce_aggregate_groups); sums in list order, bit-exact."""
+    L = N.require_gpu()
+    dev = consensus.device
+    G = group_offsets.numel() - 1
+    f64 = dict(dtype=torch.float64, device=dev)
+    r = AggregateResult(torch.empty(max(G, 1), **f64), torch.empty(max(G, 1), **f64),
+                        torch.empty(max(G, 1), **f64), torch.empty(max(G, 1), **f64),
+                        torch.empty(max(G, 1), dtype=torch.int64, device=dev))
+    N.check(L.bce_aggregate_groups(N.ptr(group_offsets), G, N.ptr(members), consensus.numel(), N.ptr(consensus),
+                                   N.ptr(confidence), N.ptr(has_consensus), N.ptr(r.wavg),
+                                   N.ptr(r.median) if median else None, N.ptr(r.majority), N.ptr(r.mean_conf),
+                                   N.ptr(r.n_included), N.stream(dev)), "bce_aggregate_groups")
+    return AggregateResult(*(t[:G] for t in (r.wavg, r.median, r.majority, r.mean_conf, r.n_included)))
+
+
 def reestimate(P: torch.Tensor, iters: int, w0: float = 0.5, w: Optional[torch.Tensor] = None,
                keep_history: bool = False):
     """Config 5: ``iters`` rounds of consensus <-> reliability on agent-major P [A, M]."""

@@ -12,8 +12,12 @@ The multi-market layer is where the batched engine pays off:
 * ``CrossMarketAggregator.summarize_sources`` (market.py:256-321) -- the per-source
   correct/total counts run in the ``bce_agreement_stats`` kernel (exact int atomics).
 
-Metadata (MarketId glob matching, status, category summaries) and the cross-market
-``aggregate_consensus`` (not yet a kernel) are host Python with the
+* ``CrossMarketAggregator.aggregate_consensus`` (market.py:340-408) --
+  weighted_average / median / majority over member groups in the ``bce_aggregate_groups``
+  kernel (list-order sums, exact radix-select median); ``aggregate_many`` does many
+  pattern lists in one launch.
+
+Metadata (MarketId glob matching, status, category summaries) is host Python with the
 reference's semantics.
 """
 from __future__ import annotations
@@ -325,34 +329,57 @@ class CrossMarketAggregator:
                 "open": len(open_markets), "markets": [str(m.id) for m in markets]}
 
     def aggregate_consensus(self, patterns: List[str], method: str = "weighted_average") -> Dict[str, Any]:
-        """Cross-market aggregation (market.py:338-408); host-side."""
-        markets: List[Market] = []
-        for pattern in patterns:
-            markets.extend(self._store.list_markets(pattern=pattern))
-        if not markets:
-            return {"schemaVersion": "1.0.0", "consensus": None, "confidence": 0.0, "marketsIncluded": 0}
-        consensuses = []
-        for market in markets:
-            if market.consensus_result and market.consensus_result.get("consensus") is not None:
-                consensuses.append({"marketId": str(market.id), "consensus": market.consensus_result["consensus"],
-                                    "confidence": market.consensus_result.get("confidence", 0.5)})
-        if not consensuses:
-            return {"schemaVersion": "1.0.0", "consensus": None, "confidence": 0.0,
-                    "marketsIncluded": len(markets)}
-        if method == "weighted_average":
-            total_weight = sum(c["confidence"] for c in consensuses)
-            if total_weight == 0:
-                aggregated = sum(c["consensus"] for c in consensuses) / len(consensuses)
+        """Cross-market aggregation (market.py:338-408), computed by bce_aggregate_groups."""
+        return self.aggregate_many([patterns], method)[0]
+
+    def aggregate_many(self, pattern_lists: List[List[str]], method: str = "weighted_average") -> List[Dict[str, Any]]:
+        """aggregate_consensus for many pattern lists in ONE kernel launch: each list is a
+        member group (markets in list_markets order per pattern, duplicates kept,
+        market.py:355-357); the sums run in that order on the GPU (bit-exact)."""
+        groups: List[List[int]] = []
+        index: Dict[str, int] = {}
+        cons: List[float] = []
+        conf: List[float] = []
+        has: List[int] = []
+        for patterns in pattern_lists:
+            members: List[int] = []
+            for pattern in patterns:
+                for market in self._store.list_markets(pattern=pattern):
+                    key = str(market.id)
+                    if key not in index:
+                        index[key] = len(cons)
+                        res = market.consensus_result
+                        ok = bool(res) and res.get("consensus") is not None  # market.py:369-370
+                        cons.append(float(res["consensus"]) if ok else 0.0)
+                        conf.append(float(res.get("confidence", 0.5)) if ok else 0.0)
+                        has.append(1 if ok else 0)
+                    members.append(index[key])
+            groups.append(members)
+        empty = {"schemaVersion": "1.0.0", "consensus": None, "confidence": 0.0}
+        if not any(has[m] for g in groups for m in g):
+            return [dict(empty, marketsIncluded=len(g)) for g in groups]
+        if method not in ("weighted_average", "median", "majority"):
+            for g in groups:  # the reference raises only once a group has consensuses
+                if any(has[m] for m in g):
+                    raise ValueError(f"Unknown aggregation method: {method}")
+        N.require_gpu()
+        dev = N.device()
+        T = lambda a: torch.from_numpy(a).to(dev)  # noqa: E731
+        goff = np.zeros(len(groups) + 1, np.int64)
+        goff[1:] = np.cumsum([len(g) for g in groups])
+        flat = np.array([m for g in groups for m in g], np.int64)
+        r = batch.aggregate(T(goff), T(flat if flat.size else np.zeros(1, np.int64)), T(np.array(cons, np.float64)),
+                            T(np.array(conf, np.float64)), T(np.array(has, np.uint8)), median=method == "median")
+        pick = {"weighted_average": r.wavg, "median": r.median, "majority": r.majority}[method].cpu().numpy()
+        mconf = r.mean_conf.cpu().numpy()
+        k = r.n_included.cpu().numpy()
+        out = []
+        for gi, g in enumerate(groups):
+            if not g:
+                out.append(dict(empty, marketsIncluded=0))
+            elif k[gi] == 0:
+                out.append(dict(empty, marketsIncluded=len(g)))
             else:
-                aggregated = sum(c["consensus"] * c["confidence"] for c in consensuses) / total_weight
-        elif method == "median":
-            sorted_cons = sorted(c["consensus"] for c in consensuses)
-            aggregated = sorted_cons[len(sorted_cons) // 2]
-        elif method == "majority":
-            votes = [1 if c["consensus"] >= 0.5 else 0 for c in consensuses]
-            aggregated = sum(votes) / len(votes)
-        else:
-            raise ValueError(f"Unknown aggregation method: {method}")
-        return {"schemaVersion": "1.0.0", "consensus": aggregated,
-                "confidence": sum(c["confidence"] for c in consensuses) / len(consensuses),
-                "marketsIncluded": len(consensuses), "method": method}
+                out.append({"schemaVersion": "1.0.0", "consensus": float(pick[gi]), "confidence": float(mconf[gi]),
+                            "marketsIncluded": int(k[gi]), "method": method})
+        return out

@@ -159,6 +159,66 @@ __global__ __launch_bounds__(256) void replay_step_kernel(int64_t n, double* __r
   }
 }
 
+// NamespacedReliabilityStore.get_reliability for every source at once
+// (reliability_abstraction.py:119-188): the first scope (market, domain, global) whose row
+// has a truthy updated_at supplies the record -- decayed as
+// SQLiteReliabilityStore.get_reliability does (reliability.py:110-131) -- else the
+// cold-start defaults (:177-186).  One pass writes the packed consensus table directly.
+struct NsScope {
+  const double* rel;
+  const double* conf;
+  const int64_t* t_us;
+  const uint8_t* has;
+};
+struct NsArgs {
+  NsScope sc[3];
+  int n_scopes;  // leading non-NULL scopes after compaction (host)
+  uint8_t scope_code[3];
+  int apply_decay;
+  int mark_cold;
+  DecayConst k;
+  double2* relconf;
+  uint32_t* bits;
+  uint8_t* scope;
+};
+
+__global__ __launch_bounds__(256) void namespace_resolve_kernel(int64_t n, NsArgs a) {
+  // whole waves walk 64 consecutive sources so the present bits come from one ballot
+  for (int64_t base = (int64_t)blockIdx.x * 256; base < n; base += (int64_t)gridDim.x * 256) {
+    const int64_t s = base + threadIdx.x;
+    const bool in = s < n;
+    double r = a.k.default_rel, c = a.k.default_conf;
+    int code = 3;  // cold start
+    if (in) {
+      // the `has` bytes of every scope are independent loads: issue them together
+      uint8_t h[3] = {0, 0, 0};
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        if (q < a.n_scopes) h[q] = a.sc[q].has[s];
+      int pick = -1;
+#pragma unroll
+      for (int q = 2; q >= 0; --q)
+        if (q < a.n_scopes && h[q]) pick = q;
+      if (pick >= 0) {
+        const NsScope& sc = a.sc[pick];
+        r = sc.rel[s];
+        c = sc.conf[s];
+        if (a.apply_decay) r = decayed(r, sc.t_us[s], a.k);
+        code = a.scope_code[pick];
+      }
+      if (a.relconf) a.relconf[s] = make_double2(r, c);
+      if (a.scope) a.scope[s] = (uint8_t)code;
+    }
+    if (a.bits) {
+      const unsigned long long m = __ballot(in && (!a.mark_cold || code != 3));
+      const int ln = (int)(threadIdx.x & 63);
+      const int64_t w0 = (base + (threadIdx.x & ~63)) >> 5;
+      const int64_t nw = (n + 31) >> 5;
+      if (ln < 2 && w0 + ln < nw) a.bits[w0 + ln] = (uint32_t)(m >> (32 * ln));
+    }
+  }
+}
+
 static int grid_for(int64_t work, int threads) {
   int64_t g = (work + threads - 1) / threads;
   const int64_t cap = (int64_t)cu_count() * 16;
@@ -222,4 +282,37 @@ extern "C" int bce_replay_step(int64_t n, double* rel, double* conf, int64_t* t_
   hipLaunchKernelGGL(replay_step_kernel, dim3(grid_for(n / 2 + 1, 256)), dim3(256), 0,
                      as_stream(stream), n, rel, conf, t_us, present, flags2, k, view);
   return check_launch("replay_step_kernel");
+}
+
+extern "C" int bce_namespace_resolve(int64_t n, const double* rel0, const double* conf0,
+                                     const int64_t* t0, const uint8_t* has0, const double* rel1,
+                                     const double* conf1, const int64_t* t1, const uint8_t* has1,
+                                     const double* rel2, const double* conf2, const int64_t* t2,
+                                     const uint8_t* has2, int apply_decay, int64_t now_us,
+                                     double half_life_days, double min_rel, double default_rel,
+                                     double default_conf, int mark_cold, double* relconf,
+                                     uint32_t* present_bits, uint8_t* scope, void* stream) {
+  BCE_REQUIRE(n >= 0, "namespace_resolve: n < 0");
+  if (n == 0) return BCE_OK;
+  BCE_REQUIRE(relconf || present_bits || scope, "namespace_resolve: no output");
+  BCE_REQUIRE(relconf == nullptr || (uintptr_t)relconf % 16 == 0,
+              "namespace_resolve: relconf must be 16-byte aligned");
+  NsArgs a{};
+  const NsScope in[3] = {{rel0, conf0, t0, has0}, {rel1, conf1, t1, has1}, {rel2, conf2, t2, has2}};
+  for (int q = 0; q < 3; ++q) {
+    if (in[q].rel == nullptr) continue;  // scope not requested (falsy market_id / domain)
+    BCE_REQUIRE(in[q].conf && in[q].has && (in[q].t_us || !apply_decay),
+                "namespace_resolve: scope %d: NULL array", q);
+    a.scope_code[a.n_scopes] = (uint8_t)q;
+    a.sc[a.n_scopes++] = in[q];
+  }
+  a.apply_decay = apply_decay;
+  a.mark_cold = mark_cold;
+  a.k = DecayConst{now_us, half_life_days, min_rel, default_rel, default_conf};
+  a.relconf = reinterpret_cast<double2*>(relconf);
+  a.bits = present_bits;
+  a.scope = scope;
+  hipLaunchKernelGGL(namespace_resolve_kernel, dim3(grid_for(n, 256)), dim3(256), 0,
+                     as_stream(stream), n, a);
+  return check_launch("namespace_resolve_kernel");
 }

@@ -159,6 +159,27 @@ int bce_replay_step(int64_t n, double* rel, double* conf, int64_t* t_us, uint8_t
                     double min_rel, double default_rel, double default_conf, double* view,
                     void* stream);
 
+/* ---- namespaced fallback: NamespacedReliabilityStore.get_reliability ----------------
+ * Replaces reliability_abstraction.py:119-188 for every source of a rank space at once.
+ * Up to three scope tables in precedence order: scope 0 = market (the row keyed by
+ * market_id), 1 = domain ("__domain__:<domain>"), 2 = global ("__global__"); a NULL rel
+ * skips the scope, as a falsy market_id / domain does (:136, :150).  has[s] != 0 iff the
+ * scope holds a row with a truthy updated_at (the `if record.updated_at:` tests).  The
+ * first scope with has[s] supplies (reliability, confidence); the reliability is decayed
+ * at now_us when apply_decay, as SQLiteReliabilityStore.get_reliability does
+ * (reliability.py:114-123; t_us == BCE_NO_TIMESTAMP = unparseable = no decay).  No scope
+ * => the cold-start defaults (:177-186).  Outputs (each nullable, at least one given):
+ * relconf[2*n] = the packed consensus table, present_bits = bit set for every source
+ * (mark_cold = 0: callers put every sourceId in the dict) or only for sources that
+ * resolved to a stored row (mark_cold = 1), scope[s] = 0/1/2, or 3 for cold start. */
+int bce_namespace_resolve(int64_t n, const double* rel0, const double* conf0, const int64_t* t0,
+                          const uint8_t* has0, const double* rel1, const double* conf1,
+                          const int64_t* t1, const uint8_t* has1, const double* rel2,
+                          const double* conf2, const int64_t* t2, const uint8_t* has2,
+                          int apply_decay, int64_t now_us, double half_life_days, double min_rel,
+                          double default_rel, double default_conf, int mark_cold, double* relconf,
+                          uint32_t* present_bits, uint8_t* scope, void* stream);
+
 /* ---- tie-break: DeterministicTieBreaker.resolve (tiebreak.py:73-152) per market -----
  * Per signal: pred (AgentSignal.prediction), conf, weight, rel (reliability_score).
  * Per market: winner (rounded group key, or the raw prediction for a single agent),
@@ -188,6 +209,20 @@ int bce_tiebreak_csr_long(const int64_t* offsets, int64_t n_markets, const int32
 int bce_agreement_stats(const int64_t* offsets, int64_t n_markets, const int32_t* sid,
                         const double* prob, const int8_t* outcome, int32_t* correct,
                         int32_t* total, void* stream);
+
+/* ---- cross-market aggregation: CrossMarketAggregator.aggregate_consensus ------------
+ * (market.py:340-408) for n_groups groups at once.  Group g is the ordered member list
+ * members[group_offsets[g] .. group_offsets[g+1]) of market indices (< n_markets; the
+ * markets matched by the patterns in list_markets order, duplicates kept, :355-357).
+ * has_consensus[m] != 0 iff market m has a consensus result whose consensus is not None
+ * (:369-375).  Per group (outputs nullable): wavg = weighted_average (:386-393), median
+ * = sorted(consensus)[k // 2] (:394-397), majority (:398-401), mean_conf = the result's
+ * confidence (:407), n_included = k.  k == 0 => the float outputs are NaN (the reference
+ * returns consensus None).  Sums are left to right in list order: bit-exact. */
+int bce_aggregate_groups(const int64_t* group_offsets, int64_t n_groups, const int64_t* members,
+                         int64_t n_markets, const double* consensus, const double* confidence,
+                         const uint8_t* has_consensus, double* wavg, double* median,
+                         double* majority, double* mean_conf, int64_t* n_included, void* stream);
 
 /* ---- re-estimation (config 5): consensus <-> reliability over a dense matrix --------
  * P is agent-major [A][ld] fp64 (column m of market m; ld >= M).  One pass:

@@ -300,3 +300,70 @@ void orc_reestimate(const double* P, int64_t A, int64_t M, int iters, double* w,
     free(corr);
     free(tot);
 }
+
+/* reliability_abstraction.py:119-188 (NamespacedReliabilityStore.get_reliability) for every
+ * source: scopes in precedence order (market, domain, global; rel[q] == NULL = scope not
+ * requested), first scope with has[q][s] wins (reliability decayed via
+ * reliability.py:114-123 when apply_decay), else cold start.  scope_out 0/1/2, 3 = cold. */
+void orc_namespace_resolve(int64_t n, const double* const rel[3], const double* const conf[3],
+                           const int64_t* const t_us[3], const uint8_t* const has[3],
+                           int apply_decay, int64_t now_us, double half_life_days, double min_rel,
+                           double default_rel, double default_conf, double* rel_out,
+                           double* conf_out, uint8_t* scope_out) {
+    for (int64_t s = 0; s < n; ++s) {
+        double r = default_rel, c = default_conf;
+        int code = 3;
+        for (int q = 0; q < 3; ++q) {
+            if (rel[q] == NULL || !has[q][s]) continue;
+            r = rel[q][s];
+            c = conf[q][s];
+            if (apply_decay) {
+                const double e = orc_days_since(now_us, t_us[q][s]);
+                if (e > 0) r = orc_apply_decay(r, e, half_life_days, min_rel);
+            }
+            code = q;
+            break;
+        }
+        rel_out[s] = r;
+        conf_out[s] = c;
+        scope_out[s] = (uint8_t)code;
+    }
+}
+
+static int cmp_f64(const void* a, const void* b) {
+    const double x = *(const double*)a, y = *(const double*)b;
+    return (x < y) ? -1 : (x > y) ? 1 : 0;
+}
+
+/* market.py:340-408 (CrossMarketAggregator.aggregate_consensus) per member group:
+ * k = members with a consensus; sums left to right in list order from 0.0. */
+void orc_aggregate_groups(const int64_t* goff, int64_t n_groups, const int64_t* members,
+                          const double* cons, const double* conf, const uint8_t* has,
+                          double* wavg, double* median, double* majority, double* mean_conf,
+                          int64_t* n_included) {
+    for (int64_t g = 0; g < n_groups; ++g) {
+        double tconf = 0.0, tcons = 0.0, tprod = 0.0;
+        int64_t k = 0, votes = 0;
+        double* vals = (double*)malloc(sizeof(double) * (size_t)(goff[g + 1] - goff[g] + 1));
+        for (int64_t i = goff[g]; i < goff[g + 1]; ++i) {
+            const int64_t m = members[i];
+            if (!has[m]) continue;
+            tconf = tconf + conf[m];
+            tcons = tcons + cons[m];
+            tprod = tprod + cons[m] * conf[m];
+            votes += cons[m] >= 0.5;
+            vals[k++] = cons[m];
+        }
+        n_included[g] = k;
+        if (k == 0) {
+            wavg[g] = median[g] = majority[g] = mean_conf[g] = NAN;
+        } else {
+            wavg[g] = (tconf == 0.0) ? tcons / (double)k : tprod / tconf;
+            majority[g] = (double)votes / (double)k;
+            mean_conf[g] = tconf / (double)k;
+            qsort(vals, (size_t)k, sizeof(double), cmp_f64);
+            median[g] = vals[k / 2];
+        }
+        free(vals);
+    }
+}

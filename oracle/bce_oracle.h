@@ -80,6 +80,20 @@ int orc_tiebreak_csr(const int64_t* offsets, int64_t n_markets, const double* pr
 void orc_reestimate(const double* P, int64_t A, int64_t M, int iters, double* w,
                     double* cons_out, uint8_t* null_out, int64_t* agree_out);
 
+/* NamespacedReliabilityStore.get_reliability (reliability_abstraction.py:119-188) over
+ * a rank space: three scopes (market, domain, global), NULL rel = not requested. */
+void orc_namespace_resolve(int64_t n, const double* const rel[3], const double* const conf[3],
+                           const int64_t* const t_us[3], const uint8_t* const has[3],
+                           int apply_decay, int64_t now_us, double half_life_days, double min_rel,
+                           double default_rel, double default_conf, double* rel_out,
+                           double* conf_out, uint8_t* scope_out);
+
+/* CrossMarketAggregator.aggregate_consensus (market.py:340-408) per member group. */
+void orc_aggregate_groups(const int64_t* goff, int64_t n_groups, const int64_t* members,
+                          const double* cons, const double* conf, const uint8_t* has,
+                          double* wavg, double* median, double* majority, double* mean_conf,
+                          int64_t* n_included);
+
 #ifdef __cplusplus
 }
 #endif

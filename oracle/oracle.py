@@ -143,3 +143,40 @@ def reestimate(P, iters, w0=0.5):
     lib().orc_reestimate(_p(P), C.c_int64(A), C.c_int64(M), C.c_int(iters), _p(w), _p(cons), _p(null),
                          _p(agree))
     return w, cons, null, agree
+
+
+def namespace_resolve(scopes, apply_decay, now_us, half_life=30.0, min_rel=0.10, default_rel=0.50,
+                      default_conf=0.25):
+    """scopes: 3 entries (market, domain, global), each None or (rel, conf, t_us, has)."""
+    n = next(len(sc[0]) for sc in scopes if sc is not None) if any(sc is not None for sc in scopes) else 0
+    keep = []
+    ptrs = {k: (C.c_void_p * 3)() for k in ("rel", "conf", "t", "has")}
+    for q, sc in enumerate(scopes):
+        if sc is None:
+            continue
+        arrs = (np.ascontiguousarray(sc[0], np.float64), np.ascontiguousarray(sc[1], np.float64),
+                np.ascontiguousarray(sc[2], np.int64), np.ascontiguousarray(sc[3], np.uint8))
+        keep.append(arrs)
+        for k, a in zip(("rel", "conf", "t", "has"), arrs):
+            ptrs[k][q] = a.ctypes.data
+    rel, conf, scope = np.zeros(n), np.zeros(n), np.zeros(n, np.uint8)
+    lib().orc_namespace_resolve(C.c_int64(n), ptrs["rel"], ptrs["conf"], ptrs["t"], ptrs["has"],
+                                C.c_int(int(apply_decay)), C.c_int64(int(now_us)), C.c_double(half_life),
+                                C.c_double(min_rel), C.c_double(default_rel), C.c_double(default_conf),
+                                _p(rel), _p(conf), _p(scope))
+    return rel, conf, scope
+
+
+def aggregate_groups(goff, members, cons, conf, has):
+    goff = np.ascontiguousarray(goff, np.int64)
+    members = np.ascontiguousarray(members, np.int64)
+    cons = np.ascontiguousarray(cons, np.float64)
+    conf = np.ascontiguousarray(conf, np.float64)
+    has = np.ascontiguousarray(has, np.uint8)
+    G = len(goff) - 1
+    out = dict(wavg=np.zeros(G), median=np.zeros(G), majority=np.zeros(G), mean_conf=np.zeros(G),
+               n_included=np.zeros(G, np.int64))
+    lib().orc_aggregate_groups(_p(goff), C.c_int64(G), _p(members), _p(cons), _p(conf), _p(has),
+                               _p(out["wavg"]), _p(out["median"]), _p(out["majority"]), _p(out["mean_conf"]),
+                               _p(out["n_included"]))
+    return out

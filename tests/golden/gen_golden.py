@@ -25,6 +25,10 @@ Fixture map:
   c4_replay.npz           config-4-shaped decay + outcome replay (S=2000, T=30)
   c5_reestimate.npz       config-5-shaped re-estimation (A=64, M=512, k=3)
   cli_cases.json          CLI stdout/rc (config 1 = examples/sample_input.json)
+  namespace_cases.json    NamespacedReliabilityStore.get_reliability      (reliability_abstraction.py:119-188)
+  aggregate_cases.json    CrossMarketAggregator.aggregate_consensus       (market.py:340-408)
+
+  python3 tests/golden/gen_golden.py [name ...]   regenerates only the named fixtures
 """
 
 from __future__ import annotations
@@ -689,7 +693,115 @@ def gen_cli_cases() -> None:
     dump("cli_cases.json", {"inputs": cases_inputs, "cases": cases})
 
 
+def gen_namespace_cases(rng: np.random.Generator) -> None:
+    """Rows are inserted with chosen updated_at strings (set_global_reliability stamps the
+    real wall clock, reliability_abstraction.py:233-235), then every (market_id, domain)
+    query shape is resolved through the reference's fallback chain with decay on and off."""
+    from bayesian_engine.reliability_abstraction import NamespacedReliabilityStore
+
+    now = datetime(2026, 3, 1, 12, 0, 0, tzinfo=timezone.utc)
+    freeze(now)
+    S = 48
+    names = sorted(f"src-{i:03d}" for i in range(S)) + ["\u00e9t\u00e9", "Zed", "a b"]
+    names = sorted(names)
+    scopes = {"market": "m1", "domain": "__domain__:crypto", "global": "__global__"}
+    stamp_kinds = ["", "not-a-date", "aware", "naive", "future", "aware_old"]
+    rows = []
+    store = NamespacedReliabilityStore(":memory:")
+    conn = store._store._conn
+    for sid in names:
+        for scope, mid in scopes.items():
+            if rng.random() < 0.35:
+                continue  # no row in this scope
+            kind = stamp_kinds[int(rng.integers(0, len(stamp_kinds)))]
+            age = float(rng.uniform(0, 200))
+            if kind in ("", "not-a-date"):
+                ts = kind
+            elif kind == "aware":
+                ts = (now - timedelta(days=age)).isoformat()
+            elif kind == "naive":
+                ts = (now - timedelta(days=age)).replace(tzinfo=None).isoformat()
+            elif kind == "future":
+                ts = (now + timedelta(days=age)).isoformat()
+            else:
+                ts = (now - timedelta(days=1000 + age)).isoformat()
+            r = float(rng.choice([0.0, 0.05, 1.0, 1.3, float(rng.random())]))
+            c = float(rng.random())
+            conn.execute("INSERT INTO sources (source_id, market_id, reliability, confidence, updated_at) "
+                         "VALUES (?, ?, ?, ?, ?)", (sid, mid, r, c, ts))
+            rows.append([sid, mid, r, c, ts])
+    queries = [("m1", "crypto"), (None, "crypto"), ("m1", None), (None, None), ("m2", "sports"), ("", "")]
+    results = []
+    for mid, dom in queries:
+        for decay in (True, False):
+            out = []
+            for sid in names:
+                rec = store.get_reliability(sid, market_id=mid, domain=dom, apply_decay=decay)
+                out.append([rec.namespace.value, rec.namespace_value, rec.reliability, rec.confidence,
+                            rec.updated_at, rec.is_fallback])
+            results.append({"market_id": mid, "domain": dom, "apply_decay": decay, "records": out})
+    store.close()
+    dump("namespace_cases.json", {"now": now.isoformat(), "now_us": to_us(now), "names": names, "rows": rows,
+                                  "queries": results})
+
+
+def gen_aggregate_cases(rng: np.random.Generator) -> None:
+    """Markets in several categories; some with consensus, some never computed, some empty
+    (Market.compute_consensus on an empty market sets no result, market.py:117-123), some
+    with a null consensus (all-zero weights); aggregate_consensus over pattern lists that
+    overlap (duplicated members) for every method, plus an unknown method."""
+    store = MarketStore()
+    cats = ["crypto", "sports", "politics"]
+    ids = []
+    for i in range(60):
+        cat = cats[i % 3]
+        mid = MarketId(f"{cat}:m{i:02d}")
+        m = store.create_market(mid)
+        ids.append(str(mid))
+        kind = rng.random()
+        if kind < 0.1:
+            continue  # no signals, never computed
+        n = int(rng.integers(1, 9))
+        grid = rng.random() < 0.4
+        for j in range(n):
+            p = float(rng.choice([0.1, 0.5, 0.5, 0.9, 0.3])) if grid else float(rng.random())
+            m.add_signal({"sourceId": f"s{int(rng.integers(0, 6))}", "probability": p})
+        rel = {f"s{k}": {"reliability": float(rng.choice([0.0, 0.2, 0.7, 1.0])),
+                         "confidence": float(rng.choice([0.0, 0.25, 0.6]))} for k in range(6)}
+        if rng.random() < 0.1:
+            rel = {f"s{k}": {"reliability": 0.0, "confidence": 0.5} for k in range(6)}  # null consensus
+        if kind < 0.9:
+            m.compute_consensus(rel if rng.random() < 0.7 else None)
+    agg = CrossMarketAggregator(store)
+    pattern_sets = [["crypto:*"], ["sports:*"], ["*"], ["crypto:*", "*"], ["politics:m0*", "politics:*"],
+                    ["nothing:*"], ["crypto:m00"], ["sports:m01", "sports:m04"]]
+    cases = []
+    for pats in pattern_sets:
+        for method in ("weighted_average", "median", "majority", "bogus"):
+            try:
+                res = agg.aggregate_consensus(pats, method=method)
+                cases.append({"patterns": pats, "method": method, "result": res})
+            except ValueError as e:
+                cases.append({"patterns": pats, "method": method, "error": str(e)})
+    markets = []
+    for key in ids:
+        m = store.get_market(MarketId(key))
+        markets.append({"id": key, "signals": m.signals,
+                        "result": None if m.consensus_result is None else
+                        {"consensus": m.consensus_result["consensus"],
+                         "confidence": m.consensus_result["confidence"]}})
+    dump("aggregate_cases.json", {"markets": markets, "cases": cases})
+
+
 def main() -> None:
+    only = set(sys.argv[1:])
+    if only:
+        freeze(datetime(2026, 3, 1, 12, 0, 0, tzinfo=timezone.utc))
+        if "namespace" in only:
+            gen_namespace_cases(np.random.default_rng(17))
+        if "aggregate" in only:
+            gen_aggregate_cases(np.random.default_rng(18))
+        return
     freeze(datetime(2026, 3, 1, 12, 0, 0, tzinfo=timezone.utc))
     gen_consensus_cases(np.random.default_rng(11))
     gen_validate_cases()
@@ -703,6 +815,8 @@ def main() -> None:
     gen_c4_replay(np.random.default_rng(4))
     gen_c5(np.random.default_rng(5))
     gen_cli_cases()
+    gen_namespace_cases(np.random.default_rng(17))
+    gen_aggregate_cases(np.random.default_rng(18))
 
 
 if __name__ == "__main__":

@@ -33,7 +33,7 @@ VARIANTS = {
     "pipe_nocheck": ["-DBCE_ABLATE=32"],
     "pipe_nts_lprio3": ["-DBCE_PIPE_NTS=1", "-DBCE_PIPE_LPRIO=3"],
 }
-SRCS = ["capi.hip", "consensus.hip", "elementwise.hip", "tiebreak.hip", "stats.hip"]
+SRCS = ["capi.hip", "consensus.hip", "elementwise.hip", "tiebreak.hip", "stats.hip", "aggregate.hip"]
 
 
 def build(names):
