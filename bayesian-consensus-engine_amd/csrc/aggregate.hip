@@ -10,8 +10,9 @@
 //   confidence        sum(conf) / k (:407)
 // Sums run left to right in list order from 0.0 (builtin sum), FP contraction off, so
 // every output is bit-identical to the reference.  One 256-thread workgroup per group:
-// chunks of 256 members are gathered, compacted into LDS in list order with ballots, and
-// three lanes of wave 0 carry the three ordered chains; the median is an exact 8-pass
+// chunks of 1024 members are gathered (indices two chunks ahead, values one chunk ahead of
+// use), compacted into LDS in list order with ballots, and three lanes of wave 0 carry the
+// three ordered chains in 8-term batches; the median is an exact 8-pass
 // MSB radix select over order-preserving 64-bit keys (no sort, no extra memory).
 #include "bce_device.hpp"
 #include "bce_internal.hpp"
@@ -48,11 +49,14 @@ __device__ __forceinline__ double key_f64(uint64_t k) {
 }
 
 constexpr int kAggT = 256;
+constexpr int kAggPer = 4;                  // members per thread per chunk
+constexpr int kAggCh = kAggT * kAggPer;     // chunk = 1024 members, list order r-major
 
 __global__ __launch_bounds__(kAggT) void aggregate_kernel(AggArgs a) {
-  __shared__ double sV[3][kAggT];  // conf, cons, cons*conf of the chunk's valid members
-  __shared__ int sWave[kAggT / 64 + 1];
+  __shared__ double sV[3][kAggCh];  // conf, cons, cons*conf of the chunk's valid members
+  __shared__ int sWave[kAggPer][kAggT / 64];
   __shared__ int sHist[256];
+  __shared__ int sWsum[kAggT / 64];
   __shared__ unsigned long long sVotes;
   __shared__ double sTot[3];
   __shared__ uint64_t sPrefix;
@@ -61,42 +65,75 @@ __global__ __launch_bounds__(kAggT) void aggregate_kernel(AggArgs a) {
   const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   for (int64_t g = blockIdx.x; g < a.n_groups; g += gridDim.x) {
     const int64_t b = a.goff[g], e = a.goff[g + 1];
+    // software pipeline: member indices one chunk ahead of the gathers, gathers one chunk
+    // ahead of the compaction, so the ordered chains run while the next chunk is in flight
+    auto load_idx = [&](int64_t c0, int64_t* id) {
+#pragma unroll
+      for (int r = 0; r < kAggPer; ++r) {
+        const int64_t i = c0 + r * kAggT + t;
+        id[r] = (i < e) ? a.members[i] : -1;
+      }
+    };
+    bool v[kAggPer];
+    double x[kAggPer], c[kAggPer];
+    auto gather = [&](const int64_t* id) {
+#pragma unroll
+      for (int r = 0; r < kAggPer; ++r) {
+        const int64_t m = id[r];
+        const bool in = m >= 0 && m < a.n_markets;
+        v[r] = in && a.has[m] != 0;
+        x[r] = in ? a.cons[m] : 0.0;
+        c[r] = in ? a.conf[m] : 0.0;
+      }
+    };
+    int64_t idn[kAggPer];
+    load_idx(b, idn);
+    gather(idn);
+    load_idx(b + kAggCh, idn);
     double chain = 0.0;  // lanes 0..2 of wave 0: sum(conf), sum(cons), sum(cons*conf)
     int64_t k = 0;
     if (t == 0) sVotes = 0;
-    for (int64_t c0 = b; c0 < e; c0 += kAggT) {
-      const int64_t i = c0 + t;
-      bool valid = false;
-      double x = 0.0, c = 0.0;
-      if (i < e) {
-        const int64_t m = a.members[i];
-        valid = (m >= 0 && m < a.n_markets) && a.has[m] != 0;
-        if (valid) {
-          x = a.cons[m];
-          c = a.conf[m];
-        }
-      }
-      const unsigned long long msk = ballot(valid);
-      if (lane == 0) sWave[w] = __popcll(msk);
-      __syncthreads();
-      int base = 0, cnt = 0;
+    for (int64_t c0 = b; c0 < e; c0 += kAggCh) {
+      unsigned long long msk[kAggPer];
+      unsigned votes = 0;
 #pragma unroll
-      for (int q = 0; q < kAggT / 64; ++q) {
-        base += (q < w) ? sWave[q] : 0;
-        cnt += sWave[q];
+      for (int r = 0; r < kAggPer; ++r) {
+        msk[r] = ballot(v[r]);
+        if (lane == 0) sWave[r][w] = __popcll(msk[r]);
+        votes += __popcll(ballot(v[r] && x[r] >= 0.5));  // market.py:400
       }
-      if (valid) {
-        const int pos = base + __popcll(msk & lt);
-        sV[0][pos] = c;
-        sV[1][pos] = x;
-        sV[2][pos] = x * c;  // market.py:391
-      }
-      const unsigned long long vm = ballot(valid && x >= 0.5);  // market.py:400
-      if (lane == 0 && vm) atomicAdd(&sVotes, (unsigned long long)__popcll(vm));
       __syncthreads();
+      int run = 0;
+#pragma unroll
+      for (int r = 0; r < kAggPer; ++r) {
+        int before = run;
+#pragma unroll
+        for (int q = 0; q < kAggT / 64; ++q) before += (q < w) ? sWave[r][q] : 0;
+        if (v[r]) {
+          const int pos = before + __popcll(msk[r] & lt);
+          sV[0][pos] = c[r];
+          sV[1][pos] = x[r];
+          sV[2][pos] = x[r] * c[r];  // market.py:391
+        }
+#pragma unroll
+        for (int q = 0; q < kAggT / 64; ++q) run += sWave[r][q];
+      }
+      const int cnt = run;
+      if (lane == 0 && votes) atomicAdd(&sVotes, (unsigned long long)votes);
+      __syncthreads();
+      gather(idn);                     // next chunk in flight during the chains
+      load_idx(c0 + 2 * kAggCh, idn);
       if (t < 3) {
-        const double* v = sV[t];
-        for (int j = 0; j < cnt; ++j) chain = chain + v[j];
+        const double* vv = sV[t];
+        int j = 0;
+        for (; j + 8 <= cnt; j += 8) {
+          double q8[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) q8[q] = vv[j + q];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) chain = chain + q8[q];
+        }
+        for (; j < cnt; ++j) chain = chain + vv[j];
       }
       k += cnt;
       __syncthreads();  // chunk buffer reused
@@ -119,29 +156,46 @@ __global__ __launch_bounds__(kAggT) void aggregate_kernel(AggArgs a) {
         sPrefix = 0;
         sRank = k / 2;
       }
+      // a group that fit in one chunk still has its valid consensus values in sV[1]
+      const bool in_lds = (e - b) <= kAggCh;
       for (int pass = 0; pass < 8 && k > 0; ++pass) {
         const int sh = 56 - 8 * pass;
         sHist[t] = 0;
         __syncthreads();
         const uint64_t pre = sPrefix;
         const uint64_t pmask = (pass == 0) ? 0ull : (~0ull << (sh + 8));
-        for (int64_t i = b + t; i < e; i += kAggT) {
-          const int64_t m = a.members[i];
-          if (m >= 0 && m < a.n_markets && a.has[m]) {
-            const uint64_t key = f64_key(a.cons[m]);
+        if (in_lds) {
+          for (int j = t; j < (int)k; j += kAggT) {
+            const uint64_t key = f64_key(sV[1][j]);
             if ((key & pmask) == pre) atomicAdd(&sHist[(key >> sh) & 255], 1);
+          }
+        } else {
+          for (int64_t i = b + t; i < e; i += kAggT) {
+            const int64_t m = a.members[i];
+            if (m >= 0 && m < a.n_markets && a.has[m]) {
+              const uint64_t key = f64_key(a.cons[m]);
+              if ((key & pmask) == pre) atomicAdd(&sHist[(key >> sh) & 255], 1);
+            }
           }
         }
         __syncthreads();
-        if (t == 0) {
-          int64_t r = sRank, acc = 0;
-          int d = 0;
-          for (; d < 255; ++d) {
-            if (acc + sHist[d] > r) break;
-            acc += sHist[d];
-          }
-          sRank = r - acc;
-          sPrefix = pre | ((uint64_t)d << sh);
+        // bin holding rank r: block-wide inclusive scan of the 256 bin counts
+        const int hv = sHist[t];
+        int inc = hv;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int y = __shfl_up(inc, o);
+          if (lane >= o) inc += y;
+        }
+        if (lane == 63) sWsum[w] = inc;
+        const int64_t r = sRank;
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < kAggT / 64; ++q) inc += (q < w) ? sWsum[q] : 0;
+        const int exc = inc - hv;
+        if ((int64_t)exc <= r && r < (int64_t)inc) {  // exactly one bin
+          sRank = r - exc;
+          sPrefix = pre | ((uint64_t)t << sh);
         }
         __syncthreads();
       }

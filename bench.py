@@ -17,7 +17,7 @@ Also measured here:
                 launch time from HIP events on the launch stream, vs 8.0 TB/s.
   cpu_baseline  the C restatement of the reference (oracle/, kind "port") timed on one
                 host core over a bounded sample, rank 0 at N=1 only.
-Other configs (--config c3|c4|c5) are secondary bench lines; the default is c2.
+Other configs (--config c3|c4|c5|ns|agg) are secondary bench lines; the default is c2.
 """
 from __future__ import annotations
 
@@ -44,7 +44,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=50)
-    p.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
+    p.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5", "ns", "agg"])
     p.add_argument("--markets", type=int, default=1_000_000)
     p.add_argument("--len", type=int, default=32)
     p.add_argument("--sources", type=int, default=10_000)

@@ -13,9 +13,18 @@ steps, K timed steps bracketed by barrier + synchronize, max over ranks, one JSO
   c5  dense A x M re-estimation (default 16384 x 1e6 fp64 = 131 GB), markets sharded by
       column over N ranks; per iteration pass 1 (consensus), pass 2 (agreement), an
       all-reduce of the per-agent counts, the weight update.  Step = one iteration.
+  ns  SURVEY §8(f) f3: namespaced fallback over a 10M-source rank space (market, domain,
+      global scopes, each holding a row for ~50% of sources, 10% unparseable stamps),
+      decay on.  Step = one bce_namespace_resolve launch producing the packed consensus
+      table.  Sources shard by owner (weak scaling), no collective.
+  agg SURVEY §8(f) f4: aggregate_consensus over 10k member groups of 1000 markets each
+      (contiguous pattern-matched ranges of a 1M-market batch, 20% without consensus).
+      Step = one bce_aggregate_groups launch (weighted_average, majority, confidence;
+      median in the config string's second figure).  Groups shard over ranks (weak).
 """
 from __future__ import annotations
 
+import ctypes as C
 import time
 
 import numpy as np
@@ -48,7 +57,7 @@ def _timed(step, args, world, stream, barrier, max_over):
 def run_extra(args, world, rank):
     from bench import barrier, max_over_ranks, sum_over_ranks  # noqa: E402
 
-    fn = {"c3": _c3, "c4": _c4, "c5": _c5}[args.config]
+    fn = {"c3": _c3, "c4": _c4, "c5": _c5, "ns": _ns, "agg": _agg}[args.config]
     return fn(args, world, rank, barrier, max_over_ranks, sum_over_ranks)
 
 
@@ -250,5 +259,100 @@ def _c5(args, world, rank, barrier, max_over, sum_over):
                      "kernel": "reestimate_consensus + reestimate_agreement (one iteration)",
                      "bytes_per_launch": bytes_iter, "avg_launch_ms": kern * 1e3,
                      "mfma": "not used: GEMV at ~0.25 flop/B; exact agent-order sums on the VALU"},
+        "cpu_baseline": None,
+    }
+
+
+# ---------------------------------------------------------------------------------------
+def _ns(args, world, rank, barrier, max_over, sum_over):
+    from bayesian_engine import _native as N
+    from bayesian_engine import batch
+    from bayesian_engine.timeutil import NO_TIMESTAMP
+
+    S = 10_000_000
+    dev = torch.device("cuda", torch.cuda.current_device())
+    g = torch.Generator(device=dev)
+    g.manual_seed(40 + rank)
+    now_us = 1_772_323_200_000_000
+    day = 86_400_000_000
+    scopes = []
+    for q in range(3):
+        rel = torch.rand(S, generator=g, device=dev, dtype=torch.float64)
+        conf = torch.rand(S, generator=g, device=dev, dtype=torch.float64)
+        t = now_us - (torch.rand(S, generator=g, device=dev, dtype=torch.float64) * 200 * day).to(torch.int64)
+        t[torch.rand(S, generator=g, device=dev) < 0.1] = NO_TIMESTAMP
+        has = (torch.rand(S, generator=g, device=dev) < 0.5).to(torch.uint8)
+        scopes.append(batch.ScopeTable(rel, conf, t, has))
+    relconf = torch.empty((S, 2), dtype=torch.float64, device=dev)
+    bits = torch.empty((S + 31) // 32, dtype=torch.int32, device=dev)
+    code = torch.empty(S, dtype=torch.uint8, device=dev)
+    L = N.require_gpu()
+    st = torch.cuda.current_stream(dev)
+    ptrs = [N.ptr(a) for sc in scopes for a in (sc.rel, sc.conf, sc.t_us, sc.has)]
+
+    def step():
+        N.check(L.bce_namespace_resolve(S, *ptrs, 1, now_us, 30.0, 0.1, 0.5, 0.25, 1, N.ptr(relconf), N.ptr(bits),
+                                        N.ptr(code), C.c_void_p(st.cuda_stream)), "bce_namespace_resolve")
+
+    wall, per = _timed(step, args, world, st, barrier, max_over)
+    # per source: 3 has bytes + the chosen scope's rel/conf/t (24 B, non-cold only) +
+    # relconf 16 B + scope code 1 B + 1/8 B present bit
+    noncold = float((code != 3).float().mean().item())
+    bps = 3 + 24 * noncold + 17.125
+    achieved = bps * S / per / 1e9
+    tot = sum_over(float(S * args.steps), world)
+    return {
+        "metric": "sources resolved/sec (node), namespaced fallback market->domain->global->cold (SURVEY f3)",
+        "value": tot / wall, "unit": "sources/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic (3 scopes, 50% rows each, 10% unparseable stamps)",
+        "config": {"workload": f"ns: {S} sources x 3 scopes per rank, decay on, mark_cold",
+                   "noncold_fraction": noncold, "parallelism": f"sources sharded over {world} rank(s), no collective"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "namespace_resolve_kernel",
+                     "bytes_per_launch": bps * S, "avg_launch_ms": per * 1e3},
+        "cpu_baseline": None,
+    }
+
+
+def _agg(args, world, rank, barrier, max_over, sum_over):
+    from bayesian_engine import _native as N
+
+    M, G, K = 1_000_000, 10_000, 1000
+    dev = torch.device("cuda", torch.cuda.current_device())
+    rng = np.random.default_rng(50 + rank)
+    cons = torch.from_numpy(rng.random(M)).to(dev)
+    conf = torch.from_numpy(rng.random(M)).to(dev)
+    has = torch.from_numpy((rng.random(M) < 0.8).astype(np.uint8)).to(dev)
+    starts = rng.integers(0, M - K, G)
+    members = torch.from_numpy((starts[:, None] + np.arange(K)[None, :]).reshape(-1).astype(np.int64)).to(dev)
+    goff = torch.from_numpy(np.arange(G + 1, dtype=np.int64) * K).to(dev)
+    f64 = dict(dtype=torch.float64, device=dev)
+    wavg, med, maj, mc = (torch.empty(G, **f64) for _ in range(4))
+    nin = torch.empty(G, dtype=torch.int64, device=dev)
+    L = N.require_gpu()
+    st = torch.cuda.current_stream(dev)
+
+    def launch(with_median):
+        N.check(L.bce_aggregate_groups(N.ptr(goff), G, N.ptr(members), M, N.ptr(cons), N.ptr(conf), N.ptr(has),
+                                       N.ptr(wavg), N.ptr(med) if with_median else None, N.ptr(maj), N.ptr(mc),
+                                       N.ptr(nin), C.c_void_p(st.cuda_stream)), "bce_aggregate_groups")
+
+    wall, per = _timed(lambda: launch(False), args, world, st, barrier, max_over)
+    _, per_med = _timed(lambda: launch(True), args, world, st, barrier, max_over)
+    bpm = 8 + 1 + 16  # member index, has byte, consensus + confidence
+    achieved = bpm * G * K / per / 1e9
+    tot = sum_over(float(G * K * args.steps), world)
+    return {
+        "metric": "market results aggregated/sec (node), aggregate_consensus over member groups (SURVEY f4)",
+        "value": tot / wall, "unit": "members/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic (1M markets, 80% with consensus)",
+        "config": {"workload": f"agg: {G} groups x {K} members over {M} markets per rank; "
+                               f"weighted_average+majority+confidence {per * 1e3:.4f} ms, +median {per_med * 1e3:.4f} ms",
+                   "parallelism": f"groups sharded over {world} rank(s), no collective"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "aggregate_kernel",
+                     "bytes_per_launch": bpm * G * K, "avg_launch_ms": per * 1e3},
         "cpu_baseline": None,
     }
