@@ -27,6 +27,12 @@ VARIANTS = {
     "pipe_noout": ["-DBCE_ABLATE=8"],
     "pipe_nogather": ["-DBCE_ABLATE=2"],
     "pipe_prof": ["-DBCE_PIPE_PROF=1"],
+    "pipe_prof_nocheck": ["-DBCE_PIPE_PROF=1", "-DBCE_ABLATE=32"],
+    "pipe_nogather_noout": ["-DBCE_ABLATE=10"],
+    "pipe_nosort": ["-DBCE_ABLATE=1"],
+    "pipe_l2_ngno": ["-DBCE_PIPE_L=2", "-DBCE_ABLATE=10"],
+    "pipe_l2_c3": ["-DBCE_PIPE_L=2", "-DBCE_PIPE_C32=3", "-DBCE_PIPE_R32=6"],
+    "pipe_c3": ["-DBCE_PIPE_C32=3", "-DBCE_PIPE_R32=6"],
     "pipe_lprio3": ["-DBCE_PIPE_LPRIO=3"],
     "pipe_lprio1": ["-DBCE_PIPE_LPRIO=1"],
     "pipe_nts": ["-DBCE_PIPE_NTS=1"],
