@@ -109,7 +109,7 @@ def make_c2(M, L, S, seed):
     return offsets, sid, prob, rel, conf, present
 
 
-def cpu_baseline_c2(offsets, sid, prob, rel, conf, present, sample_markets):
+def cpu_baseline_c2(offsets, sid, prob, rel, conf, present, sample_markets, min_seconds=10.0):
     """The oracle's C restatement (kind 'port') on one core over a bounded sample."""
     sys.path.insert(0, ROOT)
     from oracle import oracle as orc
@@ -117,12 +117,19 @@ def cpu_baseline_c2(offsets, sid, prob, rel, conf, present, sample_markets):
     M = min(sample_markets, len(offsets) - 1)
     off = offsets[: M + 1]
     n = int(off[-1])
+    # repeat the pass until ~10 s of CPU work (the bounded-sample rule), report the mean rate
     t0 = time.perf_counter()
-    out = orc.consensus_csr(off, sid[:n], prob[:n], rel, conf, present)
-    dt = time.perf_counter() - t0
-    return n / dt, dict(value=n / dt, unit="signals/s", cores=1, kind="port",
-                        sample=f"{M} markets x {int(n // max(M, 1))} signals of the same workload "
-                               f"(seed-identical), oracle/bce_oracle.c single-threaded, {dt:.2f} s"), out, M
+    reps = 0
+    while True:
+        out = orc.consensus_csr(off, sid[:n], prob[:n], rel, conf, present)
+        reps += 1
+        dt = time.perf_counter() - t0
+        if dt >= min_seconds:
+            break
+    rate = n * reps / dt
+    return rate, dict(value=rate, unit="signals/s", cores=1, kind="port",
+                      sample=f"{M} markets x {int(n // max(M, 1))} signals of the same workload "
+                             f"(seed-identical), oracle/bce_oracle.c single-threaded, {reps} passes in {dt:.2f} s"), out, M
 
 
 def bench_c2(args, world, rank):
