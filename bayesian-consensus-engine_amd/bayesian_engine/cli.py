@@ -49,6 +49,26 @@ def _cmd_consensus(args: argparse.Namespace) -> None:
         raise SystemExit(1) from exc
 
 
+def _cmd_consensus_batch(args: argparse.Namespace) -> None:
+    """Build-defined: a JSONL file of payloads, one consensus launch for all.
+    Prints, per line, exactly what ``consensus`` prints for that payload alone (results on
+    stdout, ``Validation error: ...`` on stderr); exit 1 if any line failed.  Sources are
+    cold (no ``--db`` lookup), as in the legacy path."""
+    from .jsonl import consensus_jsonl
+
+    if args.input:
+        with open(args.input, "r", encoding="utf-8") as f:
+            lines = f.readlines()
+    else:
+        lines = sys.stdin.readlines()
+    failed = False
+    for ok, text in consensus_jsonl(lines, dry_run=args.dry_run):
+        print(text, file=sys.stdout if ok else sys.stderr)
+        failed |= not ok
+    if failed:
+        raise SystemExit(1)
+
+
 def _cmd_report_outcome(args: argparse.Namespace) -> None:
     if not args.db:
         print("Error: --db is required for report-outcome", file=sys.stderr)
@@ -91,6 +111,9 @@ def main() -> None:
     consensus_parser = subparsers.add_parser("consensus", help="Compute consensus from signals")
     consensus_parser.add_argument("--input", help="Path to JSON input file")
     consensus_parser.set_defaults(func=_cmd_consensus)
+    batch_parser = subparsers.add_parser("consensus-batch", help="Compute consensus for a JSONL batch of payloads")
+    batch_parser.add_argument("--input", help="Path to JSONL input file (one payload per line)")
+    batch_parser.set_defaults(func=_cmd_consensus_batch)
     outcome_parser = subparsers.add_parser("report-outcome", help="Report outcome and update reliability")
     outcome_parser.add_argument("--source-id", required=True, help="Source identifier")
     outcome_parser.add_argument("--market-id", required=True, help="Market identifier")

@@ -25,7 +25,7 @@ from . import _native as N
 from . import batch
 from .config import DEFAULT_CONFIDENCE, DEFAULT_RELIABILITY, SCHEMA_VERSION
 
-__all__ = ["ValidationError", "validate_input_payload", "compute_consensus", "SCHEMA_VERSION",
+__all__ = ["ValidationError", "validate_input_payload", "check_structure", "compute_consensus", "SCHEMA_VERSION",
            "DEFAULT_RELIABILITY", "DEFAULT_CONFIDENCE"]
 
 
@@ -48,6 +48,24 @@ def _as_float(p) -> float:
 
 def validate_input_payload(payload: dict[str, Any]) -> None:
     """Validate the v1.0.0 input contract (core.py:24-60), same order and messages."""
+    probs, type_error = check_structure(payload)
+    if probs:  # range check of the signals before the first type error, on the GPU
+        N.require_gpu()
+        dev = N.device()
+        off = torch.tensor([0, len(probs)], dtype=torch.int64, device=dev)
+        p = torch.tensor(probs, dtype=torch.float64, device=dev)
+        k = int(batch.validate(off, p)[0].item())
+        if k >= 0:
+            raise ValidationError(f"signals[{k}].probability must be between 0 and 1")
+    if type_error is not None:
+        raise type_error
+
+
+def check_structure(payload: dict[str, Any]) -> tuple[list[float], ValidationError | None]:
+    """Host half of validate_input_payload (core.py:34-58): raises the header errors; returns
+    the probabilities before the first signal-level type error, and that error (or None).
+    The numeric range check (core.py:59-60) over the returned probabilities is the caller's
+    GPU launch -- one per payload here, one per batch in :mod:`bayesian_engine.jsonl`."""
     schema_version = _require(payload, "schemaVersion")
     if schema_version != SCHEMA_VERSION:
         raise ValidationError(f"schemaVersion must be '{SCHEMA_VERSION}' (got '{schema_version}')")
@@ -81,17 +99,7 @@ def validate_input_payload(payload: dict[str, Any]) -> None:
             type_error = ValidationError(f"signals[{idx}].probability must be a number")
             break
         probs.append(_as_float(probability))
-
-    if probs:  # range check of the signals before the first type error, on the GPU
-        N.require_gpu()
-        dev = N.device()
-        off = torch.tensor([0, len(probs)], dtype=torch.int64, device=dev)
-        p = torch.tensor(probs, dtype=torch.float64, device=dev)
-        k = int(batch.validate(off, p)[0].item())
-        if k >= 0:
-            raise ValidationError(f"signals[{k}].probability must be between 0 and 1")
-    if type_error is not None:
-        raise type_error
+    return probs, type_error
 
 
 def _no_signals() -> dict[str, Any]:

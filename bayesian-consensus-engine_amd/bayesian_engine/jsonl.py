@@ -1,0 +1,163 @@
+"""Batched JSON front end: many payloads -> one CSR -> one launch.
+
+The reference handles one payload per CLI call (cli.py:25-52: ``json.load`` ->
+``validate_input_payload`` -> ``compute_consensus`` -> ``json.dumps(indent=2)``).  Here a
+whole JSONL batch goes through the same steps with the per-signal work batched:
+
+* parse + structural checks on the host (core.py:34-58 via :func:`core.check_structure`);
+* ONE ``bce_validate_csr`` launch for the range check of every payload (core.py:59-60);
+* source ids of every valid payload interned once in code-point order (Python ``sorted``,
+  core.py:103), so a market's ranks sort exactly like its ids;
+* ONE consensus launch (length-binned plan) over the CSR of all markets;
+* each result rendered with ``json.dumps(indent=2)`` -- byte-identical to what the
+  single-payload CLI prints for that payload.
+
+All payloads of a batch share one ``source_reliability`` dict (the CLI's no-``--db`` path
+uses none: every source cold).  A non-numeric reliability/confidence in it raises the same
+TypeError as compute_consensus would, for the whole batch.
+"""
+from __future__ import annotations
+
+import json
+from typing import Any, Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _native as N
+from . import batch
+from .config import DEFAULT_CONFIDENCE, DEFAULT_RELIABILITY, SCHEMA_VERSION
+from .core import ValidationError, _as_float, _check_number, _no_signals, check_structure
+
+__all__ = ["consensus_many", "consensus_jsonl", "parse_batch"]
+
+
+def consensus_many(signal_lists: Sequence[list], source_reliability: Optional[dict] = None, *,
+                   mode: str = "exact") -> List[dict]:
+    """``[compute_consensus(s, source_reliability) for s in signal_lists]`` in one launch."""
+    M = len(signal_lists)
+    if M == 0:
+        return []
+    sr = source_reliability or {}
+    names = sorted({s["sourceId"] for sig in signal_lists for s in sig})
+    rank = {n: i for i, n in enumerate(names)}
+    lens = np.fromiter((len(sig) for sig in signal_lists), np.int64, M)
+    off = np.zeros(M + 1, np.int64)
+    np.cumsum(lens, out=off[1:])
+    Ns = int(off[-1])
+    if Ns == 0:
+        return [_no_signals() for _ in range(M)]
+
+    raw = [s["probability"] for sig in signal_lists for s in sig]
+    for p in raw:
+        if not isinstance(p, (int, float)):
+            0 + p  # noqa: B018  -- builtin sum()'s TypeError (core.py:116)
+    prob = np.fromiter((_as_float(p) for p in raw), np.float64, Ns)
+    sid = np.fromiter((rank[s["sourceId"]] for sig in signal_lists for s in sig), np.int32, Ns)
+    rel_objs = []
+    for n in names:
+        d = sr.get(n, {})
+        r = d.get("reliability", DEFAULT_RELIABILITY)
+        c = d.get("confidence", DEFAULT_CONFIDENCE)
+        _check_number(r, None)
+        if not isinstance(c, (int, float)):
+            c * r  # noqa: B018  -- the reference's TypeError at core.py:142
+        rel_objs.append(r)
+
+    N.require_gpu()
+    dev = N.device()
+    T = lambda a: torch.from_numpy(a).to(dev)  # noqa: E731
+    table = batch.SourceTable.from_dict(names, sr, dev)
+    max_len = int(lens.max())
+    plan = None if max_len <= 64 else batch.Plan.build(off, dev)
+    res = batch.consensus(T(off), T(sid), T(prob), table, plan=plan,
+                          max_len=max_len if plan is None else None, mode=mode, validate=False)
+    cons = res.consensus.cpu().numpy()
+    conf = res.confidence.cpu().numpy()
+    total = res.total_weight.cpu().numpy()
+    nu = res.n_unique.cpu().numpy()
+    usid = res.usid[:Ns].cpu().numpy()
+    nweight = res.nweight[:Ns].cpu().numpy()
+
+    out = []
+    for m in range(M):
+        n = int(lens[m])
+        if n == 0:
+            out.append(_no_signals())
+            continue
+        o, S = int(off[m]), int(nu[m])
+        us = usid[o:o + S]
+        rk = (us & 0x7FFFFFFF).tolist()
+        nw = nweight[o:o + S].tolist()
+        null = total[m] == 0  # core.py:131
+        out.append({
+            "schemaVersion": SCHEMA_VERSION,
+            "consensus": None if null else float(cons[m]),
+            "confidence": 0.0 if null else float(conf[m]),
+            "sourceWeights": [{"sourceId": names[r], "weight": rel_objs[r], "normalizedWeight": w}
+                              for r, w in zip(rk, nw)],
+            "normalization": {"totalWeight": float(total[m]), "sourceCount": S},
+            "diagnostics": {
+                "status": "computed",
+                "sources": n,
+                "uniqueSources": S,
+                "coldStartSources": [names[r] for r, u in zip(rk, us.tolist()) if u < 0],
+            },
+        })
+    return out
+
+
+def parse_batch(lines: Iterable[str]) -> Tuple[List[Any], List[Optional[str]], List[list],
+                                                 List[Optional[ValidationError]]]:
+    """Host pass: per non-blank line the payload (or None), its header/JSON error text (or
+    None), the probabilities to range-check and the first signal-level type error."""
+    payloads, errors, probs, type_errors = [], [], [], []
+    for line in lines:
+        if not line.strip():
+            continue
+        try:
+            payload = json.loads(line)
+            p, te = check_structure(payload)
+        except (json.JSONDecodeError, ValidationError) as exc:
+            payloads.append(None)
+            errors.append(f"Validation error: {exc}")
+            probs.append([])
+            type_errors.append(None)
+            continue
+        payloads.append(payload)
+        errors.append(None)
+        probs.append(p)
+        type_errors.append(te)
+    return payloads, errors, probs, type_errors
+
+
+def consensus_jsonl(lines: Iterable[str], source_reliability: Optional[dict] = None, *,
+                    dry_run: bool = False, mode: str = "exact") -> List[Tuple[bool, str]]:
+    """One ``(ok, text)`` per non-blank JSONL line: ``text`` is what ``bayesian-engine
+    consensus`` prints for that payload alone -- the ``json.dumps(indent=2)`` result on
+    success, the ``Validation error: ...`` line otherwise (cli.py:46-52)."""
+    payloads, errors, probs, type_errors = parse_batch(lines)
+    M = len(payloads)
+    lens = np.fromiter((len(p) for p in probs), np.int64, M)
+    if M and lens.sum() > 0:  # one range-check launch for the whole batch (core.py:59-60)
+        N.require_gpu()
+        dev = N.device()
+        off = np.zeros(M + 1, np.int64)
+        np.cumsum(lens, out=off[1:])
+        flat = np.fromiter((x for p in probs for x in p), np.float64, int(off[-1]))
+        err = batch.validate(torch.from_numpy(off).to(dev), torch.from_numpy(flat).to(dev)).cpu().numpy()
+        for i in range(M):
+            if errors[i] is None and err[i] >= 0:
+                errors[i] = f"Validation error: signals[{int(err[i])}].probability must be between 0 and 1"
+    for i in range(M):
+        if errors[i] is None and type_errors[i] is not None:
+            errors[i] = f"Validation error: {type_errors[i]}"
+
+    ok = [i for i in range(M) if errors[i] is None]
+    results = consensus_many([payloads[i]["signals"] for i in ok], source_reliability, mode=mode)
+    texts: List[Tuple[bool, str]] = [(False, e) if e is not None else (True, "") for e in errors]
+    for i, r in zip(ok, results):
+        if dry_run:
+            r["diagnostics"]["dryRun"] = True
+        texts[i] = (True, json.dumps(r, indent=2))
+    return texts
