@@ -9,8 +9,9 @@ whole JSONL batch goes through the same steps with the per-signal work batched:
 * source ids of every valid payload interned once in code-point order (Python ``sorted``,
   core.py:103), so a market's ranks sort exactly like its ids;
 * ONE consensus launch (length-binned plan) over the CSR of all markets;
-* each result rendered with ``json.dumps(indent=2)`` -- byte-identical to what the
-  single-payload CLI prints for that payload.
+* each result rendered as ``json.dumps(indent=2)`` would (:func:`render`, a fixed-shape
+  formatter: byte-identical, ~10x faster than the pure-Python indenting encoder) -- what
+  the single-payload CLI prints for that payload.
 
 All payloads of a batch share one ``source_reliability`` dict (the CLI's no-``--db`` path
 uses none: every source cold).  A non-numeric reliability/confidence in it raises the same
@@ -19,6 +20,7 @@ TypeError as compute_consensus would, for the whole batch.
 from __future__ import annotations
 
 import json
+from json.encoder import encode_basestring_ascii as _q
 from typing import Any, Iterable, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -29,7 +31,61 @@ from . import batch
 from .config import DEFAULT_CONFIDENCE, DEFAULT_RELIABILITY, SCHEMA_VERSION
 from .core import ValidationError, _as_float, _check_number, _no_signals, check_structure
 
-__all__ = ["consensus_many", "consensus_jsonl", "parse_batch"]
+__all__ = ["consensus_many", "consensus_jsonl", "parse_batch", "render"]
+
+_INF = float("inf")
+_TOP = ["schemaVersion", "consensus", "confidence", "sourceWeights", "normalization", "diagnostics"]
+_DIAG = ["status", "sources", "uniqueSources", "coldStartSources"]
+_SW = ["sourceId", "weight", "normalizedWeight"]
+
+
+def _num(x) -> str:
+    """json.dumps' rendering of a number / None (json/encoder.py floatstr, allow_nan)."""
+    if x is None:
+        return "null"
+    if x is True:
+        return "true"
+    if x is False:
+        return "false"
+    if isinstance(x, int):
+        return int.__repr__(x)
+    if x != x:
+        return "NaN"
+    if x == _INF:
+        return "Infinity"
+    if x == -_INF:
+        return "-Infinity"
+    return float.__repr__(x)
+
+
+def render(r: dict) -> str:
+    """``json.dumps(r, indent=2)`` for a compute_consensus result, byte for byte, without
+    the pure-Python indenting encoder (it dominated the batch: ~80 us per payload).  Any
+    dict not of the exact computed-result shape goes through json.dumps itself."""
+    d = r.get("diagnostics")
+    if (list(r) != _TOP or not isinstance(d, dict) or d.get("status") != "computed"
+            or list(d)[:4] != _DIAG or len(d) > 5 or (len(d) == 5 and list(d)[4] != "dryRun")
+            or list(r["normalization"]) != ["totalWeight", "sourceCount"] or r["schemaVersion"] != SCHEMA_VERSION):
+        return json.dumps(r, indent=2)
+    sw = r["sourceWeights"]
+    if any(list(w) != _SW for w in sw):
+        return json.dumps(r, indent=2)
+    if sw:
+        sws = "[\n" + ",\n".join(
+            '    {\n      "sourceId": %s,\n      "weight": %s,\n      "normalizedWeight": %s\n    }'
+            % (_q(w["sourceId"]), _num(w["weight"]), _num(w["normalizedWeight"])) for w in sw) + "\n  ]"
+    else:
+        sws = "[]"
+    cold = d["coldStartSources"]
+    cs = ("[\n" + ",\n".join("      " + _q(c) for c in cold) + "\n    ]") if cold else "[]"
+    tail = (',\n    "dryRun": ' + _num(d["dryRun"])) if len(d) == 5 else ""
+    nm = r["normalization"]
+    return ('{\n  "schemaVersion": "%s",\n  "consensus": %s,\n  "confidence": %s,\n  "sourceWeights": %s,\n'
+            '  "normalization": {\n    "totalWeight": %s,\n    "sourceCount": %s\n  },\n'
+            '  "diagnostics": {\n    "status": "computed",\n    "sources": %s,\n    "uniqueSources": %s,\n'
+            '    "coldStartSources": %s%s\n  }\n}'
+            % (SCHEMA_VERSION, _num(r["consensus"]), _num(r["confidence"]), sws, _num(nm["totalWeight"]),
+               _num(nm["sourceCount"]), _num(d["sources"]), _num(d["uniqueSources"]), cs, tail))
 
 
 def consensus_many(signal_lists: Sequence[list], source_reliability: Optional[dict] = None, *,
@@ -159,5 +215,5 @@ def consensus_jsonl(lines: Iterable[str], source_reliability: Optional[dict] = N
     for i, r in zip(ok, results):
         if dry_run:
             r["diagnostics"]["dryRun"] = True
-        texts[i] = (True, json.dumps(r, indent=2))
+        texts[i] = (True, render(r))
     return texts

@@ -24,3 +24,31 @@ def test_parse_batch_structure_errors_match_golden():
         else:  # range errors are the GPU launch's to find
             assert "between 0 and 1" in c["error"], c["name"]
     assert payloads[-1] is None and errors[-1].startswith("Validation error: ")
+
+
+def test_render_is_json_dumps_indent2():
+    """render() must be byte-identical to json.dumps(indent=2) on every value kind a result
+    can hold: NaN/inf, -0.0, int and bool weights, null consensus, unicode/escaped ids,
+    empty and non-empty cold lists, dryRun; other shapes fall back to json.dumps."""
+    import random
+    from bayesian_engine.jsonl import render
+    rnd = random.Random(5)
+    vals = [0.0, -0.0, 1.0, 0.1, 1e-320, 1e300, float("nan"), float("inf"), -float("inf"), 0.6966666666666667,
+            1, 0, -3, True, False]
+    ids = ["a", "src-001", "Ä", "éé", "x\"y", "tab\t", "☃", "\U0001f600", " sp"]
+    for i in range(400):
+        S = rnd.randint(1, 6)
+        sw = [{"sourceId": rnd.choice(ids), "weight": rnd.choice(vals), "normalizedWeight": rnd.choice(vals[:10])}
+              for _ in range(S)]
+        r = {"schemaVersion": "1.0.0", "consensus": rnd.choice([None, rnd.choice(vals[:10])]),
+             "confidence": rnd.choice(vals[:10]), "sourceWeights": sw,
+             "normalization": {"totalWeight": rnd.choice(vals[:10]), "sourceCount": S},
+             "diagnostics": {"status": "computed", "sources": rnd.randint(1, 99), "uniqueSources": S,
+                             "coldStartSources": rnd.sample(ids, rnd.randint(0, 3))}}
+        if i % 3 == 0:
+            r["diagnostics"]["dryRun"] = True
+        assert render(r) == json.dumps(r, indent=2)
+    no_sig = {"schemaVersion": "1.0.0", "consensus": None, "confidence": 0.0, "sourceWeights": [],
+              "normalization": {"totalWeight": 0.0, "sourceCount": 0},
+              "diagnostics": {"status": "no_signals", "sources": 0}}
+    assert render(no_sig) == json.dumps(no_sig, indent=2)
