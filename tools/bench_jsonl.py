@@ -43,11 +43,11 @@ def main():
         res = jsonl.consensus_many([p["signals"] for p in payloads])
         torch.cuda.synchronize()
         t2 = time.perf_counter()
-        texts = [json.dumps(r, indent=2) for r in res]
+        texts = [jsonl.render(r) for r in res]
         t3 = time.perf_counter()
         out = jsonl.consensus_jsonl(lines)
         t4 = time.perf_counter()
-        assert all(ok for ok, _ in out) and out[-1][1] == texts[-1]
+        assert all(ok for ok, _ in out) and out[-1][1] == texts[-1] == json.dumps(res[-1], indent=2)
         ph = {"parse_check_s": t1 - t0, "intern_launch_assemble_s": t2 - t1, "render_s": t3 - t2, "end_to_end_s": t4 - t3}
         if best is None or ph["end_to_end_s"] < best["end_to_end_s"]:
             best = ph
