@@ -95,8 +95,6 @@ def consensus_many(signal_lists: Sequence[list], source_reliability: Optional[di
     if M == 0:
         return []
     sr = source_reliability or {}
-    names = sorted({s["sourceId"] for sig in signal_lists for s in sig})
-    rank = {n: i for i, n in enumerate(names)}
     lens = np.fromiter((len(sig) for sig in signal_lists), np.int64, M)
     off = np.zeros(M + 1, np.int64)
     np.cumsum(lens, out=off[1:])
@@ -104,12 +102,18 @@ def consensus_many(signal_lists: Sequence[list], source_reliability: Optional[di
     if Ns == 0:
         return [_no_signals() for _ in range(M)]
 
+    ids = [s["sourceId"] for sig in signal_lists for s in sig]
     raw = [s["probability"] for sig in signal_lists for s in sig]
-    for p in raw:
-        if not isinstance(p, (int, float)):
-            0 + p  # noqa: B018  -- builtin sum()'s TypeError (core.py:116)
-    prob = np.fromiter((_as_float(p) for p in raw), np.float64, Ns)
-    sid = np.fromiter((rank[s["sourceId"]] for sig in signal_lists for s in sig), np.int32, Ns)
+    names = sorted(set(ids))
+    rank = dict(zip(names, range(len(names))))
+    sid = np.fromiter(map(rank.__getitem__, ids), np.int32, Ns)
+    if set(map(type, raw)) == {float}:  # the JSON common case: one C-level conversion
+        prob = np.array(raw, np.float64)
+    else:
+        for p in raw:
+            if not isinstance(p, (int, float)):
+                0 + p  # noqa: B018  -- builtin sum()'s TypeError (core.py:116)
+        prob = np.fromiter((_as_float(p) for p in raw), np.float64, Ns)
     rel_objs = []
     for n in names:
         d = sr.get(n, {})
@@ -128,36 +132,40 @@ def consensus_many(signal_lists: Sequence[list], source_reliability: Optional[di
     plan = None if max_len <= 64 else batch.Plan.build(off, dev)
     res = batch.consensus(T(off), T(sid), T(prob), table, plan=plan,
                           max_len=max_len if plan is None else None, mode=mode, validate=False)
-    cons = res.consensus.cpu().numpy()
-    conf = res.confidence.cpu().numpy()
-    total = res.total_weight.cpu().numpy()
-    nu = res.n_unique.cpu().numpy()
+    # one device->host copy per array, then plain lists (numpy scalar/slice access per
+    # market cost more than the whole launch)
+    cons = res.consensus.cpu().tolist()
+    conf = res.confidence.cpu().tolist()
+    total = res.total_weight.cpu().tolist()
+    nu = res.n_unique.cpu().tolist()
     usid = res.usid[:Ns].cpu().numpy()
-    nweight = res.nweight[:Ns].cpu().numpy()
+    rank_all = (usid & 0x7FFFFFFF).tolist()
+    cold_all = (usid < 0).tolist()
+    nweight = res.nweight[:Ns].cpu().tolist()
+    offl = off.tolist()
 
     out = []
     for m in range(M):
-        n = int(lens[m])
+        o = offl[m]
+        n = offl[m + 1] - o
         if n == 0:
             out.append(_no_signals())
             continue
-        o, S = int(off[m]), int(nu[m])
-        us = usid[o:o + S]
-        rk = (us & 0x7FFFFFFF).tolist()
-        nw = nweight[o:o + S].tolist()
+        S = nu[m]
+        rk = rank_all[o:o + S]
         null = total[m] == 0  # core.py:131
         out.append({
             "schemaVersion": SCHEMA_VERSION,
-            "consensus": None if null else float(cons[m]),
-            "confidence": 0.0 if null else float(conf[m]),
+            "consensus": None if null else cons[m],
+            "confidence": 0.0 if null else conf[m],
             "sourceWeights": [{"sourceId": names[r], "weight": rel_objs[r], "normalizedWeight": w}
-                              for r, w in zip(rk, nw)],
-            "normalization": {"totalWeight": float(total[m]), "sourceCount": S},
+                              for r, w in zip(rk, nweight[o:o + S])],
+            "normalization": {"totalWeight": total[m], "sourceCount": S},
             "diagnostics": {
                 "status": "computed",
                 "sources": n,
                 "uniqueSources": S,
-                "coldStartSources": [names[r] for r, u in zip(rk, us.tolist()) if u < 0],
+                "coldStartSources": [names[r] for r, c in zip(rk, cold_all[o:o + S]) if c],
             },
         })
     return out
