@@ -40,7 +40,7 @@ from .config import (
     MAX_UPDATE_STEP,
 )
 from .decay import apply_reliability_decay, days_since_update
-from .timeutil import NO_TIMESTAMP, dt_to_us, iso_to_us, us_to_iso
+from .timeutil import NO_TIMESTAMP, dt_to_us, iso_to_us, iso_to_us_many, us_to_iso
 
 __all__ = ["ReliabilityRecord", "SQLiteReliabilityStore", "DEFAULT_RELIABILITY", "DEFAULT_CONFIDENCE",
            "MAX_UPDATE_STEP", "DECAY_HALF_LIFE_DAYS", "DECAY_MINIMUM"]
@@ -180,11 +180,15 @@ class SQLiteReliabilityStore:
         conf = np.full(S, DEFAULT_CONFIDENCE)
         t_us = np.full(S, NO_TIMESTAMP, np.int64)
         present = np.zeros(S, np.uint8)
-        for sid, r, c, ts in rows:
-            i = idx.get(sid)
-            if i is None:
-                continue
-            rel[i], conf[i], t_us[i], present[i] = r, c, iso_to_us(ts), 1
+        if rows:
+            pos = np.fromiter((idx.get(r[0], -1) for r in rows), np.int64, len(rows))
+            keep = pos >= 0
+            cols = list(zip(*rows))
+            p = pos[keep]
+            rel[p] = np.asarray(cols[1], np.float64)[keep]
+            conf[p] = np.asarray(cols[2], np.float64)[keep]
+            t_us[p] = iso_to_us_many(cols[3])[keep]
+            present[p] = 1
         dev = device or N.device()
         T = lambda a: torch.from_numpy(a).to(dev)  # noqa: E731
         return batch.ReliabilityTable(T(rel), T(conf), T(t_us), T(present), list(names))

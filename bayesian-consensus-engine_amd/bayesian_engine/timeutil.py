@@ -10,7 +10,9 @@ correctly rounded in both).
 from __future__ import annotations
 
 from datetime import datetime, timezone
-from typing import Union
+from typing import Sequence, Union
+
+import numpy as np
 
 NO_TIMESTAMP = -(2**63)  # "falsy or unparseable" -> days_since_update returns 0.0
 _EPOCH = datetime(1970, 1, 1, tzinfo=timezone.utc)
@@ -33,6 +35,12 @@ def iso_to_us(value: Union[str, datetime, None]) -> int:
         except ValueError:
             return NO_TIMESTAMP
     return dt_to_us(value)
+
+
+def iso_to_us_many(values: Sequence[Union[str, datetime, None]]) -> np.ndarray:
+    """``[iso_to_us(v) for v in values]`` as int64.  (A numpy datetime64 parse of the UTC
+    stamps was measured slower than CPython's C ``fromisoformat``: 0.73 vs 0.58 s per 1M.)"""
+    return np.fromiter(map(iso_to_us, values), np.int64, len(values))
 
 
 def us_to_iso(us: int) -> str:

@@ -52,3 +52,18 @@ def test_render_is_json_dumps_indent2():
               "normalization": {"totalWeight": 0.0, "sourceCount": 0},
               "diagnostics": {"status": "no_signals", "sources": 0}}
     assert render(no_sig) == json.dumps(no_sig, indent=2)
+
+
+def test_iso_to_us_many_matches_per_value():
+    """Bulk stamp parsing (f1 load_table) == the per-value mirror of decay.py:125-141."""
+    from datetime import datetime, timezone
+    from bayesian_engine.timeutil import iso_to_us, iso_to_us_many
+    vals = ["2026-03-01T12:34:56.123456+00:00", "2026-03-01T12:34:56+00:00", "1969-12-31T23:59:59.999999+00:00",
+            "2026-02-30T00:00:00+00:00", "2026-03-01T12:34:56+02:00", "2026-03-01T12:34:56", "2026-03-01",
+            "", None, "garbage", "2026-13-01T00:00:00+00:00", "2024-02-29T23:59:59.000001+00:00",
+            datetime(2026, 1, 1, tzinfo=timezone.utc), "0001-01-01T00:00:00+00:00", "9999-12-31T23:59:59.999999+00:00"]
+    want = [iso_to_us(v) for v in vals]
+    assert iso_to_us_many(vals).tolist() == want
+    good = [v for v in vals if isinstance(v, str) and v.endswith("+00:00") and "02-30" not in v and "-13-" not in v]
+    assert iso_to_us_many(good).tolist() == [iso_to_us(v) for v in good]
+    assert iso_to_us_many([]).tolist() == []
