@@ -98,7 +98,7 @@ def check_structure(payload: dict[str, Any]) -> tuple[list[float], ValidationErr
         if not isinstance(probability, (int, float)):
             type_error = ValidationError(f"signals[{idx}].probability must be a number")
             break
-        probs.append(_as_float(probability))
+        probs.append(probability if type(probability) is float else _as_float(probability))
     return probs, type_error
 
 
