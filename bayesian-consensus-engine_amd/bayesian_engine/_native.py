@@ -46,6 +46,7 @@ _SIGS = {
     "bce_abi_version": (C.c_int, []),
     "bce_last_error": (C.c_char_p, []),
     "bce_device_count": (C.c_int, []),
+    "bce_fault_check": (C.c_int, [_vp]),
     "bce_consensus_csr": (C.c_int, [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _i32, _vp, _i64, _i32,
                                     _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "bce_table_pack": (C.c_int, [_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
@@ -108,6 +109,13 @@ def check(rc: int, what: str = "") -> None:
     if rc != BCE_OK:
         msg = lib().bce_last_error().decode(errors="replace")
         raise BCEError(f"{what or 'bce call'} failed (status {rc}): {msg}")
+
+
+def check_faults(device=None, what: str = "") -> None:
+    """Synchronise the current stream and raise :class:`BCEError` if a kernel recorded a
+    device fault (bce_fault_check): a persistent wave that gave up waiting, a sid >=
+    n_sources, a market longer than the max_len it was launched with."""
+    check(lib().bce_fault_check(stream(device)), what or "device fault check")
 
 
 def ptr(t, row_strided: bool = False) -> C.c_void_p:

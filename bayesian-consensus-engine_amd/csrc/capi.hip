@@ -3,6 +3,7 @@
 #include <stdio.h>
 
 #include "bce_internal.hpp"
+#include "consensus_common.hpp"
 
 namespace bce {
 
@@ -37,7 +38,47 @@ int cu_count() {
   return cached;
 }
 
+int* fault_word() {
+  static int* words[64] = {nullptr};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (!words[dev]) {
+    int* p = nullptr;
+    if (hipMalloc((void**)&p, sizeof(int)) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, sizeof(int)) != hipSuccess) return nullptr;
+    words[dev] = p;
+  }
+  return words[dev];
+}
+
+static const char* fault_text(int code) {
+  switch (code) {
+    case kFaultSpinLoader: return "consensus_pipe_kernel: loader wave timed out waiting for a free slot";
+    case kFaultSpinCompute: return "consensus_pipe_kernel: compute wave timed out waiting for its tile";
+    case kFaultSid: return "consensus: a sid is >= n_sources (its row read was clamped)";
+    case kFaultTooLong: return "consensus: a market is longer than the launch's max_len (left unprocessed)";
+    default: return "unknown device fault";
+  }
+}
+
 }  // namespace bce
+
+extern "C" int bce_fault_check(void* stream) {
+  int* w = bce::fault_word();
+  if (!w) {
+    bce::set_error("bce_fault_check: no fault word on this device");
+    return BCE_EHIP;
+  }
+  hipStream_t st = bce::as_stream(stream);
+  int h = 0;
+  BCE_HIP(hipMemcpyAsync(&h, w, sizeof h, hipMemcpyDeviceToHost, st));
+  BCE_HIP(hipStreamSynchronize(st));
+  if (h == 0) return BCE_OK;
+  BCE_HIP(hipMemsetAsync(w, 0, sizeof(int), st));
+  BCE_HIP(hipStreamSynchronize(st));
+  bce::set_error("device fault %d: %s", h, bce::fault_text(h));
+  return BCE_EHIP;
+}
 
 extern "C" int bce_abi_version(void) { return BCE_ABI_VERSION; }
 extern "C" const char* bce_last_error(void) { return bce::g_err; }

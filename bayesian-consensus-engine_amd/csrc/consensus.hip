@@ -24,15 +24,13 @@
 //
 // FP contraction is off for the whole file: every mul/add rounds like CPython.
 #include <stdio.h>
-#include <type_traits>
 #include <stdlib.h>
+#include <type_traits>
 
-#include "bce_device.hpp"
-#include "bce_internal.hpp"
+#include "consensus_common.hpp"
 
 #pragma clang fp contract(off)
 
-// Experiment-only switches (tools/ablate.py builds variants; the product build uses 0).
 #ifndef BCE_ABLATE
 #define BCE_ABLATE 0
 #endif
@@ -89,35 +87,6 @@
 #endif
 
 namespace bce {
-
-struct ConsArgs {
-  const int64_t* offsets;
-  const int32_t* sid;
-  const double* prob;
-  const double2* relconf;    // [S] interleaved {reliability, confidence}: one 16-B gather
-  const uint32_t* pbits;     // [ceil(S/32)] present bitmask (bit s%32 of word s/32)
-  int32_t n_sources;
-  int64_t n_signals;
-  const int32_t* list;  // nullable
-  int64_t n_list;       // number of markets to process
-  double* consensus;
-  double* confidence;
-  double* total_weight;
-  int32_t* n_unique;
-  int32_t* err_idx;   // nullable
-  int32_t* usid;      // nullable
-  double* weight;     // nullable
-  double* nweight;    // nullable
-  int32_t mode;
-  void* scratch;      // long kernel, global variant
-  int64_t scratch_stride;  // elements (keys) per workgroup slice
-};
-
-constexpr int kBitsLds = 512;  // present bitmask words staged in LDS (S <= 16384)
-
-__device__ __forceinline__ bool is_present(const uint32_t* bits, int s) {
-  return ((bits[s >> 5] >> (s & 31)) & 1u) != 0;
-}
 
 // ------------------------------------------------------------------------------------
 // short markets: wave-per-tile, lane-per-signal then lane-per-market
@@ -385,67 +354,6 @@ void consensus_seg_kernel(ConsArgs a) {
 // ------------------------------------------------------------------------------------
 // short markets, lane per market: consensus_lpm_kernel<G>  (n <= G, G in {8, 16, 32})
 // ------------------------------------------------------------------------------------
-// Batcher odd-even merge sort network for N (power of two) keys, generated at compile
-// time; with full unrolling every key index is a constant, so the keys live in VGPRs.
-template <int N>
-struct OemNet {
-  static constexpr int count() {
-    int c = 0;
-    for (int p = 1; p < N; p <<= 1)
-      for (int k = p; k >= 1; k >>= 1)
-        for (int j = k % p; j + k < N; j += 2 * k)
-          for (int i = 0; i < k && i + j + k < N; ++i)
-            if ((i + j) / (2 * p) == (i + j + k) / (2 * p)) ++c;
-    return c;
-  }
-  static constexpr int C = count();
-  struct Pairs {
-    int a[C > 0 ? C : 1];
-    int b[C > 0 ? C : 1];
-  };
-  static constexpr Pairs make() {
-    Pairs r{};
-    int c = 0;
-    for (int p = 1; p < N; p <<= 1)
-      for (int k = p; k >= 1; k >>= 1)
-        for (int j = k % p; j + k < N; j += 2 * k)
-          for (int i = 0; i < k && i + j + k < N; ++i)
-            if ((i + j) / (2 * p) == (i + j + k) / (2 * p)) {
-              r.a[c] = i + j;
-              r.b[c] = i + j + k;
-              ++c;
-            }
-    return r;
-  }
-};
-
-template <int N>
-__device__ __forceinline__ void oem_sort(unsigned (&key)[N]) {
-  constexpr auto P = OemNet<N>::make();
-#pragma unroll
-  for (int c = 0; c < OemNet<N>::C; ++c) {
-    const unsigned x = key[P.a[c]], y = key[P.b[c]];
-    key[P.a[c]] = x < y ? x : y;
-    key[P.b[c]] = x < y ? y : x;
-  }
-}
-
-// Same network carrying a payload (the probability) with each key.
-template <int N>
-__device__ __forceinline__ void oem_sort_kv(unsigned (&key)[N], double (&val)[N]) {
-  constexpr auto P = OemNet<N>::make();
-#pragma unroll
-  for (int c = 0; c < OemNet<N>::C; ++c) {
-    const unsigned x = key[P.a[c]], y = key[P.b[c]];
-    const double vx = val[P.a[c]], vy = val[P.b[c]];
-    const bool sw = y < x;
-    key[P.a[c]] = sw ? y : x;
-    key[P.b[c]] = sw ? x : y;
-    val[P.a[c]] = sw ? vy : vx;
-    val[P.b[c]] = sw ? vx : vy;
-  }
-}
-
 // LDS ordering inside a single-wave workgroup: the wave's LDS instructions execute in
 // order, so a compiler barrier + lgkmcnt drain is all a cross-lane hand-off needs.
 __device__ __forceinline__ void wave_sync() {
@@ -455,11 +363,6 @@ __device__ __forceinline__ void wave_sync() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #endif
 }
-
-// Cross-lane LDS hand-off inside ONE wave (waves of a workgroup run independently): the
-// wave's LDS instructions execute in order, so draining lgkmcnt behind a compiler
-// barrier orders every earlier ds_write before every later ds_read / LDS-DMA.
-__device__ __forceinline__ void wave_sync_lds() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 __device__ __forceinline__ void dma4(const void* g, void* lds) {
   __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds, 4, 0, 0);
@@ -957,27 +860,6 @@ __device__ __forceinline__ void wait_lgkm0() {
   asm volatile("" ::: "memory");
 }
 
-// LDS-DMA issued from inline asm.  The compiler's wait-count pass treats every LDS
-// access after a *builtin* LDS-DMA as a possible alias and drains vmcnt(0) in front of
-// it, which would make the copy-out of tile k wait for the DMA of tile k+1.  The stream
-// kernel orders its images itself (one explicit vmcnt(0) before the image is read; the
-// staging rows are never DMA targets), so the DMA is hidden from that pass.
-// Cache policy of the streamed (read-once) LDS-DMA loads ("nt", "sc1 nt", ... measured no
-// faster than the default on C2: the source table's gathers are not losing lines to them).
-#ifndef BCE_DMA_CP
-#define BCE_DMA_CP ""
-#endif
-__device__ __forceinline__ void dma_b128(const void* g, const void* lds) {
-  const uint32_t l = (uint32_t)(uintptr_t)lds;
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off " BCE_DMA_CP ::"s"(l), "v"(g)
-               : "memory", "m0");
-}
-__device__ __forceinline__ void dma_b32(const void* g, const void* lds) {
-  const uint32_t l = (uint32_t)(uintptr_t)lds;
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off " BCE_DMA_CP ::"s"(l), "v"(g)
-               : "memory", "m0");
-}
-
 template <int G, int TM, int WPB, int CH>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(BCE_FLAT_WPE, 8)))
 void consensus_stream_kernel(ConsArgs a) {
@@ -1284,15 +1166,10 @@ void consensus_stream_kernel(ConsArgs a) {
 #if BCE_PIPE_PROF
 __device__ unsigned long long g_pipe_prof[16];  // s_memtime cycles per compute-wave phase (debug build)
 #endif
-constexpr int kSpinCap = 1 << 22;  // ~0.1-0.3 s of s_sleep polling per wait
-
-// Acquire-load of an LDS flag, broadcast to a wave-uniform (SGPR) value: every spin and
-// branch on a flag is then scalar control flow (a per-lane view of the same word makes
-// the compiler build divergent loop exits around it).
-__device__ __forceinline__ int ldsflag(int* f) {
-  const int v = __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-  return __builtin_amdgcn_readfirstlane(v);
-}
+#ifndef BCE_SPIN_CAP
+#define BCE_SPIN_CAP (1 << 22)  // ~0.1-0.3 s of s_sleep polling per wait
+#endif
+constexpr int kSpinCap = BCE_SPIN_CAP;
 
 #ifndef BCE_PIPE_C32
 #define BCE_PIPE_C32 4  // compute waves at G = 32
@@ -1452,7 +1329,10 @@ void consensus_pipe_kernel(ConsArgs a) {
           int spins = 0;
           while (ldsflag(&sFree[s]) < need) {
             __builtin_amdgcn_s_sleep(2);
-            if (++spins > kSpinCap) return;  // never expected; bounded so a bug cannot hang the GPU
+            if (++spins > kSpinCap) {  // never expected: bounded so a bug cannot hang the GPU,
+              raise_fault(a.fault, kFaultSpinLoader);  // and reported (bce_fault_check)
+              return;
+            }
           }
         }
       }
@@ -1572,7 +1452,10 @@ void consensus_pipe_kernel(ConsArgs a) {
     int spins = 0;
     while (ldsflag(&sReady[s]) != seq + 1) {
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > kSpinCap) return;  // never expected; bounded so a bug cannot hang the GPU
+      if (++spins > kSpinCap) {  // never expected: bounded so a bug cannot hang the GPU,
+        raise_fault(a.fault, kFaultSpinCompute);  // and reported (bce_fault_check)
+        return;
+      }
     }
     PROF_MARK(0);  // waiting for a loaded slot
     const int64_t tile0 = sTile[s];
@@ -2611,6 +2494,8 @@ int launch_flat(const ConsArgs& a, hipStream_t st) {
 }
 
 int launch_seg_for_len(int max_len, const ConsArgs& a, hipStream_t st) {
+  if (a.list == nullptr && max_len > 16 && max_len <= 32 && a.n_sources <= kTabMaxSources)
+    return launch_tab32(a, st);
   if (BCE_FLAT == 3 && a.list == nullptr && max_len <= 32 && a.n_sources <= 32 * kBitsLds && a.n_signals >= 4 &&
       a.usid && a.weight && a.nweight) {
     if (max_len <= 8) return launch_pipe<8>(a, st);
@@ -2763,6 +2648,7 @@ extern "C" int bce_consensus_csr(const int64_t* offsets, int64_t n_markets, cons
   a.consensus = consensus; a.confidence = confidence; a.total_weight = total_weight;
   a.n_unique = n_unique; a.err_idx = err_idx; a.usid = usid; a.weight = weight; a.nweight = nweight;
   a.mode = mode;
+  a.fault = fault_word();
   if (a.n_list == 0) return BCE_OK;
   int64_t L = max_len;
   if (L <= 0) {  // unknown: measure on device (synchronises)
@@ -2857,6 +2743,7 @@ extern "C" int bce_consensus_planned(const int64_t* offsets, int64_t n_markets, 
   base.n_sources = n_sources; base.n_signals = n_signals; base.consensus = consensus; base.confidence = confidence;
   base.total_weight = total_weight; base.n_unique = n_unique; base.err_idx = err_idx;
   base.usid = usid; base.weight = weight; base.nweight = nweight; base.mode = mode;
+  base.fault = fault_word();
   const bool seg_ok = n_sources <= (1 << 25);
   for (int b = 0; b < BCE_NBINS; ++b) {
     ConsArgs a = base;

@@ -1,0 +1,485 @@
+// consensus_tab.hip -- core.compute_consensus (core.py:63-179) for contiguous markets with
+// n <= 32, the source table held in LDS.
+//
+// Why this shape (tools/gather_probe.hip, profiles/r02_gather_probe.txt): streaming the
+// C2 bytes alone takes 0.185 ms; adding one random 16-B {rel, conf} gather per signal
+// from the 160 KB table in global memory takes it to 0.288 ms (the round-1 kernel's time:
+// those gathers, not HBM, bound it), while the same gathers served from LDS cost almost
+// nothing (0.189 ms).  So one workgroup per CU stages the whole table (16 B per source +
+// the present bitmask, S <= kTabMaxSources = the 160 KB LDS) once, and everything else
+// stays in VGPRs -- no LDS staging ring, no producer/consumer waves:
+//
+//  load       a wave owns a tile of 64 consecutive markets.  A REGULAR tile (every market
+//             has 32 signals, 16-B aligned) is read with fully coalesced 16-B loads whose
+//             lane->address map puts the position bits on lane bits 5..3 and the market
+//             bits on lane bits 2..0 + the register index; three butterflies that swap
+//             lane bits 5, 4, 3 with register-index bits (v_permlane32_swap,
+//             v_permlane16_swap, DPP row_ror:8) leave lane = market, register = position.
+//             Other tiles (ragged lengths, the last tile, misaligned shards) load per lane.
+//  sort       keys (sid << 5 | position) with the probability as payload, Batcher
+//             odd-even merge network in VGPRs: duplicates of a source stay in input order.
+//  walk       sorted positions left to right: {rel, conf} from LDS (ds_read_b128, eight
+//             ahead), duplicate runs summed in input order and averaged (core.py:115-116),
+//             the reference's three left-to-right chains over unique sources
+//             (core.py:120,135-143) -- each lane is one market, so the exact order is free.
+//  compact    the per-unique (usid, weight) pairs are emitted at their run's last sorted
+//             position, then shifted down by the number of duplicates before them (a
+//             five-stage shift network, skipped when no lane of the wave has duplicates).
+//  store      per-market scalars lane = market (coalesced); per-unique outputs go back
+//             through the same butterflies and leave as coalesced 16-B stores, slots past
+//             n_unique untouched (narrower stores for the one partial chunk per market).
+//             normalizedWeight = weight / total is divided in the store layout, the
+//             market's total fetched with ds_bpermute.
+// Validation (core.py:59-60: first p < 0 or p > 1, NaN passes) reads the probabilities in
+// input order before the sort.  Exact mode only: every sum is the reference's own order.
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "consensus_common.hpp"
+
+#pragma clang fp contract(off)
+
+namespace bce {
+namespace {
+
+#ifndef BCE_TAB_WAVES
+#define BCE_TAB_WAVES 8
+#endif
+#ifndef BCE_TAB_PREFETCH
+#define BCE_TAB_PREFETCH 0
+#endif
+constexpr int kTabWaves = BCE_TAB_WAVES;  // waves per workgroup; one workgroup per CU (LDS-bound)
+constexpr int kTabRing = 8;    // LDS table reads issued ahead of the walk
+
+// ---- lane-bit <-> register-bit butterflies -------------------------------------------
+// For a register pair (a: index bit 0, b: index bit 1) swap lane bit L with that index
+// bit: a' = bit_L ? b[lane ^ 2^L] : a,  b' = bit_L ? b : a[lane ^ 2^L] -- exactly what
+// v_permlane32_swap (L = 5) and v_permlane16_swap (L = 4) do, one instruction per pair.
+__device__ __forceinline__ void bfly5(uint32_t& a, uint32_t& b) {
+  const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+  a = r[0];
+  b = r[1];
+}
+__device__ __forceinline__ void bfly4(uint32_t& a, uint32_t& b) {
+  const auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
+  a = r[0];
+  b = r[1];
+}
+// Swap lane bits 5, 4 with dword-index bits 3, 2 of r[N] (an involution).
+template <int N>
+__device__ __forceinline__ void xpose(uint32_t (&r)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+    if (!(i & 8)) bfly5(r[i], r[i | 8]);
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+    if (!(i & 4)) bfly4(r[i], r[i | 4]);
+}
+
+// Regular-tile address maps (tile = 64 markets x 32 signals from B; load index k,
+// r16 = lane & 15, c = lane >> 4; each wave-instruction reads 64 contiguous bytes of 16
+// markets):
+//   sid   k < 8:  market 16(k&3) + r16, positions 16(k>>2) + 4c + d    dword index 4k + d
+//   prob  k < 16: market 16(k&3) + r16, positions 8(k>>2) + 2c + h     double index 2k + h
+// Swapping lane bits (5, 4) with load-index bits (1, 0) makes the lane the market and the
+// register index the position, for both arrays.
+// Odd-even merge network over 31-bit keys with a 64-bit payload, branch- and SGPR-free:
+// the swap mask is the sign of y - x (keys < 2^31), the payload moves with v_bfi_b32.
+// (Compare-and-select would give every comparator of a stage its own SGPR-pair condition;
+// the 191-comparator network then spills SGPRs.)
+__device__ __forceinline__ void oem_sort_kv31(unsigned (&key)[32], double (&val)[32]) {
+  constexpr auto P = OemNet<32>::make();
+#pragma unroll
+  for (int c = 0; c < OemNet<32>::C; ++c) {
+    const unsigned x = key[P.a[c]], y = key[P.b[c]];
+    unsigned m = (unsigned)((int)(y - x) >> 31);  // all ones <=> y < x
+    asm("" : "+v"(m));
+    key[P.a[c]] = min(x, y);
+    key[P.b[c]] = max(x, y);
+    const uint64_t vx = (uint64_t)__double_as_longlong(val[P.a[c]]), vy = (uint64_t)__double_as_longlong(val[P.b[c]]);
+    const uint64_t mm = ((uint64_t)m << 32) | m;
+    val[P.a[c]] = __longlong_as_double((long long)((mm & vy) | (~mm & vx)));
+    val[P.b[c]] = __longlong_as_double((long long)((mm & vx) | (~mm & vy)));
+  }
+}
+
+__device__ __forceinline__ double dbl(uint32_t lo, uint32_t hi) {
+  return __hiloint2double((int)hi, (int)lo);
+}
+__device__ __forceinline__ uint32_t lo32(double x) { return (uint32_t)__double_as_longlong(x); }
+__device__ __forceinline__ uint32_t hi32(double x) { return (uint32_t)((uint64_t)__double_as_longlong(x) >> 32); }
+
+__global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char tab_smem[];
+  const int S = a.n_sources > 0 ? a.n_sources : 1;
+  const int nwords = (S + 31) >> 5;
+  double2* const sT = reinterpret_cast<double2*>(tab_smem);
+  uint32_t* const sB = reinterpret_cast<uint32_t*>(tab_smem + 16 * (size_t)S);
+  // ---- stage the table once per workgroup ----------------------------------------------
+  if (a.n_sources > 0) {
+    int i = threadIdx.x;
+    for (; i + 3 * 64 * kTabWaves < S; i += 4 * 64 * kTabWaves) {
+      double2 v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = a.relconf[i + q * 64 * kTabWaves];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sT[i + q * 64 * kTabWaves] = v[q];
+    }
+    for (; i < S; i += 64 * kTabWaves) sT[i] = a.relconf[i];
+    for (int j = threadIdx.x; j < nwords; j += 64 * kTabWaves) sB[j] = a.pbits[j];
+  } else if (threadIdx.x == 0) {
+    sT[0] = make_double2(0.5, 0.25);  // DEFAULT_RELIABILITY / _CONFIDENCE (config.py:17-18)
+    sB[0] = 0u;
+  }
+  __syncthreads();
+
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // wave-uniform loop
+  const unsigned smax = (unsigned)(S - 1);
+  const int64_t M = a.n_list;
+  const int64_t n_tiles = (M + 63) >> 6;
+  const int64_t stride = (int64_t)gridDim.x * kTabWaves;
+  const bool do_u = a.usid != nullptr, do_w = a.weight != nullptr, do_nw = a.nweight != nullptr;
+  const bool do_any = do_u || do_w || do_nw;
+
+  // Tile metadata: this lane's market bounds, the tile base B and whether the tile is
+  // regular (64 markets x 32 signals from a 16-B aligned B).
+  struct Meta {
+    int64_t off;
+    int n;
+    int64_t B;
+    bool reg;
+  };
+  auto meta = [&](int64_t tile, int lane) -> Meta {
+    Meta m{0, 0, 0, false};
+    if (tile >= n_tiles) return m;
+    const int64_t mk = tile * 64 + lane;
+    int64_t end = 0;
+    if (mk < M) {
+      m.off = a.offsets[mk];
+      end = a.offsets[mk + 1];
+    }
+    m.n = (int)(end - m.off);
+    if (ballot(mk < M && (m.n < 0 || m.n > 32))) {  // the launch promised max_len <= 32
+      raise_fault(a.fault, kFaultTooLong);
+      if (m.n < 0 || m.n > 32) m.n = 0;
+    }
+    m.B = ((int64_t)__builtin_amdgcn_readfirstlane((int)(m.off >> 32)) << 32) |
+          (uint32_t)__builtin_amdgcn_readfirstlane((int)m.off);
+    m.reg = ballot(!(mk < M && m.n == 32 && m.off == m.B + 32 * (int64_t)lane)) == 0 &&
+            ((((uintptr_t)(a.sid + m.B)) | ((uintptr_t)(a.prob + m.B))) & 15) == 0;
+    return m;
+  };
+  // Regular-tile loads (the address maps above); raw, not yet transposed.
+  auto load_regular = [&](int64_t B, int lane, uint32_t (&rs)[32], uint32_t (&rp)[64]) {
+    const int r16 = lane & 15, c = lane >> 4;
+    const uint32_t* sb = reinterpret_cast<const uint32_t*>(a.sid + B);
+    const double* pb = a.prob + B;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint4 v = *reinterpret_cast<const uint4*>(sb + 32 * (16 * (k & 3) + r16) + 16 * (k >> 2) + 4 * c);
+      rs[4 * k] = v.x; rs[4 * k + 1] = v.y; rs[4 * k + 2] = v.z; rs[4 * k + 3] = v.w;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint4 v = *reinterpret_cast<const uint4*>(pb + 32 * (16 * (k & 3) + r16) + 8 * (k >> 2) + 2 * c);
+      rp[4 * k] = v.x; rp[4 * k + 1] = v.y; rp[4 * k + 2] = v.z; rp[4 * k + 3] = v.w;
+    }
+  };
+
+  // Software pipeline: the next tile's metadata is read at the top of a tile and its
+  // signals are loaded right after this tile's sort, so they arrive during the walk,
+  // the compaction and the stores.
+  int64_t tile = (int64_t)blockIdx.x * kTabWaves + w;
+  Meta cur = meta(tile, lane_id());
+  uint32_t s[32], pw[64];
+  if (BCE_TAB_PREFETCH && cur.reg) load_regular(cur.B, lane_id(), s, pw);
+  for (; tile < n_tiles; tile += stride) {
+    // lane-derived offsets are recomputed per tile: hoisted out of the loop, the 24 load
+    // and 40 store address offsets would stay live across the whole tile
+    int lane = lane_id();
+    asm volatile("" : "+v"(lane));
+    const int64_t m0 = tile * 64, mk = m0 + lane;
+    const bool has = mk < M;
+    const int64_t off = cur.off, B = cur.B;
+    const int n = cur.n;
+    const bool reg = cur.reg;
+    const Meta nxt = meta(tile + stride, lane);
+
+    // ---- lane = market, s[t] = sid, pw = probabilities ------------------------------------
+    if (reg) {
+      if (!BCE_TAB_PREFETCH) load_regular(B, lane, s, pw);
+      xpose<32>(s);
+      xpose<64>(pw);
+    } else if (a.n_signals > 0) {
+      // per-lane rows, straight-line: positions past n re-read the market's last signal
+      // (or signal 0 of the batch for an empty market) and are masked later
+      const int64_t base = (n > 0) ? off : 0;
+      const int last = (n > 0) ? n - 1 : 0;
+#pragma unroll
+      for (int t = 0; t < 32; ++t) {
+        const int64_t i = base + min(t, last);
+        s[t] = (uint32_t)a.sid[i];
+        const double v = a.prob[i];
+        pw[2 * t] = lo32(v);
+        pw[2 * t + 1] = hi32(v);
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < 64; ++t) pw[t] = 0u;
+#pragma unroll
+      for (int t = 0; t < 32; ++t) s[t] = 0u;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    double p[32];
+#pragma unroll
+    for (int t = 0; t < 32; ++t) p[t] = dbl(pw[2 * t], pw[2 * t + 1]);
+
+    // ---- validation (core.py:59-60) in input order ----------------------------------------
+    // per-position predicates are folded into lane bitmasks right away (t < n as a
+    // compare would be CSE'd into 32 SGPR-pair conditions held across the sort)
+    const unsigned vb = (n >= 32) ? 0xFFFFFFFFu : ((1u << n) - 1u);
+    unsigned badp = 0, bads = 0;
+#pragma unroll
+    for (int t = 0; t < 32; ++t) {
+      badp |= ((p[t] < 0.0 || p[t] > 1.0) ? 1u : 0u) << t;  // NaN passes
+      bads |= ((s[t] > smax) ? 1u : 0u) << t;
+    }
+    badp &= vb;
+    const int err = badp ? (int)__builtin_ctz(badp) : -1;
+    if (ballot((bads & vb) != 0u)) raise_fault(a.fault, kFaultSid);
+
+    // ---- sort (sid, position) with the probability as payload -----------------------------
+    unsigned key[32];
+#pragma unroll
+    for (int t = 0; t < 32; ++t) {
+      const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe(vb, t, 1);
+      key[t] = (m & ((min(s[t], smax) << 5) | (unsigned)t)) | (~m & 0x7FFFFFFFu);
+    }
+    oem_sort_kv31(key, p);
+    // the next tile's signals go in flight now (s/pw are dead: keys and p hold the tile)
+    if (BCE_TAB_PREFETCH && nxt.reg) load_regular(nxt.B, lane, s, pw);
+    __builtin_amdgcn_sched_barrier(0);
+    unsigned nq = 0;
+#pragma unroll
+    for (int t = 30; t >= 0; --t) nq = (nq << 1) | ((((key[t] ^ key[t + 1]) >> 5) != 0u) ? 1u : 0u);
+    const unsigned lb = (nq | 0x80000000u) & vb;  // last position of a run
+    const unsigned fb = ((nq << 1) | 1u) & vb;    // first position of a run
+
+    // ---- walk (core.py:107-144 in sorted-source order) ----------------------------------
+    double2 ring[kTabRing];
+    uint32_t rbits[kTabRing];
+#pragma unroll
+    for (int t = 0; t < kTabRing; ++t) {
+      const unsigned ix = min(key[t] >> 5, smax);
+      ring[t] = sT[ix];
+      rbits[t] = sB[ix >> 5];
+    }
+    double total = 0.0, ws = 0.0, cs = 0.0, psum = 0.0;
+    int cnt = 0;
+#pragma unroll
+    for (int t = 0; t < 32; ++t) {
+      const unsigned sid = key[t] >> 5;
+      const double2 rc = ring[t % kTabRing];
+      const uint32_t bw = rbits[t % kTabRing];
+      if (t + kTabRing < 32) {
+        const unsigned ix = min(key[t + kTabRing < 32 ? t + kTabRing : t] >> 5, smax);
+        ring[t % kTabRing] = sT[ix];
+        rbits[t % kTabRing] = sB[ix >> 5];
+      }
+      const double wt = rc.x, cf = rc.y, pv = p[t];
+      // branch-free: a source seen once has fst & lst, psum = 0 + p (== p; -0.0 * w adds
+      // nothing), cnt = 1, avg = psum / 1 == psum; duplicates sum in input order (builtin
+      // sum() from int 0, core.py:116) and are averaged at the run's last position
+      const bool fst = ((fb >> t) & 1u) != 0u, lst = ((lb >> t) & 1u) != 0u;
+      psum = (fst ? 0.0 : psum) + pv;
+      cnt = fst ? 1 : cnt + 1;
+      const double avg = psum / (double)cnt;  // exact (== psum) for a single signal
+      // accumulate only at the last position of a run; + 0.0 leaves every chain bit-exact
+      // (the chains start at +0.0 and can never become -0.0)
+      total += lst ? wt : 0.0;         // core.py:120
+      ws += lst ? avg * wt : 0.0;      // core.py:135-137
+      cs += lst ? cf * wt : 0.0;       // core.py:141-143
+      // emitted at the run's last position: usid (cold bit, core.py:167-170) and weight
+      key[t] = sid | ((((bw >> (sid & 31)) & 1u) != 0u) ? 0u : 0x80000000u);
+      p[t] = wt;
+      asm volatile("" : "+v"(total), "+v"(ws), "+v"(cs), "+v"(psum), "+v"(cnt));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const int u = __builtin_popcount(lb);
+
+    // ---- per-market results (lane = market, coalesced) -----------------------------------
+    if (has) {
+      const bool null_ = (total == 0.0);  // core.py:131-133
+      a.consensus[mk] = null_ ? 0.0 : ws / total;
+      a.confidence[mk] = null_ ? 0.0 : cs / total;
+      a.total_weight[mk] = total;
+      a.n_unique[mk] = u;
+      if (a.err_idx) a.err_idx[mk] = err;
+    }
+    if (!do_any) {
+      cur = nxt;
+      continue;
+    }
+
+    // ---- compaction: unique j = the j-th emitted position ---------------------------------
+    const unsigned full = (u >= 32) ? 0xFFFFFFFFu : ((1u << u) - 1u);
+    if (ballot(lb != full)) {
+      // dd[t]: bit 5 = an emitted unique sits here, bits 0..4 = positions it still has to
+      // move down (the number of duplicates before it).  Stage st moves every element
+      // whose move has bit st by 2^st; the moves are nondecreasing in t and the targets
+      // strictly increasing, so no two elements ever meet.  Selects use VGPR masks
+      // (v_bfe_i32 -> v_bfi_b32): compare-and-select would hold 32 SGPR pairs per stage.
+      uint32_t dd[32];
+      int jj = 0;
+#pragma unroll
+      for (int t = 0; t < 32; ++t) {
+        const bool e = ((lb >> t) & 1u) != 0u;
+        dd[t] = e ? (uint32_t)((t - jj) | 32) : 0u;
+        jj += e ? 1 : 0;
+      }
+      const int dmax = n - u;
+#pragma unroll
+      for (int st = 0; st < 5; ++st) {
+        if (ballot(dmax >= (1 << st))) {
+          const int sh = 1 << st;
+          uint32_t mv = 0;
+#pragma unroll
+          for (int t = 0; t < 32; ++t) mv |= ((dd[t] >> st) & (dd[t] >> 5) & 1u) << t;
+          asm("" : "+v"(mv));
+#pragma unroll
+          for (int i = 0; i < 32; ++i) {
+            const uint32_t mo = (uint32_t)__builtin_amdgcn_sbfe(mv, i, 1);  // leaves slot i
+            if (i + sh < 32) {
+              const uint32_t mi = (uint32_t)__builtin_amdgcn_sbfe(mv, i + sh, 1);  // arrives
+              key[i] = (mi & key[i + sh]) | (~mi & key[i]);
+              const uint64_t m64 = ((uint64_t)mi << 32) | mi;
+              const uint64_t x = (uint64_t)__double_as_longlong(p[i + sh]), y = (uint64_t)__double_as_longlong(p[i]);
+              p[i] = __longlong_as_double((long long)((m64 & x) | (~m64 & y)));
+              dd[i] = (mi & dd[i + sh]) | (~mi & dd[i] & ~mo);
+            } else {
+              dd[i] &= ~mo;
+            }
+          }
+        }
+      }
+    }
+
+    // ---- per-unique outputs --------------------------------------------------------------
+    __builtin_amdgcn_sched_barrier(0);
+    if (reg) {
+      // re-derive the tile base and the lane offsets here: without the opaque copies the
+      // compiler hoists all 40 store addresses to the top of the tile (SGPR/VGPR spills)
+      uint32_t blo = (uint32_t)B, bhi = (uint32_t)((uint64_t)B >> 32);
+      asm volatile("" : "+s"(blo), "+s"(bhi));
+      const int64_t B = (int64_t)(((uint64_t)bhi << 32) | blo);
+      int lane = lane_id();
+      asm volatile("" : "+v"(lane));
+      const int r16 = lane & 15, c = lane >> 4;
+      int uk[4];
+      double tk[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {  // the market of load index k at this lane: 16k + r16
+        const int src = (16 * k + r16) << 2;
+        uk[k] = __builtin_amdgcn_ds_bpermute(src, u);
+        tk[k] = dbl((uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)lo32(total)),
+                    (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)hi32(total)));
+      }
+      if (do_u) {
+        uint32_t o[32];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) o[t] = key[t];
+        xpose<32>(o);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int slot = 16 * (k >> 2) + 4 * c;
+          const int v = uk[k & 3] - slot;
+          int32_t* q = a.usid + B + 32 * (16 * (k & 3) + r16) + slot;
+          if (v >= 4) {
+            *reinterpret_cast<uint4*>(q) = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+          } else if (v > 0) {
+            q[0] = (int32_t)o[4 * k];
+            if (v > 1) q[1] = (int32_t)o[4 * k + 1];
+            if (v > 2) q[2] = (int32_t)o[4 * k + 2];
+          }
+        }
+      }
+      if (do_w || do_nw) {
+        uint32_t o[64];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) {
+          o[2 * t] = lo32(p[t]);
+          o[2 * t + 1] = hi32(p[t]);
+        }
+        xpose<64>(o);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const int slot = 8 * (k >> 2) + 2 * c;
+          const int v = uk[k & 3] - slot;
+          const int64_t pos = B + 32 * (16 * (k & 3) + r16) + slot;
+          const double w0 = dbl(o[4 * k], o[4 * k + 1]), w1 = dbl(o[4 * k + 2], o[4 * k + 3]);
+          const double tot = tk[k & 3];
+          if (v >= 2) {
+            if (do_w) *reinterpret_cast<double2*>(a.weight + pos) = make_double2(w0, w1);
+            if (do_nw)  // core.py:151
+              *reinterpret_cast<double2*>(a.nweight + pos) =
+                  make_double2(tot > 0.0 ? w0 / tot : 0.0, tot > 0.0 ? w1 / tot : 0.0);
+          } else if (v == 1) {
+            if (do_w) a.weight[pos] = w0;
+            if (do_nw) a.nweight[pos] = tot > 0.0 ? w0 / tot : 0.0;
+          }
+        }
+      }
+    } else {
+      // per-lane rows (irregular tiles): weight first, then normalizedWeight
+#pragma unroll
+      for (int j = 0; j < 32; ++j) {
+        if (j < u) {
+          if (do_u) a.usid[off + j] = (int32_t)key[j];
+          if (do_w) a.weight[off + j] = p[j];
+        }
+      }
+      if (do_nw) {
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+          const double v = total > 0.0 ? p[j] / total : 0.0;
+          if (j < u) a.nweight[off + j] = v;
+        }
+      }
+    }
+    cur = nxt;
+  }
+}
+
+}  // namespace
+
+int launch_tab32(const ConsArgs& a, hipStream_t st) {
+  const int64_t tiles = (a.n_list + 63) / 64;
+  if (tiles == 0) return BCE_OK;
+  const int S = a.n_sources > 0 ? a.n_sources : 1;
+  const size_t lds = 16 * (size_t)S + 4 * (size_t)((S + 31) / 32);
+  static bool attr_set = false;
+  if (!attr_set) {
+    const size_t cap = 16 * (size_t)kTabMaxSources + 4 * (size_t)(kTabMaxSources / 32);
+    BCE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&consensus_tab32_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)cap));
+    attr_set = true;
+  }
+  static int cached_S = -1, per_cu = 1;
+  if (cached_S != S) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, consensus_tab32_kernel, 64 * kTabWaves, lds) !=
+            hipSuccess || nb <= 0)
+      nb = 1;
+    per_cu = nb;
+    cached_S = S;
+    if (getenv("BCE_DEBUG_LAUNCH"))
+      fprintf(stderr, "[bce] consensus_tab32_kernel: %d blocks/CU x %d CUs, %zu B LDS\n", nb, cu_count(), lds);
+  }
+  const int64_t blocks = (tiles + kTabWaves - 1) / kTabWaves;
+  const int64_t cap = (int64_t)cu_count() * per_cu;
+  const int grid = (int)(blocks < cap ? blocks : cap);
+  hipLaunchKernelGGL(consensus_tab32_kernel, dim3(grid), dim3(64 * kTabWaves), lds, st, a);
+  return check_launch("consensus_tab32_kernel");
+}
+
+}  // namespace bce

@@ -70,6 +70,12 @@ int bce_abi_version(void);
 const char* bce_last_error(void);
 /* Number of visible devices (0 on a machine without a GPU; never fails). */
 int bce_device_count(void);
+/* Synchronise `stream` and report (then clear) the current device's fault word: a kernel
+ * that had to give up -- a persistent wave whose bounded wait expired, a sid >= n_sources,
+ * a market longer than the max_len it was launched with -- records a code there instead
+ * of failing silently.  BCE_OK when clean, else BCE_EHIP with the reason in
+ * bce_last_error(). */
+int bce_fault_check(void* stream);
 
 /* ---- consensus: core.compute_consensus (core.py:63-179) + validation -------------
  *
