@@ -43,46 +43,57 @@ namespace bce {
 namespace {
 
 #ifndef BCE_TAB_WAVES
-#define BCE_TAB_WAVES 8
+#define BCE_TAB_WAVES 4
 #endif
 #ifndef BCE_TAB_PREFETCH
 #define BCE_TAB_PREFETCH 0
+#endif
+#ifndef BCE_TAB_PROF
+#define BCE_TAB_PROF 0  // experiment builds only (tools/tab_variants.py): per-phase s_memtime
+#endif
+#if BCE_TAB_PROF
+__device__ unsigned long long g_tab_prof[8];
+#define TAB_MARK(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); prof[k] += t_ - prof_t; prof_t = t_; } while (0)
+#else
+#define TAB_MARK(k) do {} while (0)
 #endif
 constexpr int kTabWaves = BCE_TAB_WAVES;  // waves per workgroup; one workgroup per CU (LDS-bound)
 constexpr int kTabRing = 8;    // LDS table reads issued ahead of the walk
 
 // ---- lane-bit <-> register-bit butterflies -------------------------------------------
-// For a register pair (a: index bit 0, b: index bit 1) swap lane bit L with that index
-// bit: a' = bit_L ? b[lane ^ 2^L] : a,  b' = bit_L ? b : a[lane ^ 2^L] -- exactly what
-// v_permlane32_swap (L = 5) and v_permlane16_swap (L = 4) do, one instruction per pair.
-__device__ __forceinline__ void bfly5(uint32_t& a, uint32_t& b) {
-  const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
-  a = r[0];
-  b = r[1];
+// For a register pair (a: index bit 0, b: index bit 1) swap lane bit L (0 or 1) with that
+// index bit: a' = bit_L ? b[lane ^ 2^L] : a,  b' = bit_L ? b : a[lane ^ 2^L].  The partner
+// lane comes from a DPP quad_perm; the select mask is a wave constant.
+template <int L>
+__device__ __forceinline__ void bfly(uint32_t& a, uint32_t& b, int lane) {
+  constexpr int qp = (L == 0) ? 0xB1 : 0x4E;  // quad_perm [1,0,3,2] / [2,3,0,1]
+  const bool hi = ((lane >> L) & 1) != 0;
+  const uint32_t bx = (uint32_t)__builtin_amdgcn_mov_dpp((int)b, qp, 0xF, 0xF, true);
+  const uint32_t ax = (uint32_t)__builtin_amdgcn_mov_dpp((int)a, qp, 0xF, 0xF, true);
+  const uint32_t na = hi ? bx : a;
+  b = hi ? b : ax;
+  a = na;
 }
-__device__ __forceinline__ void bfly4(uint32_t& a, uint32_t& b) {
-  const auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
-  a = r[0];
-  b = r[1];
-}
-// Swap lane bits 5, 4 with dword-index bits 3, 2 of r[N] (an involution).
+// Swap lane bits 1, 0 with dword-index bits 3, 2 of r[N] (an involution).
 template <int N>
-__device__ __forceinline__ void xpose(uint32_t (&r)[N]) {
+__device__ __forceinline__ void xpose(uint32_t (&r)[N], int lane) {
 #pragma unroll
   for (int i = 0; i < N; ++i)
-    if (!(i & 8)) bfly5(r[i], r[i | 8]);
+    if (!(i & 8)) bfly<1>(r[i], r[i | 8], lane);
 #pragma unroll
   for (int i = 0; i < N; ++i)
-    if (!(i & 4)) bfly4(r[i], r[i | 4]);
+    if (!(i & 4)) bfly<0>(r[i], r[i | 4], lane);
 }
 
 // Regular-tile address maps (tile = 64 markets x 32 signals from B; load index k,
-// r16 = lane & 15, c = lane >> 4; each wave-instruction reads 64 contiguous bytes of 16
-// markets):
-//   sid   k < 8:  market 16(k&3) + r16, positions 16(k>>2) + 4c + d    dword index 4k + d
-//   prob  k < 16: market 16(k&3) + r16, positions 8(k>>2) + 2c + h     double index 2k + h
-// Swapping lane bits (5, 4) with load-index bits (1, 0) makes the lane the market and the
-// register index the position, for both arrays.
+// q = lane >> 2, c = lane & 3): every four consecutive lanes read one contiguous 64-byte
+// piece of one market's row, so each wave-instruction is 16 fully coalesced pieces
+//   sid   k < 8:  market 16(k&3) + q, positions 16(k>>2) + 4c + d    dword index 4k + d
+//   prob  k < 16: market 16(k&3) + q, positions 8(k>>2) + 2c + h     double index 2k + h
+// Swapping lane bits (1, 0) with load-index bits (1, 0) leaves one market per lane --
+// lane L holds market tmkt(L) = 16 (L & 3) + (L >> 2) -- and the register index = the
+// position, for both arrays.
+__device__ __forceinline__ int tmkt(int lane) { return ((lane & 3) << 4) | (lane >> 2); }
 // Odd-even merge network over 31-bit keys with a 64-bit payload, branch- and SGPR-free:
 // the swap mask is the sign of y - x (keys < 2^31), the payload moves with v_bfi_b32.
 // (Compare-and-select would give every comparator of a stage its own SGPR-pair condition;
@@ -152,7 +163,8 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
   auto meta = [&](int64_t tile, int lane) -> Meta {
     Meta m{0, 0, 0, false};
     if (tile >= n_tiles) return m;
-    const int64_t mk = tile * 64 + lane;
+    const int j = tmkt(lane);
+    const int64_t mk = tile * 64 + j;
     int64_t end = 0;
     if (mk < M) {
       m.off = a.offsets[mk];
@@ -164,24 +176,24 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
       if (m.n < 0 || m.n > 32) m.n = 0;
     }
     m.B = ((int64_t)__builtin_amdgcn_readfirstlane((int)(m.off >> 32)) << 32) |
-          (uint32_t)__builtin_amdgcn_readfirstlane((int)m.off);
-    m.reg = ballot(!(mk < M && m.n == 32 && m.off == m.B + 32 * (int64_t)lane)) == 0 &&
+          (uint32_t)__builtin_amdgcn_readfirstlane((int)m.off);  // lane 0 holds market 0
+    m.reg = ballot(!(mk < M && m.n == 32 && m.off == m.B + 32 * (int64_t)j)) == 0 &&
             ((((uintptr_t)(a.sid + m.B)) | ((uintptr_t)(a.prob + m.B))) & 15) == 0;
     return m;
   };
   // Regular-tile loads (the address maps above); raw, not yet transposed.
   auto load_regular = [&](int64_t B, int lane, uint32_t (&rs)[32], uint32_t (&rp)[64]) {
-    const int r16 = lane & 15, c = lane >> 4;
+    const int q = lane >> 2, c = lane & 3;
     const uint32_t* sb = reinterpret_cast<const uint32_t*>(a.sid + B);
     const double* pb = a.prob + B;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const uint4 v = *reinterpret_cast<const uint4*>(sb + 32 * (16 * (k & 3) + r16) + 16 * (k >> 2) + 4 * c);
+      const uint4 v = *reinterpret_cast<const uint4*>(sb + 32 * (16 * (k & 3) + q) + 16 * (k >> 2) + 4 * c);
       rs[4 * k] = v.x; rs[4 * k + 1] = v.y; rs[4 * k + 2] = v.z; rs[4 * k + 3] = v.w;
     }
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-      const uint4 v = *reinterpret_cast<const uint4*>(pb + 32 * (16 * (k & 3) + r16) + 8 * (k >> 2) + 2 * c);
+      const uint4 v = *reinterpret_cast<const uint4*>(pb + 32 * (16 * (k & 3) + q) + 8 * (k >> 2) + 2 * c);
       rp[4 * k] = v.x; rp[4 * k + 1] = v.y; rp[4 * k + 2] = v.z; rp[4 * k + 3] = v.w;
     }
   };
@@ -193,12 +205,15 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
   Meta cur = meta(tile, lane_id());
   uint32_t s[32], pw[64];
   if (BCE_TAB_PREFETCH && cur.reg) load_regular(cur.B, lane_id(), s, pw);
+#if BCE_TAB_PROF
+  unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prof_t = __builtin_amdgcn_s_memtime();
+#endif
   for (; tile < n_tiles; tile += stride) {
     // lane-derived offsets are recomputed per tile: hoisted out of the loop, the 24 load
     // and 40 store address offsets would stay live across the whole tile
     int lane = lane_id();
     asm volatile("" : "+v"(lane));
-    const int64_t m0 = tile * 64, mk = m0 + lane;
+    const int64_t m0 = tile * 64, mk = m0 + tmkt(lane);
     const bool has = mk < M;
     const int64_t off = cur.off, B = cur.B;
     const int n = cur.n;
@@ -208,8 +223,8 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
     // ---- lane = market, s[t] = sid, pw = probabilities ------------------------------------
     if (reg) {
       if (!BCE_TAB_PREFETCH) load_regular(B, lane, s, pw);
-      xpose<32>(s);
-      xpose<64>(pw);
+      xpose<32>(s, lane);
+      xpose<64>(pw, lane);
     } else if (a.n_signals > 0) {
       // per-lane rows, straight-line: positions past n re-read the market's last signal
       // (or signal 0 of the batch for an empty market) and are masked later
@@ -229,6 +244,7 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
 #pragma unroll
       for (int t = 0; t < 32; ++t) s[t] = 0u;
     }
+    TAB_MARK(0);  // metadata + loads + transposes
     __builtin_amdgcn_sched_barrier(0);
     double p[32];
 #pragma unroll
@@ -258,12 +274,49 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
     oem_sort_kv31(key, p);
     // the next tile's signals go in flight now (s/pw are dead: keys and p hold the tile)
     if (BCE_TAB_PREFETCH && nxt.reg) load_regular(nxt.B, lane, s, pw);
+    TAB_MARK(1);  // validation + keys + sort
     __builtin_amdgcn_sched_barrier(0);
     unsigned nq = 0;
 #pragma unroll
     for (int t = 30; t >= 0; --t) nq = (nq << 1) | ((((key[t] ^ key[t + 1]) >> 5) != 0u) ? 1u : 0u);
     const unsigned lb = (nq | 0x80000000u) & vb;  // last position of a run
     const unsigned fb = ((nq << 1) | 1u) & vb;    // first position of a run
+
+    // ---- duplicate runs: averaged in input order (core.py:115-116) ----------------------
+    // dupend = last positions of runs of two or more signals.  Each round handles every
+    // lane's highest remaining run: its signals are summed left to right (the other
+    // positions add +0.0, which is exact: the sum starts at +0.0 like builtin sum() from
+    // int 0 and never becomes -0.0), divided once, and the average replaces the
+    // probability at the run's last position.  Rounds = the wave's most duplicated market
+    // (nearly always one).
+    unsigned dupend = lb & ~fb;
+    while (ballot(dupend != 0u)) {
+      const int te = dupend ? 31 - __builtin_clz(dupend) : -1;
+      const unsigned upto = (te >= 0) ? (0xFFFFFFFFu >> (31 - te)) : 0u;  // bits 0..te
+      dupend &= ~(upto ^ (upto >> 1));
+      const unsigned fm = fb & upto;
+      const int ts = fm ? 31 - __builtin_clz(fm) : 0;
+      const unsigned run = upto & ~((1u << ts) - 1u);  // bits ts..te (0 when te < 0)
+      double psum = 0.0;
+#pragma unroll
+      for (int t = 0; t < 32; ++t) {
+        uint32_t m = (uint32_t)__builtin_amdgcn_sbfe(run, t, 1);
+        asm("" : "+v"(m));
+        const uint64_t m64 = ((uint64_t)m << 32) | m;
+        psum += __longlong_as_double((long long)(m64 & (uint64_t)__double_as_longlong(p[t])));
+      }
+      const double avg = psum / (double)(te - ts + 1);
+      const unsigned at = upto ^ (upto >> 1);  // bit te
+#pragma unroll
+      for (int t = 0; t < 32; ++t) {
+        uint32_t m = (uint32_t)__builtin_amdgcn_sbfe(at, t, 1);
+        asm("" : "+v"(m));
+        const uint64_t m64 = ((uint64_t)m << 32) | m;
+        p[t] = __longlong_as_double((long long)((m64 & (uint64_t)__double_as_longlong(avg)) |
+                                                (~m64 & (uint64_t)__double_as_longlong(p[t]))));
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
 
     // ---- walk (core.py:107-144 in sorted-source order) ----------------------------------
     double2 ring[kTabRing];
@@ -274,8 +327,7 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
       ring[t] = sT[ix];
       rbits[t] = sB[ix >> 5];
     }
-    double total = 0.0, ws = 0.0, cs = 0.0, psum = 0.0;
-    int cnt = 0;
+    double total = 0.0, ws = 0.0, cs = 0.0;
 #pragma unroll
     for (int t = 0; t < 32; ++t) {
       const unsigned sid = key[t] >> 5;
@@ -286,27 +338,22 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
         ring[t % kTabRing] = sT[ix];
         rbits[t % kTabRing] = sB[ix >> 5];
       }
-      const double wt = rc.x, cf = rc.y, pv = p[t];
-      // branch-free: a source seen once has fst & lst, psum = 0 + p (== p; -0.0 * w adds
-      // nothing), cnt = 1, avg = psum / 1 == psum; duplicates sum in input order (builtin
-      // sum() from int 0, core.py:116) and are averaged at the run's last position
-      const bool fst = ((fb >> t) & 1u) != 0u, lst = ((lb >> t) & 1u) != 0u;
-      psum = (fst ? 0.0 : psum) + pv;
-      cnt = fst ? 1 : cnt + 1;
-      const double avg = psum / (double)cnt;  // exact (== psum) for a single signal
-      // accumulate only at the last position of a run; + 0.0 leaves every chain bit-exact
-      // (the chains start at +0.0 and can never become -0.0)
+      // p[t] at a run's last position is the source's average (a single signal: p itself;
+      // -0.0 * w adds nothing); accumulate only there -- + 0.0 leaves every chain bit-exact
+      const double wt = rc.x, cf = rc.y, avg = p[t];
+      const bool lst = ((lb >> t) & 1u) != 0u;
       total += lst ? wt : 0.0;         // core.py:120
       ws += lst ? avg * wt : 0.0;      // core.py:135-137
       cs += lst ? cf * wt : 0.0;       // core.py:141-143
       // emitted at the run's last position: usid (cold bit, core.py:167-170) and weight
       key[t] = sid | ((((bw >> (sid & 31)) & 1u) != 0u) ? 0u : 0x80000000u);
       p[t] = wt;
-      asm volatile("" : "+v"(total), "+v"(ws), "+v"(cs), "+v"(psum), "+v"(cnt));
+      asm volatile("" : "+v"(total), "+v"(ws), "+v"(cs));
       __builtin_amdgcn_sched_barrier(0);
     }
     const int u = __builtin_popcount(lb);
 
+    TAB_MARK(2);  // walk
     // ---- per-market results (lane = market, coalesced) -----------------------------------
     if (has) {
       const bool null_ = (total == 0.0);  // core.py:131-133
@@ -321,49 +368,32 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
       continue;
     }
 
+    TAB_MARK(3);  // per-market stores
     // ---- compaction: unique j = the j-th emitted position ---------------------------------
     const unsigned full = (u >= 32) ? 0xFFFFFFFFu : ((1u << u) - 1u);
     if (ballot(lb != full)) {
-      // dd[t]: bit 5 = an emitted unique sits here, bits 0..4 = positions it still has to
-      // move down (the number of duplicates before it).  Stage st moves every element
-      // whose move has bit st by 2^st; the moves are nondecreasing in t and the targets
-      // strictly increasing, so no two elements ever meet.  Selects use VGPR masks
-      // (v_bfe_i32 -> v_bfi_b32): compare-and-select would hold 32 SGPR pairs per stage.
-      uint32_t dd[32];
-      int jj = 0;
+      // holes = valid positions that are not the last of their run (duplicates).  Remove
+      // the highest hole of every lane per round: slots above it move down by one, the
+      // lower holes stay where they are.  Rounds = the wave's largest duplicate count
+      // (nearly always 1).  Selects use VGPR masks (v_bfi_b32): compare-and-select would
+      // hold 32 SGPR-pair conditions.
+      unsigned holes = vb & ~lb;
+      while (ballot(holes != 0u)) {
+        const int h = holes ? 31 - __builtin_clz(holes) : 32;
+        holes &= ~(1u << (h & 31));
 #pragma unroll
-      for (int t = 0; t < 32; ++t) {
-        const bool e = ((lb >> t) & 1u) != 0u;
-        dd[t] = e ? (uint32_t)((t - jj) | 32) : 0u;
-        jj += e ? 1 : 0;
-      }
-      const int dmax = n - u;
-#pragma unroll
-      for (int st = 0; st < 5; ++st) {
-        if (ballot(dmax >= (1 << st))) {
-          const int sh = 1 << st;
-          uint32_t mv = 0;
-#pragma unroll
-          for (int t = 0; t < 32; ++t) mv |= ((dd[t] >> st) & (dd[t] >> 5) & 1u) << t;
-          asm("" : "+v"(mv));
-#pragma unroll
-          for (int i = 0; i < 32; ++i) {
-            const uint32_t mo = (uint32_t)__builtin_amdgcn_sbfe(mv, i, 1);  // leaves slot i
-            if (i + sh < 32) {
-              const uint32_t mi = (uint32_t)__builtin_amdgcn_sbfe(mv, i + sh, 1);  // arrives
-              key[i] = (mi & key[i + sh]) | (~mi & key[i]);
-              const uint64_t m64 = ((uint64_t)mi << 32) | mi;
-              const uint64_t x = (uint64_t)__double_as_longlong(p[i + sh]), y = (uint64_t)__double_as_longlong(p[i]);
-              p[i] = __longlong_as_double((long long)((m64 & x) | (~m64 & y)));
-              dd[i] = (mi & dd[i + sh]) | (~mi & dd[i] & ~mo);
-            } else {
-              dd[i] &= ~mo;
-            }
-          }
+        for (int i = 0; i < 31; ++i) {
+          uint32_t m = (uint32_t)((h - 1 - i) >> 31);  // all ones <=> i >= h
+          asm("" : "+v"(m));
+          key[i] = (m & key[i + 1]) | (~m & key[i]);
+          const uint64_t m64 = ((uint64_t)m << 32) | m;
+          const uint64_t x = (uint64_t)__double_as_longlong(p[i + 1]), y = (uint64_t)__double_as_longlong(p[i]);
+          p[i] = __longlong_as_double((long long)((m64 & x) | (~m64 & y)));
         }
       }
     }
 
+    TAB_MARK(4);  // compaction
     // ---- per-unique outputs --------------------------------------------------------------
     __builtin_amdgcn_sched_barrier(0);
     if (reg) {
@@ -374,12 +404,12 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
       const int64_t B = (int64_t)(((uint64_t)bhi << 32) | blo);
       int lane = lane_id();
       asm volatile("" : "+v"(lane));
-      const int r16 = lane & 15, c = lane >> 4;
+      const int q = lane >> 2, c = lane & 3;
       int uk[4];
       double tk[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {  // the market of load index k at this lane: 16k + r16
-        const int src = (16 * k + r16) << 2;
+      for (int k = 0; k < 4; ++k) {  // market 16k + q of load index k sits in lane 4q + k
+        const int src = ((lane & ~3) | k) << 2;
         uk[k] = __builtin_amdgcn_ds_bpermute(src, u);
         tk[k] = dbl((uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)lo32(total)),
                     (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)hi32(total)));
@@ -388,19 +418,13 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
         uint32_t o[32];
 #pragma unroll
         for (int t = 0; t < 32; ++t) o[t] = key[t];
-        xpose<32>(o);
+        xpose<32>(o, lane);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const int slot = 16 * (k >> 2) + 4 * c;
-          const int v = uk[k & 3] - slot;
-          int32_t* q = a.usid + B + 32 * (16 * (k & 3) + r16) + slot;
-          if (v >= 4) {
-            *reinterpret_cast<uint4*>(q) = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
-          } else if (v > 0) {
-            q[0] = (int32_t)o[4 * k];
-            if (v > 1) q[1] = (int32_t)o[4 * k + 1];
-            if (v > 2) q[2] = (int32_t)o[4 * k + 2];
-          }
+          int32_t* dst = a.usid + B + 32 * (16 * (k & 3) + q) + slot;
+          if (uk[k & 3] > slot)
+            *reinterpret_cast<uint4*>(dst) = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
         }
       }
       if (do_w || do_nw) {
@@ -410,22 +434,18 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
           o[2 * t] = lo32(p[t]);
           o[2 * t + 1] = hi32(p[t]);
         }
-        xpose<64>(o);
+        xpose<64>(o, lane);
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
           const int slot = 8 * (k >> 2) + 2 * c;
-          const int v = uk[k & 3] - slot;
-          const int64_t pos = B + 32 * (16 * (k & 3) + r16) + slot;
+          const int64_t pos = B + 32 * (16 * (k & 3) + q) + slot;
           const double w0 = dbl(o[4 * k], o[4 * k + 1]), w1 = dbl(o[4 * k + 2], o[4 * k + 3]);
           const double tot = tk[k & 3];
-          if (v >= 2) {
+          if (uk[k & 3] > slot) {
             if (do_w) *reinterpret_cast<double2*>(a.weight + pos) = make_double2(w0, w1);
             if (do_nw)  // core.py:151
               *reinterpret_cast<double2*>(a.nweight + pos) =
                   make_double2(tot > 0.0 ? w0 / tot : 0.0, tot > 0.0 ? w1 / tot : 0.0);
-          } else if (v == 1) {
-            if (do_w) a.weight[pos] = w0;
-            if (do_nw) a.nweight[pos] = tot > 0.0 ? w0 / tot : 0.0;
           }
         }
       }
@@ -446,11 +466,25 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
         }
       }
     }
+    TAB_MARK(5);  // per-unique stores
     cur = nxt;
   }
+#if BCE_TAB_PROF
+  if (lane_id() == 0)
+    for (int k = 0; k < 6; ++k) atomicAdd(&g_tab_prof[k], prof[k]);
+#endif
 }
 
 }  // namespace
+
+#if BCE_TAB_PROF
+extern "C" int bce_tab_prof_read(unsigned long long* host8) {
+  BCE_HIP(hipMemcpyFromSymbol(host8, HIP_SYMBOL(g_tab_prof), 8 * sizeof(unsigned long long)));
+  unsigned long long z[8] = {0};
+  BCE_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_tab_prof), z, sizeof z));
+  return BCE_OK;
+}
+#endif
 
 int launch_tab32(const ConsArgs& a, hipStream_t st) {
   const int64_t tiles = (a.n_list + 63) / 64;

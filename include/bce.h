@@ -26,8 +26,11 @@
  *    the sourceId is a key of source_reliability (core.py:167-170).  bce_table_pack
  *    builds it from separate rel/conf/present arrays.
  *  - Per-unique-source outputs are written at the market's CSR offsets: slot
- *    offsets[m]+j for j < n_unique[m] (slots beyond are left untouched).  usid carries
- *    the cold-start bit in bit 31 (value = rank | cold << 31).
+ *    offsets[m]+j for j < n_unique[m].  Slots n_unique[m] <= j < n (the market's length)
+ *    are scratch: a kernel may leave them untouched or write unspecified values there
+ *    (the short-market kernel stores whole 16-byte chunks).  Nothing outside the
+ *    market's own [offsets[m], offsets[m+1]) range is ever written.  usid carries the
+ *    cold-start bit in bit 31 (value = rank | cold << 31).
  *  - Floating point follows CPython: no fused multiply-add anywhere on the parity path,
  *    sums in the reference's order in BCE_MODE_EXACT (bit-exact vs the reference).
  */

@@ -1,0 +1,126 @@
+#!/usr/bin/env python3
+"""Experiment harness (not product code): build variants of libbce_hip.so with compile-time
+switches of the LDS-table kernel (consensus_tab.hip) and time them on the config-2 workload.
+
+  python tools/tab_variants.py build [names...]     # here (hipcc cross-compiles)
+  python tools/tab_variants.py run [--rounds 3]      # on the GPU box: one process per variant
+                                                     # and round, interleaved; JSON lines out
+
+A variant named *prof* is built with -DBCE_TAB_PROF=1 and also reports the per-phase cycle
+split of the kernel's waves (s_memtime deltas summed over waves, per tile).
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "bayesian-consensus-engine_amd", "csrc")
+OUT = os.path.join(ROOT, "tools", "ablate_build")
+SRCS = ["capi.hip", "consensus.hip", "consensus_tab.hip", "elementwise.hip", "tiebreak.hip", "stats.hip",
+        "aggregate.hip"]
+
+VARIANTS = {
+    "w8": ["-DBCE_TAB_WAVES=8"],
+    "w4": ["-DBCE_TAB_WAVES=4"],
+    "w4_pf": ["-DBCE_TAB_WAVES=4", "-DBCE_TAB_PREFETCH=1"],
+    "w8_prof": ["-DBCE_TAB_WAVES=8", "-DBCE_TAB_PROF=1"],
+    "w4_prof": ["-DBCE_TAB_WAVES=4", "-DBCE_TAB_PROF=1"],
+}
+PHASES = ["load+xpose", "valid+sort", "walk", "per_market", "compaction", "per_unique_stores"]
+
+
+def build(names):
+    procs = []
+    for name in names:
+        d = os.path.join(OUT, name)
+        os.makedirs(d, exist_ok=True)
+        objs = []
+        for src in SRCS:
+            o = os.path.join(d, src.replace(".hip", ".o"))
+            objs.append(o)
+            cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
+                   "-fno-fast-math", "-munsafe-fp-atomics", "-w", *VARIANTS[name], "-c", os.path.join(CSRC, src),
+                   "-o", o]
+            procs.append((name, subprocess.Popen(cmd)))
+        for _, p in procs:
+            if p.wait() != 0:
+                raise SystemExit(f"build of {name} failed")
+        procs = []
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o",
+                        os.path.join(d, "libbce_hip.so"), *objs], check=True)
+        print("built", name, flush=True)
+
+
+def one(name, reps):
+    sys.path.insert(0, os.path.join(ROOT, "bayesian-consensus-engine_amd"))
+    sys.path.insert(0, ROOT)
+    import numpy as np
+    import torch
+
+    from bayesian_engine import _native as N, batch
+    from bench import make_c2
+
+    M, L, S = 1_000_000, 32, 10_000
+    off, sid, prob, rel, conf, present = make_c2(M, L, S, 2)
+    T = lambda a: torch.from_numpy(a).cuda()  # noqa: E731
+    table = batch.SourceTable.from_arrays(T(rel), T(conf), T(present))
+    d = [T(off), T(sid), T(prob)]
+    res = batch._alloc(M, M * L, d[0].device, True, True)
+    for _ in range(300):  # clock ramp
+        batch.consensus(*d, table, max_len=L, out=res)
+    torch.cuda.synchronize()
+    lib = N.lib()
+    prof = hasattr(lib, "bce_tab_prof_read")
+    buf = (C.c_ulonglong * 8)()
+    if prof:
+        lib.bce_tab_prof_read(buf)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for e0, e1 in ev:
+        e0.record()
+        batch.consensus(*d, table, max_len=L, out=res)
+        e1.record()
+    torch.cuda.synchronize()
+    ms = sorted(a.elapsed_time(b) for a, b in ev)
+    out = {"variant": name, "median_ms": ms[len(ms) // 2], "min_ms": ms[0]}
+    if prof:
+        lib.bce_tab_prof_read(buf)
+        v = list(buf)[:6]
+        tiles = (M + 63) // 64
+        tot = sum(v)
+        out["phases_cyc_per_tile"] = {k: round(x / reps / tiles) for k, x in zip(PHASES, v)}
+        out["phases_pct"] = {k: round(100 * x / max(tot, 1), 1) for k, x in zip(PHASES, v)}
+    N.check_faults()
+    print(json.dumps(out), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("cmd", choices=["build", "run", "one"])
+    ap.add_argument("names", nargs="*")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--reps", type=int, default=100)
+    args = ap.parse_args()
+    names = args.names or list(VARIANTS)
+    if args.cmd == "build":
+        build(names)
+    elif args.cmd == "one":
+        one(names[0], args.reps)
+    else:
+        names = [n for n in names if os.path.exists(os.path.join(OUT, n, "libbce_hip.so"))]
+        for r in range(args.rounds):
+            for n in names:
+                env = dict(os.environ, BCE_LIB=os.path.join(OUT, n, "libbce_hip.so"))
+                t0 = time.time()
+                rc = subprocess.run([sys.executable, __file__, "one", n, "--reps", str(args.reps)], env=env,
+                                    timeout=300).returncode
+                if rc != 0:
+                    raise SystemExit(f"variant {n} failed rc={rc}")
+                print(f"# round {r} {n} {time.time() - t0:.1f}s", flush=True)
+
+
+if __name__ == "__main__":
+    main()
