@@ -10,28 +10,36 @@
 // stays in VGPRs -- no LDS staging ring, no producer/consumer waves:
 //
 //  load       a wave owns a tile of 64 consecutive markets.  A REGULAR tile (every market
-//             has 32 signals, 16-B aligned) is read with fully coalesced 16-B loads whose
-//             lane->address map puts the position bits on lane bits 5..3 and the market
-//             bits on lane bits 2..0 + the register index; three butterflies that swap
-//             lane bits 5, 4, 3 with register-index bits (v_permlane32_swap,
-//             v_permlane16_swap, DPP row_ror:8) leave lane = market, register = position.
+//             has 32 signals, 16-B aligned) is read with coalesced 16-B loads: four
+//             consecutive lanes cover one contiguous 64-B piece of a market's row (chunk
+//             bits on lane bits 1..0, market bits on lane bits 5..2 and the load index).
+//             Two butterflies (DPP quad_perm + a wave-constant select) swap lane bits 1, 0
+//             with load-index bits, leaving lane = market, register index = position.
 //             Other tiles (ragged lengths, the last tile, misaligned shards) load per lane.
+//             The next tile's offsets are read at the top of each tile.
 //  sort       keys (sid << 5 | position) with the probability as payload, Batcher
-//             odd-even merge network in VGPRs: duplicates of a source stay in input order.
+//             odd-even merge network in VGPRs (branch-free, VGPR swap masks):
+//             duplicates of a source stay in input order.
+//  averages   duplicate runs (rare) are summed in input order and divided once per run
+//             (core.py:115-116), in rounds over the wave's lanes.
 //  walk       sorted positions left to right: {rel, conf} from LDS (ds_read_b128, eight
-//             ahead), duplicate runs summed in input order and averaged (core.py:115-116),
-//             the reference's three left-to-right chains over unique sources
+//             ahead), the reference's three left-to-right chains over unique sources
 //             (core.py:120,135-143) -- each lane is one market, so the exact order is free.
-//  compact    the per-unique (usid, weight) pairs are emitted at their run's last sorted
-//             position, then shifted down by the number of duplicates before them (a
-//             five-stage shift network, skipped when no lane of the wave has duplicates).
-//  store      per-market scalars lane = market (coalesced); per-unique outputs go back
-//             through the same butterflies and leave as coalesced 16-B stores, slots past
-//             n_unique untouched (narrower stores for the one partial chunk per market).
-//             normalizedWeight = weight / total is divided in the store layout, the
-//             market's total fetched with ds_bpermute.
+//  compact    per-unique (usid, weight) pairs are emitted at their run's last sorted
+//             position; the duplicates' holes are removed highest first (rounds over the
+//             wave, usually one).
+//  store      per-market scalars from the market's lane; per-unique outputs go back
+//             through the same butterflies and leave as coalesced 16-B chunk stores
+//             (chunks holding no unique are skipped; slots past n_unique inside a written
+//             chunk are scratch, include/bce.h).  normalizedWeight = weight / total is
+//             divided in the store layout, the market's total fetched with ds_bpermute.
 // Validation (core.py:59-60: first p < 0 or p > 1, NaN passes) reads the probabilities in
 // input order before the sort.  Exact mode only: every sum is the reference's own order.
+//
+// Measured (tools/tab_variants.py, profiles/r02_tab_*): 4 waves per CU (one per SIMD,
+// ~260 registers) beat 8 (2 per SIMD, 256-register budget: spills); the per-unique stores
+// are the largest phase -- the CU's share of the chip's write bandwidth -- and moving
+// them between the next tile's phases or to fully contiguous addresses did not help.
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -44,9 +52,6 @@ namespace {
 
 #ifndef BCE_TAB_WAVES
 #define BCE_TAB_WAVES 4
-#endif
-#ifndef BCE_TAB_PREFETCH
-#define BCE_TAB_PREFETCH 0
 #endif
 #ifndef BCE_TAB_PROF
 #define BCE_TAB_PROF 0  // experiment builds only (tools/tab_variants.py): per-phase s_memtime
@@ -204,7 +209,6 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
   int64_t tile = (int64_t)blockIdx.x * kTabWaves + w;
   Meta cur = meta(tile, lane_id());
   uint32_t s[32], pw[64];
-  if (BCE_TAB_PREFETCH && cur.reg) load_regular(cur.B, lane_id(), s, pw);
 #if BCE_TAB_PROF
   unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prof_t = __builtin_amdgcn_s_memtime();
 #endif
@@ -222,7 +226,7 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
 
     // ---- lane = market, s[t] = sid, pw = probabilities ------------------------------------
     if (reg) {
-      if (!BCE_TAB_PREFETCH) load_regular(B, lane, s, pw);
+      load_regular(B, lane, s, pw);
       xpose<32>(s, lane);
       xpose<64>(pw, lane);
     } else if (a.n_signals > 0) {
@@ -272,8 +276,6 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
       key[t] = (m & ((min(s[t], smax) << 5) | (unsigned)t)) | (~m & 0x7FFFFFFFu);
     }
     oem_sort_kv31(key, p);
-    // the next tile's signals go in flight now (s/pw are dead: keys and p hold the tile)
-    if (BCE_TAB_PREFETCH && nxt.reg) load_regular(nxt.B, lane, s, pw);
     TAB_MARK(1);  // validation + keys + sort
     __builtin_amdgcn_sched_barrier(0);
     unsigned nq = 0;
@@ -414,6 +416,7 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
         tk[k] = dbl((uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)lo32(total)),
                     (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)hi32(total)));
       }
+      // whole 16-byte chunks holding at least one unique (the rest of the chunk is scratch)
       if (do_u) {
         uint32_t o[32];
 #pragma unroll
@@ -422,9 +425,9 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const int slot = 16 * (k >> 2) + 4 * c;
-          int32_t* dst = a.usid + B + 32 * (16 * (k & 3) + q) + slot;
           if (uk[k & 3] > slot)
-            *reinterpret_cast<uint4*>(dst) = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+            *reinterpret_cast<uint4*>(a.usid + B + 32 * (16 * (k & 3) + q) + slot) =
+                make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
         }
       }
       if (do_w || do_nw) {

@@ -24,11 +24,10 @@ SRCS = ["capi.hip", "consensus.hip", "consensus_tab.hip", "elementwise.hip", "ti
         "aggregate.hip"]
 
 VARIANTS = {
-    "w8": ["-DBCE_TAB_WAVES=8"],
     "w4": ["-DBCE_TAB_WAVES=4"],
-    "w4_pf": ["-DBCE_TAB_WAVES=4", "-DBCE_TAB_PREFETCH=1"],
-    "w8_prof": ["-DBCE_TAB_WAVES=8", "-DBCE_TAB_PROF=1"],
+    "w8": ["-DBCE_TAB_WAVES=8"],
     "w4_prof": ["-DBCE_TAB_WAVES=4", "-DBCE_TAB_PROF=1"],
+    "w8_prof": ["-DBCE_TAB_WAVES=8", "-DBCE_TAB_PROF=1"],
 }
 PHASES = ["load+xpose", "valid+sort", "walk", "per_market", "compaction", "per_unique_stores"]
 
@@ -93,7 +92,8 @@ def one(name, reps):
         tot = sum(v)
         out["phases_cyc_per_tile"] = {k: round(x / reps / tiles) for k, x in zip(PHASES, v)}
         out["phases_pct"] = {k: round(100 * x / max(tot, 1), 1) for k, x in zip(PHASES, v)}
-    N.check_faults()
+    if os.environ.get("TAB_NOCHECK") is None:
+        N.check_faults()
     print(json.dumps(out), flush=True)
 
 
