@@ -1,15 +1,20 @@
 """Secondary bench lines for BASELINE.json configs 3-5 (``python bench.py --config c3|c4|c5``).
 
-Same contract as the headline: inputs resident in HBM before timing, W untimed warmup
-steps, K timed steps bracketed by barrier + synchronize, max over ranks, one JSON line.
+Same contract as the headline (bench.timed_loop): inputs resident in HBM before timing, a
+clock ramp, W untimed warmup steps, K timed steps bracketed by barrier + synchronize, max
+over ranks, one JSON line; cpu_baseline = the oracle's C restatement on the host cores this
+process may use (kind "port"), over a bounded sample of the same workload, rank 0 at N=1.
 
   c3  100M signals ragged CSR (lengths log-uniform on [1, 4096], Zipf(1.1) sources over
       1e6 ranks), markets sharded over N ranks at equal signal counts (strong scaling:
       the 100M total is fixed).  Step = one planned consensus pass (all length bins).
   c4  10M-source reliability table, T replay steps (decayed view + outcome update per
-      step, participation 0.1, correct 0.6).  Sources are owner-sharded; with N > 1 the
-      per-step outcome flags produced by the market shards are combined with one RCCL
-      reduce-scatter (2-bit packed, disjoint contributions).  Step = one replay step.
+      step, participation 0.1, correct 0.6).  Sources are owned by sharding.owner_of (a
+      multiplicative hash); the table is interned in owner-grouped order so each owner's
+      sources are one contiguous block.  With N > 1 every rank's market shard produces
+      2-bit outcome flags over ALL sources (each (source, step) outcome from exactly one
+      shard: disjoint) and one RCCL reduce-scatter delivers each owner its block.
+      Step = one replay step (+ the reduce-scatter).
   c5  dense A x M re-estimation (default 16384 x 1e6 fp64 = 131 GB), markets sharded by
       column over N ranks; per iteration pass 1 (consensus), pass 2 (agreement), an
       all-reduce of the per-agent counts, the weight update.  Step = one iteration.
@@ -25,6 +30,7 @@ steps, K timed steps bracketed by barrier + synchronize, max over ranks, one JSO
 from __future__ import annotations
 
 import ctypes as C
+import os
 import time
 
 import numpy as np
@@ -32,26 +38,26 @@ import torch
 import torch.distributed as dist
 
 HBM_PEAK_GBS = 8000.0
+ROOT = os.path.dirname(os.path.abspath(__file__))
 
 
-def _timed(step, args, world, stream, barrier, max_over):
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    barrier(world)
-    torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        step()
-        ev[i][1].record(stream)
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    barrier(world)
-    torch.cuda.synchronize()
-    per = float(np.mean([a.elapsed_time(b) for a, b in ev])) / 1e3
-    return max_over(wall, world), per
+def _timed(step, args, world, stream, barrier=None, max_over=None):
+    from bench import timed_loop
+
+    wall, per, _ = timed_loop(step, args, world, stream)
+    return wall, per
+
+
+def _threads():
+    from bench import host_threads
+
+    return host_threads()
+
+
+def _pmc(name, **match):
+    from bench import read_pmc
+
+    return read_pmc(name, **match)[0]
 
 
 def run_extra(args, world, rank):
@@ -59,6 +65,102 @@ def run_extra(args, world, rank):
 
     fn = {"c3": _c3, "c4": _c4, "c5": _c5, "ns": _ns, "agg": _agg}[args.config]
     return fn(args, world, rank, barrier, max_over_ranks, sum_over_ranks)
+
+
+# ---------------------------------------------------------------------------------------
+# CPU baselines: the oracle's C restatement (test infrastructure, oracle/) on host threads
+# ---------------------------------------------------------------------------------------
+def _cpu_c3(off, sid, prob, table_host, args):
+    if args.no_cpu_baseline:
+        return None
+    from bench import cpu_consensus_threaded
+
+    rel, conf, present = table_host
+    T = _threads()
+    t0, reps = time.perf_counter(), 0
+    while True:
+        cpu_consensus_threaded(off, sid, prob, rel, conf, present, T)
+        reps += 1
+        dt = time.perf_counter() - t0
+        if dt >= args.cpu_seconds:
+            break
+    n = int(off[-1])
+    return {"value": n * reps / dt, "unit": "signals/s", "cores": T, "kind": "port", "label": "restatement",
+            "sample": f"this rank's whole shard ({len(off) - 1} markets, {n} signals), oracle/bce_oracle.c on "
+                      f"{T} threads, {reps} passes in {dt:.2f} s"}
+
+
+def _cpu_c4(args, S_sample=2_000_000):
+    """decay view + outcome update (reliability.py:104-183) per source-step, on a 2M-source
+    sample of the config-4 distributions (same per-source work), over host threads."""
+    if args.no_cpu_baseline:
+        return None
+    import sys
+    from concurrent.futures import ThreadPoolExecutor
+
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as orc
+
+    rng = np.random.default_rng(4)
+    now0, day = 1_772_323_200_000_000, 86_400_000_000
+    rel, conf = rng.random(S_sample), rng.random(S_sample)
+    t_us = now0 - (rng.random(S_sample) * 90 * day).astype(np.int64)
+    present = np.ones(S_sample, np.uint8)
+    flags = [((rng.random(S_sample) < 0.1).astype(np.uint8) | ((rng.random(S_sample) < 0.6).astype(np.uint8) << 1))
+             for _ in range(4)]
+    T = _threads()
+    cuts = np.linspace(0, S_sample, T + 1).astype(np.int64)
+    state = [[rel[a:b].copy(), conf[a:b].copy(), t_us[a:b].copy(), present[a:b].copy()]
+             for a, b in zip(cuts[:-1], cuts[1:])]
+
+    def part(i, k):
+        a, b = int(cuts[i]), int(cuts[i + 1])
+        r, c, t, pr = state[i]
+        orc.decay_view(r, t, pr, now0 + k * day)
+        state[i] = list(orc.outcome_update(r, c, t, pr, flags[k % 4][a:b], now0 + k * day))
+
+    t0, k = time.perf_counter(), 0
+    with ThreadPoolExecutor(T) as ex:
+        while True:
+            list(ex.map(lambda i: part(i, k), range(T)))
+            k += 1
+            dt = time.perf_counter() - t0
+            if dt >= args.cpu_seconds:
+                break
+    return {"value": S_sample * k / dt, "unit": "source-steps/s", "cores": T, "kind": "port",
+            "label": "restatement",
+            "sample": f"{S_sample} sources x {k} replay steps (config-4 distributions), orc_decay_view + "
+                      f"orc_outcome_update on {T} threads in {dt:.2f} s"}
+
+
+def _cpu_c5(P, args, m_sample=1024):
+    """One re-estimation iteration (consensus over all agents + agreement counts) on the
+    first m_sample market columns of this rank's P, over host threads."""
+    if args.no_cpu_baseline:
+        return None
+    import sys
+    from concurrent.futures import ThreadPoolExecutor
+
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as orc
+
+    A = P.shape[0]
+    m = min(m_sample, P.shape[1])
+    Ph = P[:, :m].cpu().numpy()
+    T = _threads()
+    cuts = np.linspace(0, m, T + 1).astype(np.int64)
+    chunks = [np.ascontiguousarray(Ph[:, a:b]) for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
+    t0, reps = time.perf_counter(), 0
+    with ThreadPoolExecutor(T) as ex:
+        while True:
+            list(ex.map(lambda c: orc.reestimate(c, 1), chunks))
+            reps += 1
+            dt = time.perf_counter() - t0
+            if dt >= args.cpu_seconds:
+                break
+    return {"value": A * m * reps / dt, "unit": "cells/s", "cores": T, "kind": "port", "label": "restatement",
+            "sample": f"{A} agents x {m} markets (the first columns of this rank's P), one iteration per pass, "
+                      f"orc_reestimate on {T} threads, {reps} passes in {dt:.2f} s"}
 
 
 # ---------------------------------------------------------------------------------------
@@ -95,8 +197,9 @@ def _c3(args, world, rank, barrier, max_over, sum_over):
     rt = np.random.default_rng(34)
     rel, conf = rt.uniform(0.1, 1.0, S), rt.random(S)
     present = (rt.random(S) < 0.9).astype(np.uint8)
-    table = batch.SourceTable.from_arrays(T(np.where(present == 1, rel, 0.5)), T(np.where(present == 1, conf, 0.25)),
-                                          T(present))
+    rel_h, conf_h = np.where(present == 1, rel, 0.5), np.where(present == 1, conf, 0.25)
+    table = batch.SourceTable.from_arrays(T(rel_h), T(conf_h), T(present))
+    table_host = (rel_h, conf_h, present)
     d_off, d_sid, d_prob = T(off), T(sid), T(prob)
     plan = batch.Plan.build(off, dev)
     res = batch._alloc(len(off) - 1, n, dev, True, True)
@@ -105,6 +208,9 @@ def _c3(args, world, rank, barrier, max_over, sum_over):
         batch.consensus(d_off, d_sid, d_prob, table, plan=plan, mode=args.mode, out=res)
 
     wall, per = _timed(step, args, world, torch.cuda.current_stream(dev), barrier, max_over)
+    from bayesian_engine import _native as N
+
+    N.check_faults(dev, "c3 timed steps")
     Mloc = len(off) - 1
     sum_u = int(res.n_unique.sum().item())
     touched = int(np.unique(sid).size)
@@ -120,45 +226,57 @@ def _c3(args, world, rank, barrier, max_over, sum_over):
                    "markets_this_rank": Mloc, "signals_this_rank": n, "unique_per_market_mean": sum_u / max(Mloc, 1),
                    "bins": plan.bin_start.tolist(), "parallelism": f"markets sharded over {world} rank(s), no collective"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "consensus (all bins, one step)",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc("pmc_c3.json", signals_this_rank=n),
+                     "kernel": "consensus (all bins, one step)",
                      "bytes_per_launch": bytes_step, "avg_launch_ms": per * 1e3},
-        "cpu_baseline": None,
+        "cpu_baseline": _cpu_c3(off, sid, prob, table_host, args) if rank == 0 and world == 1 else None,
     }
 
 
 # ---------------------------------------------------------------------------------------
 def _c4(args, world, rank, barrier, max_over, sum_over):
     from bayesian_engine import batch
+    from bayesian_engine.sharding import owner_of
 
     S_total = 10_000_000
-    S = S_total // world + (1 if rank < S_total % world else 0)   # this rank's owned sources
-    S -= S % 2
     dev = torch.device("cuda", torch.cuda.current_device())
+    gid = np.arange(S_total, dtype=np.int64)
+    owner = owner_of(gid, world)                           # sharding.owner_of: hash ownership
+    counts = np.bincount(owner, minlength=world)
+    blk = int((counts.max() + 3) // 4 * 4)                 # padded owner block (4 sources/byte)
+    local = np.empty(S_total, np.int64)                    # index inside the owner's block
+    for r in range(world):
+        sel = np.nonzero(owner == r)[0]
+        local[sel] = np.arange(len(sel))
+    pos = torch.from_numpy(owner.astype(np.int64) * blk + local).to(dev)
+    # the market shard that resolves each source's outcome (another hash): flags cross ranks
+    contrib = torch.from_numpy(((gid * 0x2545F491) >> 7) % max(world, 1)).to(dev)
+    S = int(counts[rank])                                   # sources this rank owns
     g = torch.Generator(device=dev)
     g.manual_seed(4 + rank)
     now0 = 1_772_323_200_000_000  # 2026-03-01T00:00:00Z in microseconds
     day = 86_400_000_000
-    rel = torch.rand(S, generator=g, device=dev, dtype=torch.float64)
-    conf = torch.rand(S, generator=g, device=dev, dtype=torch.float64)
-    t_us = now0 - (torch.rand(S, generator=g, device=dev, dtype=torch.float64) * 90 * day).to(torch.int64)
-    present = torch.ones(S, dtype=torch.uint8, device=dev)
-    view = torch.empty(S, dtype=torch.float64, device=dev)
+    pad = blk
+    rel = torch.rand(pad, generator=g, device=dev, dtype=torch.float64)
+    conf = torch.rand(pad, generator=g, device=dev, dtype=torch.float64)
+    t_us = now0 - (torch.rand(pad, generator=g, device=dev, dtype=torch.float64) * 90 * day).to(torch.int64)
+    present = torch.ones(pad, dtype=torch.uint8, device=dev)
+    view = torch.empty(pad, dtype=torch.float64, device=dev)
     POOL = 16
-    nbytes = (S + 3) // 4
+    nbytes = blk // 4
 
-    def flags_for(k_seed, who):
+    def flags_for(k_seed):
         gg = torch.Generator(device=dev)
         gg.manual_seed(k_seed)
-        part = torch.rand(S_total if world > 1 else S, generator=gg, device=dev) < 0.1
-        corr = torch.rand(part.numel(), generator=gg, device=dev) < 0.6
-        if world > 1:  # contribution of this rank's market shard: disjoint by source
-            part &= (torch.arange(part.numel(), device=dev) % world) == who
-        f = part.to(torch.uint8) | (corr.to(torch.uint8) << 1)
-        pad = (-f.numel()) % 4
-        f = torch.cat([f, torch.zeros(pad, dtype=torch.uint8, device=dev)]).view(-1, 4)
+        part = torch.rand(S_total, generator=gg, device=dev) < 0.1
+        corr = torch.rand(S_total, generator=gg, device=dev) < 0.6
+        part &= contrib == rank  # this rank's market shard resolved these (disjoint across ranks)
+        f = torch.zeros(world * blk, dtype=torch.uint8, device=dev)
+        f[pos] = part.to(torch.uint8) | (corr.to(torch.uint8) << 1)
+        f = f.view(-1, 4)
         return (f[:, 0] | (f[:, 1] << 2) | (f[:, 2] << 4) | (f[:, 3] << 6)).contiguous()
 
-    pool = [flags_for(1000 + k, rank) for k in range(POOL)]
+    pool = [flags_for(1000 + k) for k in range(POOL)]
     recv = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     state = {"k": 0}
 
@@ -166,17 +284,19 @@ def _c4(args, world, rank, barrier, max_over, sum_over):
         k = state["k"]
         fl = pool[k % POOL]
         if world > 1:
-            # owner shard = contiguous block of the packed vector (sources permuted so each
-            # rank owns one block); disjoint 2-bit contributions -> SUM == OR
-            chunks = fl[: nbytes * world].view(world, nbytes)
-            dist.reduce_scatter_tensor(recv, chunks.contiguous().view(-1), op=dist.ReduceOp.SUM)
+            # every owner receives the sum of all shards' 2-bit flags for its block;
+            # contributions are disjoint per (source, step), so SUM == OR
+            dist.reduce_scatter_tensor(recv, fl, op=dist.ReduceOp.SUM)
             f2 = recv
         else:
             f2 = fl
-        batch.replay_step(rel, conf, t_us, present, f2, now0 + k * day, view)
+        batch.replay_step(rel[:S], conf[:S], t_us[:S], present[:S], f2, now0 + k * day, view[:S])
         state["k"] = k + 1
 
     wall, per = _timed(step, args, world, torch.cuda.current_stream(dev), barrier, max_over)
+    from bayesian_engine import _native as N
+
+    N.check_faults(dev, "c4 timed steps")
     p = 0.1
     bps = 24 + 0.25 + 8 + p * (8 + 24 + 1)
     achieved = bps * S / per / 1e9
@@ -188,11 +308,12 @@ def _c4(args, world, rank, barrier, max_over, sum_over):
         "scaling": "strong", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (SURVEY.md d4: participation 0.1, correct 0.6, 16-step flag pool)",
         "config": {"workload": f"c4: {S_total} sources, replay_step per step", "sources_this_rank": S,
-                   "parallelism": f"sources owner-sharded over {world} rank(s); flags reduce-scatter per step"},
+                   "parallelism": f"sources owned by sharding.owner_of over {world} rank(s); per-step outcome "
+                                  f"flags from every market shard reduce-scattered to the owners"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "replay_step_kernel",
-                     "bytes_per_launch": bps * S, "avg_launch_ms": per * 1e3},
-        "cpu_baseline": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc("pmc_c4.json", sources_this_rank=S),
+                     "kernel": "replay_step_kernel", "bytes_per_launch": bps * S, "avg_launch_ms": per * 1e3},
+        "cpu_baseline": _cpu_c4(args) if rank == 0 and world == 1 else None,
     }
 
 
@@ -255,11 +376,11 @@ def _c5(args, world, rank, barrier, max_over, sum_over):
                    "markets_this_rank": Mloc,
                    "parallelism": f"markets sharded by column over {world} rank(s); per-agent counts all-reduced"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc("pmc_c5.json", markets_this_rank=Mloc),
                      "kernel": "reestimate_consensus + reestimate_agreement (one iteration)",
                      "bytes_per_launch": bytes_iter, "avg_launch_ms": kern * 1e3,
                      "mfma": "not used: GEMV at ~0.25 flop/B; exact agent-order sums on the VALU"},
-        "cpu_baseline": None,
+        "cpu_baseline": _cpu_c5(P, args) if rank == 0 and world == 1 else None,
     }
 
 

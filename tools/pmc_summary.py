@@ -3,7 +3,9 @@
 
   python tools/pmc_summary.py stats <dir> <kernel-substring>
       average duration (ms) from the *kernel_stats.csv of a --kernel-trace --stats run
-  python tools/pmc_summary.py pmc <fetch-dir> <write-dir> <kernel-substring> <out.json> [--meta k=v ...]
+  python tools/pmc_summary.py pmc <fetch-dir> <write-dir> <kernel-substring> <out.json> [k=v ...]
+      (steps_total=N: sum every matching dispatch and divide by N -- per step of a
+      multi-kernel config -- instead of averaging per dispatch)
       HBM bytes per launch from two separate --pmc passes (FETCH_SIZE, WRITE_SIZE), corrected
       as MI355X_MICROARCH.md §HBM prescribes: FETCH_SIZE (KB) reports 1/2 of the bytes of a
       wide coalesced read on gfx950 -> x2; WRITE_SIZE (KB) is exact for 16-B streaming stores.
@@ -33,11 +35,13 @@ def stats(d, kern):
     raise SystemExit(f"kernel {kern} not in stats")
 
 
-def counter(d, kern, name):
+def counter(d, kern, name, per_step=None):
     vals = [float(r["Counter_Value"]) for r in _rows(d, "*counter_collection.csv")
             if kern in r.get("Kernel_Name", "") and r.get("Counter_Name") == name]
     if not vals:
         raise SystemExit(f"no {name} for {kern} under {d}")
+    if per_step:  # several kernels per step (planned launches): total / number of steps
+        return sum(vals) / per_step, len(vals)
     vals = vals[1:] if len(vals) > 2 else vals  # drop the cold first launch
     return sum(vals) / len(vals), len(vals)
 
@@ -54,8 +58,9 @@ def main():
             continue
         k, v = kv.split("=", 1)
         meta[k] = int(v) if v.isdigit() else v
-    f_kb, nf = counter(fdir, kern, "FETCH_SIZE")
-    w_kb, nw = counter(wdir, kern, "WRITE_SIZE")
+    per_step = meta.pop("steps_total", None)
+    f_kb, nf = counter(fdir, kern, "FETCH_SIZE", per_step)
+    w_kb, nw = counter(wdir, kern, "WRITE_SIZE", per_step)
     rd = 2.0 * f_kb * 1024.0
     wr = w_kb * 1024.0
     j = dict(meta, kernel=kern, fetch_size_kb=f_kb, write_size_kb=w_kb, launches=[nf, nw],
