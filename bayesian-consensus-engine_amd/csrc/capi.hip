@@ -51,6 +51,9 @@ int* fault_word() {
   return words[dev];
 }
 
+static int g_spin_cap = 1 << 22;
+int spin_cap() { return g_spin_cap; }
+
 static const char* fault_text(int code) {
   switch (code) {
     case kFaultSpinLoader: return "consensus_pipe_kernel: loader wave timed out waiting for a free slot";
@@ -78,6 +81,11 @@ extern "C" int bce_fault_check(void* stream) {
   BCE_HIP(hipStreamSynchronize(st));
   bce::set_error("device fault %d: %s", h, bce::fault_text(h));
   return BCE_EHIP;
+}
+
+extern "C" int bce_debug_set_spin_cap(int cap) {
+  bce::g_spin_cap = (cap > 0) ? cap : (1 << 22);
+  return BCE_OK;
 }
 
 extern "C" int bce_abi_version(void) { return BCE_ABI_VERSION; }

@@ -1,27 +1,22 @@
-// consensus.hip -- batched core.compute_consensus (core.py:63-179) over CSR markets.
+// consensus.hip -- batched core.compute_consensus (core.py:63-179) over CSR markets: every
+// kernel except the LDS-table one (consensus_tab.hip), the launchers and the C ABI.
 //
-// Two kernels, chosen per market length bin:
-//
-//  consensus_seg<G, TM>   markets with n <= G (G in {8,16,32,64}).  One wave owns a tile of
-//                         TM markets.  Cooperative phase (lane = signal): each round loads
-//                         64/G markets (G lanes per market, coalesced), sorts (sid, input
-//                         index) keys with a register bitonic network (DPP / ds_swizzle),
-//                         dedups with ballots, sums duplicate probabilities in input order,
-//                         gathers reliability/confidence from the (L2-resident) source table
-//                         and stages per-unique (w, p*w, c*w) rows in LDS.  Serial phase
-//                         (lane = market): the LDS rows are read transposed and summed in
-//                         sorted-source order -- the reference's exact left-to-right order
-//                         (core.py:107-144) -- with all lanes busy on different markets.
-//                         Final phase (lane = unique slot): normalizedWeight and the
-//                         per-unique outputs, written coalesced at the CSR offsets.
-//
-//  consensus_long<IN_LDS> markets with n > 64.  One 256-thread workgroup per market:
-//                         64-bit (sid, index) keys bitonic-sorted in LDS (n <= 4096) or in
-//                         a global scratch slice (n > 4096), leaders of equal-sid runs sum
-//                         their run in input order, per-position (w, p*w, c*w) arrays, then
-//                         either the exact serial sum (one lane per chain) or a fixed-order
-//                         tree (BCE_MODE_FAST).
-//
+// Kernels by market length (launch_seg_for_len / launch_wide_for_len pick them):
+//  consensus_pipe_kernel<G>    contiguous markets, n <= G in {8,16,32}, S <= 16384: one
+//                              loader wave streams tiles into an LDS ring (LDS-DMA), four
+//                              compute waves (lane = market) sort keys in VGPRs and walk
+//                              them with 16-B {rel, conf} gathers from global memory.
+//  consensus_flat_kernel<G>    contiguous markets, n <= 32, larger tables or compact
+//                              outputs: the same arithmetic, each wave loads its own tile.
+//  consensus_lpm_kernel<G>     market lists (planned ragged batches), n <= 32: lane per
+//                              market, rows staged per market by LDS-DMA.
+//  consensus_seg_kernel<64,8>  33 <= n <= 64: cooperative lane-per-signal phase (bitonic
+//                              sort, ballots) then lane-per-market ordered sums from LDS.
+//  consensus_wide_kernel<NW,R> 64 < n <= 4096: one workgroup per market, register bitonic
+//                              network over packed (sid, index) keys, exact chains.
+//  consensus_long_kernel<LDS>  fallback for long markets (LDS or global-scratch sort),
+//                              BCE_MODE_FAST fixed-order trees.
+// Every kernel sums in the reference's order in BCE_MODE_EXACT (bit-exact outputs).
 // FP contraction is off for the whole file: every mul/add rounds like CPython.
 #include <stdio.h>
 #include <stdlib.h>
@@ -31,41 +26,11 @@
 
 #pragma clang fp contract(off)
 
-#ifndef BCE_ABLATE
-#define BCE_ABLATE 0
-#endif
-#ifndef BCE_SEG32_TM
-#define BCE_SEG32_TM 8
-#endif
-#ifndef BCE_LPM_LOAD
-#define BCE_LPM_LOAD 0  // 0: per-market LDS-DMA rows; 2: direct per-lane loads + payload sort
-#endif
-#ifndef BCE_LPM_SYNC
-#define BCE_LPM_SYNC 1
-#endif
-#ifndef BCE_USE_LPM
-#define BCE_USE_LPM 1  // lane-per-market kernel for n <= 32 (else the cooperative one)
-#endif
-#ifndef BCE_SEG_GRID_PER_CU
-#define BCE_SEG_GRID_PER_CU 0  // 0 = exactly the resident occupancy (persistent grid)
-#endif
 #ifndef BCE_SEG_WPE
 #define BCE_SEG_WPE 1  // __launch_bounds__ min waves per SIMD for the segment kernel
 #endif
-#ifndef BCE_FLAT
-#define BCE_FLAT 3  // contiguous tiles, list == NULL, n <= 32: 3 = pipe, 2 = stream, 1 = flat, 0 = lpm
-#endif
 #ifndef BCE_FLAT_TM
 #define BCE_FLAT_TM 64
-#endif
-#ifndef BCE_PIPE_DBG
-#define BCE_PIPE_DBG 0
-#endif
-#ifndef BCE_STREAM_WPB
-#define BCE_STREAM_WPB 5
-#endif
-#ifndef BCE_STREAM_CH
-#define BCE_STREAM_CH 4
 #endif
 #ifndef BCE_FLAT_RING
 #define BCE_FLAT_RING 8  // relconf gathers in flight per lane
@@ -76,14 +41,8 @@
 #ifndef BCE_FLAT_WPB
 #define BCE_FLAT_WPB 2
 #endif
-#ifndef BCE_WIDE
-#define BCE_WIDE 1  // register-sort kernel for 64 < n <= 4096 (exact mode)
-#endif
 #ifndef BCE_WIDE_HR
 #define BCE_WIDE_HR 4  // wide kernel: rounds of NT uniques computed into registers at once
-#endif
-#ifndef BCE_STAGE
-#define BCE_STAGE 1  // LDS-staged 16-B input loads for contiguous tiles
 #endif
 
 namespace bce {
@@ -152,6 +111,10 @@ void consensus_seg_kernel(ConsArgs a) {
         m = a.list ? a.list[li] : (int32_t)li;
         off = a.offsets[m];
         n = (int32_t)(a.offsets[m + 1] - off);
+        if (n < 0 || n > G) {  // longer than the launch's max_len: report, skip
+          if (a.fault) atomicCAS(a.fault, 0, kFaultTooLong);
+          n = 0;
+        }
       }
       sM[lane] = m;
       sOff[lane] = off;
@@ -163,7 +126,7 @@ void consensus_seg_kernel(ConsArgs a) {
     int32_t sidv[R];
     double pv[R];
     bool valid[R];
-    if (BCE_STAGE && a.list == nullptr) {
+    if (a.list == nullptr) {
       // contiguous tile: [base, end) streamed with 16-B loads into LDS, then each lane
       // picks its (market, slot) element.
       const int64_t base = sOff[0];
@@ -238,7 +201,7 @@ void consensus_seg_kernel(ConsArgs a) {
     for (int r = 0; r < R; ++r) {
       rc[r] = make_double2(0.5, 0.25);
       pw[r] = 0xffffffffu;
-      if (!(BCE_ABLATE & 2) && valid[r]) {
+      if (valid[r]) {
         rc[r] = a.relconf[sidv[r]];
         if (!bits_in_lds) pw[r] = a.pbits[sidv[r] >> 5];
       }
@@ -249,7 +212,7 @@ void consensus_seg_kernel(ConsArgs a) {
     for (int r = 0; r < R; ++r) {
       const int mk = r * SPR + seg;
       unsigned key = valid[r] ? (((unsigned)sidv[r] << LOGG) | (unsigned)t) : kSent32;
-      if constexpr (!(BCE_ABLATE & 1)) key = bitonic_sort_seg<G>(key, t);
+      key = bitonic_sort_seg<G>(key, t);
       const bool kv = key != kSent32;
       const int ssid = (int)(key >> LOGG);
       const int src = seg_base + (int)(key & (G - 1));  // lane holding this signal
@@ -268,7 +231,7 @@ void consensus_seg_kernel(ConsArgs a) {
       const int myrun = first ? run : 1;
       double s = 0.0 + ps;  // builtin sum() starts from int 0 (core.py:116)
       double avg = s;
-      if (!(BCE_ABLATE & 16) && ballot(myrun > 1)) {  // duplicates: sum the run in input order
+      if (ballot(myrun > 1)) {  // duplicates: sum the run in input order
         for (int k = 1; k < G; ++k) {
           const int sl = (lane + k < 64) ? lane + k : 63;
           const double pk = pull_f64(ps, sl);
@@ -305,7 +268,7 @@ void consensus_seg_kernel(ConsArgs a) {
       const int u = sNU[lane];
       double total = 0.0, ws = 0.0, cs = 0.0;
       const int base = lane * RS;
-      if constexpr (!(BCE_ABLATE & 4)) {
+      {
 #pragma unroll
         for (int jj = 0; jj < G; ++jj) {
           if (jj < u) {
@@ -314,10 +277,6 @@ void consensus_seg_kernel(ConsArgs a) {
             cs += sB[base + jj];
           }
         }
-      } else {
-        total = sW[base] + (double)u;
-        ws = sA[base];
-        cs = sB[base];
       }
       sTot[lane] = total;
       const int32_t m = sM[lane];
@@ -333,7 +292,7 @@ void consensus_seg_kernel(ConsArgs a) {
     __syncthreads();
 
     // ---- per-unique outputs (coalesced at CSR offsets) --------------------------------
-    if ((a.usid || a.weight || a.nweight) && !(BCE_ABLATE & 8)) {
+    if ((a.usid || a.weight || a.nweight)) {
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const int mk = r * SPR + seg;
@@ -357,11 +316,7 @@ void consensus_seg_kernel(ConsArgs a) {
 // LDS ordering inside a single-wave workgroup: the wave's LDS instructions execute in
 // order, so a compiler barrier + lgkmcnt drain is all a cross-lane hand-off needs.
 __device__ __forceinline__ void wave_sync() {
-#if BCE_LPM_SYNC
   __syncthreads();
-#else
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#endif
 }
 
 __device__ __forceinline__ void dma4(const void* g, void* lds) {
@@ -396,72 +351,42 @@ __global__ __launch_bounds__(64) void consensus_lpm_kernel(ConsArgs a) {
       off = a.offsets[mk];
       n = (int)(a.offsets[mk + 1] - off);
     }
+    if (ballot(n < 0 || n > G)) {  // longer than the launch's max_len: report, skip
+      raise_fault(a.fault, kFaultTooLong);
+      if (n < 0 || n > G) n = 0;
+    }
 
     unsigned key[G];
     double sp[G];
     int err = -1;
-    if constexpr (BCE_LPM_LOAD == 2) {
-      // ---- direct per-lane loads: the lane's row of sids / probabilities -------------
-      const bool aligned = ballot((off & 3) != 0) == 0;
-      if (aligned) {
-#pragma unroll
-        for (int c = 0; c < G / 4; ++c) {
-          int4 v = make_int4(0, 0, 0, 0);
-          if (4 * c < n) v = *reinterpret_cast<const int4*>(a.sid + off + 4 * c);
-          key[4 * c] = (unsigned)v.x; key[4 * c + 1] = (unsigned)v.y;
-          key[4 * c + 2] = (unsigned)v.z; key[4 * c + 3] = (unsigned)v.w;
-        }
-#pragma unroll
-        for (int c = 0; c < G / 2; ++c) {
-          double2 v = make_double2(0.0, 0.0);
-          if (2 * c < n) v = *reinterpret_cast<const double2*>(a.prob + off + 2 * c);
-          sp[2 * c] = v.x; sp[2 * c + 1] = v.y;
-        }
-      } else {
-#pragma unroll
-        for (int t = 0; t < G; ++t) {
-          key[t] = (t < n) ? (unsigned)a.sid[off + t] : 0u;
-          sp[t] = (t < n) ? a.prob[off + t] : 0.0;
-        }
-      }
-#pragma unroll
-      for (int t = 0; t < G; ++t) {
-        const bool v = t < n;
-        key[t] = v ? ((key[t] << LOGG) | (unsigned)t) : kSent32;
-        if (v && err < 0 && (sp[t] < 0.0 || sp[t] > 1.0)) err = t;  // core.py:59-60
-      }
-      if constexpr (!(BCE_ABLATE & 1)) oem_sort_kv<G>(key, sp);
-    } else {
-      // ---- rows -> LDS by LDS-DMA: one dword per lane, market by market --------------
-      for (int q = 0; q < kWave; ++q) {
-        const int nq = __builtin_amdgcn_readlane(n, q);
-        if (nq == 0) continue;
-        const int64_t oq = ((int64_t)__builtin_amdgcn_readlane((int)(off >> 32), q) << 32) |
-                           (uint32_t)__builtin_amdgcn_readlane((int)off, q);
-        if (lane < nq) dma4(a.sid + oq + lane, sS + q * SST);
-        if (lane < 2 * nq) dma4(reinterpret_cast<const uint32_t*>(a.prob + oq) + lane, sP + q * PST);
-        if (2 * nq > kWave && lane < 2 * nq - kWave)
-          dma4(reinterpret_cast<const uint32_t*>(a.prob + oq) + kWave + lane, sP + q * PST + kWave);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      wave_sync();
-      const uint32_t* rowS = sS + lane * SST;
-      const double* rowP = reinterpret_cast<const double*>(sP + lane * PST);
-      // keys (sid, slot) and the validation scan in input order
-#pragma unroll
-      for (int t = 0; t < G; ++t) {
-        const bool v = t < n;
-        key[t] = v ? ((rowS[t] << LOGG) | (unsigned)t) : kSent32;
-        const double p = rowP[t];
-        if (v && err < 0 && (p < 0.0 || p > 1.0)) err = t;  // core.py:59-60 (NaN passes)
-      }
-      if constexpr (!(BCE_ABLATE & 1)) oem_sort<G>(key);
-      // probabilities in sorted order (registers); the rows become output staging
-#pragma unroll
-      for (int t = 0; t < G; ++t) sp[t] = rowP[key[t] & (G - 1)];
-      wave_sync();
+    // ---- rows -> LDS by LDS-DMA: one dword per lane, market by market --------------
+    for (int q = 0; q < kWave; ++q) {
+      const int nq = __builtin_amdgcn_readlane(n, q);
+      if (nq == 0) continue;
+      const int64_t oq = ((int64_t)__builtin_amdgcn_readlane((int)(off >> 32), q) << 32) |
+                         (uint32_t)__builtin_amdgcn_readlane((int)off, q);
+      if (lane < nq) dma4(a.sid + oq + lane, sS + q * SST);
+      if (lane < 2 * nq) dma4(reinterpret_cast<const uint32_t*>(a.prob + oq) + lane, sP + q * PST);
+      if (2 * nq > kWave && lane < 2 * nq - kWave)
+        dma4(reinterpret_cast<const uint32_t*>(a.prob + oq) + kWave + lane, sP + q * PST + kWave);
     }
-
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wave_sync();
+    const uint32_t* rowS = sS + lane * SST;
+    const double* rowP = reinterpret_cast<const double*>(sP + lane * PST);
+    // keys (sid, slot) and the validation scan in input order
+#pragma unroll
+    for (int t = 0; t < G; ++t) {
+      const bool v = t < n;
+      key[t] = v ? ((rowS[t] << LOGG) | (unsigned)t) : kSent32;
+      const double p = rowP[t];
+      if (v && err < 0 && (p < 0.0 || p > 1.0)) err = t;  // core.py:59-60 (NaN passes)
+    }
+    oem_sort<G>(key);
+    // probabilities in sorted order (registers); the rows become output staging
+#pragma unroll
+    for (int t = 0; t < G; ++t) sp[t] = rowP[key[t] & (G - 1)];
+    wave_sync();
     // ---- walk in sorted order: runs summed in input order (core.py:116), then the
     //      reference's left-to-right totals over unique sources (core.py:107-144) -----
     uint32_t* outS = sS + lane * SST;                         // usid of unique j
@@ -473,7 +398,7 @@ __global__ __launch_bounds__(64) void consensus_lpm_kernel(ConsArgs a) {
       const bool kv = key[t] != kSent32;
       const int sid = (int)(key[t] >> LOGG);
       const bool fst = kv && (t == 0 || sid != (int)(key[t - 1 > 0 ? t - 1 : 0] >> LOGG));
-      if (!(BCE_ABLATE & 2) && fst) {
+      if (fst) {
         rc[t] = a.relconf[sid];
         pw[t] = a.pbits[sid >> 5];
       } else {
@@ -521,7 +446,7 @@ __global__ __launch_bounds__(64) void consensus_lpm_kernel(ConsArgs a) {
         const bool kv2 = key[tt] != kSent32;
         const int sid2 = (int)(key[tt] >> LOGG);
         const bool fst2 = kv2 && sid2 != (int)(key[tt - 1] >> LOGG);
-        if (!(BCE_ABLATE & 2) && fst2) {
+        if (fst2) {
           rc[tt % RING] = a.relconf[sid2];
           pw[tt % RING] = a.pbits[sid2 >> 5];
         }
@@ -544,7 +469,7 @@ __global__ __launch_bounds__(64) void consensus_lpm_kernel(ConsArgs a) {
     wave_sync();
 
     // ---- per-unique outputs: MPI markets per iteration, lane = slot (coalesced) ------
-    if ((a.usid || a.weight || a.nweight) && !(BCE_ABLATE & 8)) {
+    if ((a.usid || a.weight || a.nweight)) {
       const int slot = lane & (G - 1);
 #pragma unroll 4
       for (int it = 0; it < G; ++it) {
@@ -636,6 +561,10 @@ void consensus_flat_kernel(ConsArgs a) {
       off = a.offsets[mk];
       n = (int)(a.offsets[mk + 1] - off);
     }
+    if (ballot(n < 0 || n > G)) {  // longer than the launch's max_len: report, skip
+      raise_fault(a.fault, kFaultTooLong);
+      if (n < 0 || n > G) n = 0;
+    }
 
     // ---- 1. stream [B, E) into the LDS image (16-B LDS-DMA, full chunks in bounds) -------
     {
@@ -681,7 +610,7 @@ void consensus_flat_kernel(ConsArgs a) {
     }
 #pragma unroll
     for (int t = 0; t < G; ++t) key[t] = (t < n) ? ((key[t] << LOGG) | (unsigned)t) : kSent32;
-    if constexpr (!(BCE_ABLATE & 1)) oem_sort<G>(key);
+    oem_sort<G>(key);
     // run structure as bit masks in one VGPR each (bit t: position t is the first / last
     // position of its sid run); valid positions are exactly t < n after the sort
     unsigned fb = 0, lb = 0;
@@ -712,7 +641,7 @@ void consensus_flat_kernel(ConsArgs a) {
 #pragma unroll
     for (int t = 0; t < NG; ++t) {
       const unsigned ix = min(key[t] >> LOGG, smax);
-      ring[t] = (!(BCE_ABLATE & 2) && have_tab) ? a.relconf[ix] : make_double2(0.5, 0.25);
+      ring[t] = (have_tab) ? a.relconf[ix] : make_double2(0.5, 0.25);
     }
     const int dumS = SW - 1, dumP = PW - 1;  // write sinks for invalid positions
     double total = 0.0, ws = 0.0, cs = 0.0, psum = 0.0;
@@ -728,7 +657,7 @@ void consensus_flat_kernel(ConsArgs a) {
       const double2 rc = ring[t % NG];
       if (t + NG < G) {
         const unsigned ix = min(key[t + NG < G ? t + NG : t] >> LOGG, smax);
-        if (!(BCE_ABLATE & 2) && have_tab) ring[t % NG] = a.relconf[ix];
+        if (have_tab) ring[t % NG] = a.relconf[ix];
       }
       if (kv && (p < 0.0 || p > 1.0)) err = (slot < err) ? slot : err;  // core.py:59-60
       psum = (fst ? 0.0 : psum) + p;   // builtin sum() from int 0 (core.py:116)
@@ -770,7 +699,7 @@ void consensus_flat_kernel(ConsArgs a) {
     wave_sync_lds();
 
     // ---- 4b. per-unique outputs ---------------------------------------------------------
-    if ((a.usid || a.weight || a.nweight) && !(BCE_ABLATE & 8)) {
+    if ((a.usid || a.weight || a.nweight)) {
       const int dB = (int)(B - Bs), dP = (int)(B - Bp);
       const bool vec_ok = (((uintptr_t)a.usid & 7) | ((uintptr_t)a.weight & 15) | ((uintptr_t)a.nweight & 15)) == 0;
       if (vec_ok && ballot(has && (off & 1) != 0) == 0 && (B & 1) == 0) {
@@ -832,313 +761,6 @@ void consensus_flat_kernel(ConsArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
-// consensus_stream_kernel<G, TM, WPB>: the flat kernel with the next tile in flight
-// ------------------------------------------------------------------------------------
-// Same arithmetic as consensus_flat_kernel; the schedule hides the memory latency that
-// bounds the flat kernel at ~5 waves per CU:
-//   * every wave batch-loads the [B, E) bounds of its next 64 tiles once (one vector
-//     load pair), so no per-tile scalar load sits on the critical path;
-//   * the per-market offsets travel with the tile (3 dword LDS-DMA instructions);
-//   * keys and the sorted-slot probabilities are read out of the input image into
-//     registers right after the sort, so the image is dead before the walk's last
-//     relconf gather is issued -- the NEXT tile's LDS-DMA is issued right there.  (VMEM
-//     counters retire in order: a DMA issued before a gather would make that gather's
-//     wait cover the DMA; issued after the last gather it overlaps the rest of the walk
-//     and the copy-out instead.)
-//   * weights stay in registers by sorted position; the per-unique outputs leave through
-//     a small staging area in chunks of CH positions (lane = market writes, lane =
-//     (market, position) stores at offsets[m] + j).
-// Waits the compiler's wait-count pass can see (an asm s_waitcnt is opaque to it, so it
-// would keep treating the previous tile's stores as pending and fall back to vmcnt(0)
-// for every later load).  gfx9 encoding: vmcnt[3:0] expcnt[6:4] lgkmcnt[11:8] vmcnt[15:14].
-__device__ __forceinline__ void wait_vm0() {
-  __builtin_amdgcn_s_waitcnt(0x0F70);
-  asm volatile("" ::: "memory");
-}
-__device__ __forceinline__ void wait_lgkm0() {
-  __builtin_amdgcn_s_waitcnt(0xC07F);
-  asm volatile("" ::: "memory");
-}
-
-template <int G, int TM, int WPB, int CH>
-__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(BCE_FLAT_WPE, 8)))
-void consensus_stream_kernel(ConsArgs a) {
-  static_assert(G == 8 || G == 16 || G == 32, "stream widths");
-  static_assert(TM == 64, "one market per lane");
-  static_assert(G % CH == 0 && (CH == 2 || CH == 4 || CH == 8), "chunk");
-  constexpr int LOGG = (G == 8) ? 3 : (G == 16) ? 4 : 5;
-  constexpr int TS = TM * G;             // max signals per tile
-  constexpr int SW = TS + 8 + G;         // sid image (dwords): alignment slack + row overrun
-  constexpr int PW = TS + 4 + G;         // prob image (doubles)
-  constexpr int OW = 2 * (TM + 1) + 2;   // offsets block (dwords)
-  constexpr int NG = (G < BCE_FLAT_RING) ? G : BCE_FLAT_RING;  // relconf gathers in flight
-  constexpr int SR = CH + 1;             // staging row stride (16-B entries): conflict-free
-  constexpr int QPR = kWave / CH;        // markets per copy-out round
-  constexpr int NSI = (TS + 8 + 4 * kWave - 1) / (4 * kWave);  // max sid DMA instructions per tile
-  constexpr int NPI = (TS + 4 + 2 * kWave - 1) / (2 * kWave);  // max prob DMA instructions
-
-  __shared__ uint32_t sBits[kBitsLds];
-  __shared__ __attribute__((aligned(16))) uint32_t sSid[WPB][SW];
-  __shared__ __attribute__((aligned(16))) double sProb[WPB][PW];
-  __shared__ __attribute__((aligned(16))) uint32_t sOffs[WPB][OW];
-  __shared__ __attribute__((aligned(16))) uint4 sStage[WPB][TM * SR];
-  __shared__ double sTot[WPB][TM];
-  __shared__ int64_t sMkOff[WPB][TM];
-
-  const int lane = lane_id();
-  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int nwords = (a.n_sources + 31) >> 5;  // <= kBitsLds (checked by the launcher)
-  for (int i = threadIdx.x; i < nwords; i += 64 * WPB) sBits[i] = a.pbits[i];
-  __syncthreads();  // the only workgroup barrier: waves are independent from here on
-
-  uint32_t* const iS = sSid[w];
-  double* const iP = sProb[w];
-  uint32_t* const iO = sOffs[w];
-  uint4* const stg = sStage[w];
-  const int64_t M = a.n_list;
-  const int64_t n_tiles = (M + TM - 1) / TM;
-  const int64_t t0 = (int64_t)blockIdx.x * WPB + w;
-  const int64_t tstride = (int64_t)gridDim.x * WPB;
-  if (t0 >= n_tiles) return;
-  const unsigned smax = (unsigned)(a.n_sources > 0 ? a.n_sources - 1 : 0);
-  // relconf gathers are unconditional (a branch around a load forces a vmcnt(0) at its
-  // join); with no sources the table is a single cold-start row
-  const double2* const tab = (a.n_sources > 0) ? a.relconf : kColdRow;
-  const int64_t Nf4 = a.n_signals & ~3ll, Nf2 = a.n_signals & ~1ll;
-
-  // bounds of this wave's tiles t0 + i*tstride, i in [base, base + 64): lane i holds them
-  int64_t tbB = 0, tbE = 0;
-  auto load_bounds = [&](int64_t base) {
-    const int64_t tl = t0 + (base + lane) * tstride;
-    if (tl < n_tiles) {
-      const int64_t m0 = tl * TM;
-      tbB = a.offsets[m0];
-      tbE = a.offsets[(m0 + TM < M) ? m0 + TM : M];
-    }
-  };
-  auto bound = [&](int64_t v, int i) -> int64_t {
-    return ((int64_t)__builtin_amdgcn_readlane((int)(v >> 32), i) << 32) |
-           (uint32_t)__builtin_amdgcn_readlane((int)v, i);
-  };
-  // issue the LDS-DMA of one tile into this wave's image (sid, prob, offsets block)
-  auto issue_dma = [&](int64_t tile, int64_t B, int64_t E) {
-    int lane = lane_id();
-    asm volatile("" : "+v"(lane));
-    const int64_t Bs = B & ~3ll, Bp = B & ~1ll;
-    const int64_t es = (E < Nf4) ? ((E + 3) & ~3ll) : Nf4;
-    const int nci = (int)((es - Bs) >> 2);
-#pragma unroll
-    for (int i = 0; i < NSI; ++i) {
-      const int c = i * kWave + lane;
-      if (c < nci)
-        dma_b128(a.sid + Bs + 4 * c, iS + i * 256);
-    }
-    const int64_t ep = (E < Nf2) ? ((E + 1) & ~1ll) : Nf2;
-    const int ncp = (int)((ep - Bp) >> 1);
-#pragma unroll
-    for (int i = 0; i < NPI; ++i) {
-      const int c = i * kWave + lane;
-      if (c < ncp)
-        dma_b128(a.prob + Bp + 2 * c, iP + i * 128);
-    }
-    const int64_t m0 = tile * TM;
-    const int64_t m1 = (m0 + TM < M) ? m0 + TM : M;
-    const int ndw = (int)(2 * (m1 - m0 + 1));  // dwords of offsets[m0 .. m1]
-    const uint32_t* og = reinterpret_cast<const uint32_t*>(a.offsets + m0);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const int d = i * kWave + lane;
-      if (d < ndw)
-        dma_b32(og + d, iO + i * 64);
-    }
-  };
-
-  load_bounds(0);
-  int64_t B = bound(tbB, 0), E = bound(tbE, 0);
-  issue_dma(t0, B, E);
-
-  int64_t it = 0;
-  for (int64_t tile = t0; tile < n_tiles; tile += tstride, ++it) {
-    // lane-derived addresses are recomputed per tile (opaque lane id): hoisted out of the
-    // loop they overflow the register budget and spill to scratch, and a scratch reload
-    // after the next tile's DMA would wait for that DMA
-    int lane = lane_id();
-    asm volatile("" : "+v"(lane));
-    const int64_t m0 = tile * TM;
-    const int64_t Bs = B & ~3ll, Bp = B & ~1ll;
-    const int64_t es = (E < Nf4) ? ((E + 3) & ~3ll) : Nf4;
-    const int64_t ep = (E < Nf2) ? ((E + 1) & ~1ll) : Nf2;
-    wait_vm0();
-    if (E > es && lane < (int)(E - es)) iS[es - Bs + lane] = (uint32_t)a.sid[es + lane];
-    if (E > ep && lane < (int)(E - ep)) iP[ep - Bp + lane] = a.prob[ep + lane];
-    wave_sync_lds();
-
-    // ---- this lane's market (offsets block from the image) ------------------------------
-    const int64_t mk = m0 + lane;
-    const bool has = mk < M;
-    int64_t off = B;
-    int n = 0;
-    if (has) {
-      off = ((int64_t)iO[2 * lane + 1] << 32) | iO[2 * lane];
-      n = (int)((((int64_t)iO[2 * lane + 3] << 32) | iO[2 * lane + 2]) - off);
-    }
-    const int rs = (int)(off - B);
-    const int rsi = rs + (int)(B - Bs);
-    const int rsp = rs + (int)(B - Bp);
-
-    // ---- keys + sort ------------------------------------------------------------------------
-    unsigned key[G];
-    if (ballot(has && (rsi & 3) != 0) == 0) {
-#pragma unroll
-      for (int c = 0; c < G / 4; ++c) {
-        const uint4 v = *reinterpret_cast<const uint4*>(iS + rsi + 4 * c);
-        key[4 * c] = v.x; key[4 * c + 1] = v.y; key[4 * c + 2] = v.z; key[4 * c + 3] = v.w;
-      }
-    } else {
-#pragma unroll
-      for (int t = 0; t < G; ++t) key[t] = iS[rsi + t];
-    }
-#pragma unroll
-    for (int t = 0; t < G; ++t) key[t] = (t < n) ? ((key[t] << LOGG) | (unsigned)t) : kSent32;
-    if constexpr (!(BCE_ABLATE & 1)) oem_sort<G>(key);
-    // built high position first with shift-or: (f ? 1 << t : 0) would put one literal
-    // mask per position in a VGPR of its own
-    unsigned fb = 0, lb = 0;
-#pragma unroll
-    for (int t = G - 1; t >= 0; --t) {
-      const unsigned s = key[t] >> LOGG;
-      const bool kv = key[t] != kSent32;
-      const bool f = kv && (t == 0 || s != (key[t > 0 ? t - 1 : 0] >> LOGG));
-      const bool l = kv && (t == G - 1 || s != (key[t < G - 1 ? t + 1 : t] >> LOGG));
-      fb = (fb << 1) | (f ? 1u : 0u);
-      lb = (lb << 1) | (l ? 1u : 0u);
-    }
-    unsigned vb = (n >= 32) ? 0xFFFFFFFFu : ((1u << n) - 1u);
-    // opaque to the optimiser: otherwise it folds the bit tests back into per-position
-    // compare masks and keeps ~3*G of them alive in SGPRs across the walk (spills)
-    asm volatile("" : "+v"(fb), "+v"(lb), "+v"(vb));
-    double wr[G];  // probabilities of the sorted slots; become the weights in the walk
-#pragma unroll
-    for (int t = 0; t < G; ++t) wr[t] = iP[rsp + (int)(key[t] & (G - 1))];  // sentinel: slot G-1, in the image
-    double2 ring[NG];
-#pragma unroll
-    for (int t = 0; t < NG; ++t) {
-      const unsigned ix = min(key[t] >> LOGG, smax);
-      if constexpr (!(BCE_ABLATE & 2)) ring[t] = tab[ix];
-      else ring[t] = make_double2(0.5, 0.25 + ix);
-    }
-    // the next tile: bounds from the batch, its DMA once every read of this image is done
-    const int64_t ntile = tile + tstride;
-    int64_t Bn = 0, En = 0;
-    if (ntile < n_tiles) {
-      if (((it + 1) & 63) == 0) {  // refresh the bounds batch (every 64 tiles)
-        wait_lgkm0();
-        load_bounds(it + 1);
-      }
-      Bn = bound(tbB, (int)((it + 1) & 63));
-      En = bound(tbE, (int)((it + 1) & 63));
-    }
-    auto next_dma = [&]() {
-      if (ntile < n_tiles) {
-        wait_lgkm0();  // keys / wr reads have landed
-        issue_dma(ntile, Bn, En);
-      }
-    };
-
-    // ---- walk (core.py:107-144 in sorted-source order) ---------------------------------------
-    double total = 0.0, ws = 0.0, cs = 0.0, psum = 0.0;
-    int cnt = 0, err = G;
-#pragma unroll
-    for (int t = 0; t < G; ++t) {
-      // bit tests as v_bfe with inline constants (a literal mask per position gets
-      // hoisted into a VGPR of its own: 3*G registers)
-      const bool kv = __builtin_amdgcn_ubfe(vb, t, 1) != 0u;
-      const int slot = (int)(key[t] & (G - 1));
-      const bool fst = __builtin_amdgcn_ubfe(fb, t, 1) != 0u;
-      const bool lst = __builtin_amdgcn_ubfe(lb, t, 1) != 0u;
-      const double p = wr[t];
-      const double2 rc = ring[t % NG];
-      if (t + NG < G) {
-        const unsigned ix = min(key[t + NG < G ? t + NG : t] >> LOGG, smax);
-        if constexpr (!(BCE_ABLATE & 2)) ring[t % NG] = tab[ix];
-      }
-      if (kv && (p < 0.0 || p > 1.0)) err = (slot < err) ? slot : err;  // core.py:59-60
-      psum = (fst ? 0.0 : psum) + p;   // builtin sum() from int 0 (core.py:116)
-      cnt = fst ? 1 : cnt + 1;
-      double avg = psum;
-      if (ballot(lst && cnt > 1)) {     // duplicates: sum / len (core.py:116), rare
-        if (lst && cnt > 1) avg = psum / (double)cnt;
-      }
-      const double wt = rc.x, cf = rc.y;
-      // accumulate only at the last position of a run; +0.0 leaves every chain bit-exact
-      // (the chains start at +0.0 and can never become -0.0)
-      total += lst ? wt : 0.0;          // core.py:120
-      ws += lst ? avg * wt : 0.0;       // core.py:135-137
-      cs += lst ? cf * wt : 0.0;        // core.py:141-143
-      wr[t] = wt;
-      // pin the chains here: left alone the compiler sinks every add to the end of the
-      // walk and keeps all per-position operands and masks alive
-      asm volatile("" : "+v"(total), "+v"(ws), "+v"(cs), "+v"(psum), "+v"(cnt), "+v"(err));
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // every gather of this tile has been consumed: the next tile's DMA now overlaps the
-    // per-market stores and the copy-out without any later wait covering it
-    next_dma();
-    const int u = __builtin_popcount(lb);
-
-    // ---- per-market results ---------------------------------------------------------------
-    if (has) {
-      const bool null_ = (total == 0.0);  // core.py:131-133
-      a.consensus[mk] = null_ ? 0.0 : ws / total;
-      a.confidence[mk] = null_ ? 0.0 : cs / total;
-      a.total_weight[mk] = total;
-      a.n_unique[mk] = u;
-      if (a.err_idx) a.err_idx[mk] = (err < G) ? err : -1;
-    }
-
-    // ---- per-unique outputs: CH sorted positions per chunk through the staging rows -----
-    if ((a.usid || a.weight || a.nweight) && !(BCE_ABLATE & 8)) {
-      sTot[w][lane] = total;
-      sMkOff[w][lane] = off;
-#pragma unroll
-      for (int c = 0; c < G / CH; ++c) {
-#pragma unroll
-        for (int i = 0; i < CH; ++i) {
-          const int t = c * CH + i;
-          const unsigned sid = key[t] >> LOGG;
-          const bool lst = __builtin_amdgcn_ubfe(lb, t, 1) != 0u;
-          const int j = lst ? __builtin_popcount(__builtin_amdgcn_ubfe(lb, 0, t)) : -1;
-          const unsigned ps = min(sid, smax);
-          const bool pr = is_present(sBits, (int)ps);  // host: S <= 32 * kBitsLds
-          const unsigned us = sid | (pr ? 0u : 0x80000000u);  // core.py:167-170
-          const uint2 wb = *reinterpret_cast<const uint2*>(&wr[t]);
-          stg[lane * SR + i] = make_uint4(us, (unsigned)j, wb.x, wb.y);
-        }
-        wave_sync_lds();
-#pragma unroll
-        for (int r = 0; r < CH; ++r) {
-          const int q = r * QPR + lane / CH;
-          const int i = lane % CH;
-          const uint4 e = stg[q * SR + i];
-          const int j = (int)e.y;
-          if (j >= 0) {
-            const int64_t pos = sMkOff[w][q] + j;
-            const double tot = sTot[w][q];
-            const double wt = __hiloint2double((int)e.w, (int)e.z);
-            if (a.usid) a.usid[pos] = (int32_t)e.x;
-            if (a.weight) a.weight[pos] = wt;
-            if (a.nweight) a.nweight[pos] = (tot > 0.0) ? wt / tot : 0.0;  // core.py:151
-          }
-        }
-        wave_sync_lds();
-      }
-    }
-    B = Bn;
-    E = En;
-  }
-}
-
-// ------------------------------------------------------------------------------------
 // consensus_pipe_kernel<G, C, R>: one loader wave + C compute waves per workgroup
 // ------------------------------------------------------------------------------------
 // The headline schedule.  Per workgroup (one per CU) an LDS ring of R tile slots:
@@ -1157,19 +779,9 @@ void consensus_stream_kernel(ConsArgs a) {
 // never touches registers the compute waves need.  Flags live in LDS (one workgroup).
 // Progress: the loader only waits for the release of sequence i-R, which a compute wave
 // is processing or has released (sequences are grabbed in order and R > C).
-#ifndef BCE_PIPE_PROF
-#define BCE_PIPE_PROF 0
-#endif
 #ifndef BCE_PIPE_RING
 #define BCE_PIPE_RING 16  // relconf gathers in flight per compute lane
 #endif
-#if BCE_PIPE_PROF
-__device__ unsigned long long g_pipe_prof[16];  // s_memtime cycles per compute-wave phase (debug build)
-#endif
-#ifndef BCE_SPIN_CAP
-#define BCE_SPIN_CAP (1 << 22)  // ~0.1-0.3 s of s_sleep polling per wait
-#endif
-constexpr int kSpinCap = BCE_SPIN_CAP;
 
 #ifndef BCE_PIPE_C32
 #define BCE_PIPE_C32 4  // compute waves at G = 32
@@ -1179,18 +791,9 @@ constexpr int kSpinCap = BCE_SPIN_CAP;
 #endif
 // Slots R >= C + 2: with one spare slot the ring is load-latency bound (a released slot
 // must be refilled within tile_time / C); two spares keep two tiles in flight.
-#ifndef BCE_PIPE_LPRIO
-#define BCE_PIPE_LPRIO 0  // loader wave priority (s_setprio)
-#endif
-#ifndef BCE_PIPE_NTS
-#define BCE_PIPE_NTS 0  // nontemporal per-unique output stores
-#endif
-#ifndef BCE_PIPE_L
-#define BCE_PIPE_L 1  // loader waves (each keeps its own tiles in flight; 2 measured slower: TA contention)
-#endif
 template <int G>
 struct PipeCfg {
-  static constexpr int L = BCE_PIPE_L;
+  static constexpr int L = 1;  // one loader wave (two measured slower: TA contention)
   static constexpr int C = (G == 32) ? BCE_PIPE_C32 : 6;
   static constexpr int R = (G == 32) ? BCE_PIPE_R32 : C + 3;
 };
@@ -1223,8 +826,6 @@ void consensus_pipe_kernel(ConsArgs a) {
   constexpr int RING = BCE_PIPE_RING;
   constexpr int NG = (G < RING) ? G : RING;
   constexpr int PA = 4;          // probabilities read this many positions ahead
-  constexpr int P2 = G / 2;      // copy-out lanes per market (two slots per lane)
-  constexpr int MPI = kWave / P2;
 
   __shared__ uint32_t sBits[kBitsLds];
   __shared__ __attribute__((aligned(16))) uint32_t sSid[R][SW];
@@ -1253,14 +854,7 @@ void consensus_pipe_kernel(ConsArgs a) {
 
   if (w < NL) {
     // ================================ loaders =========================================
-    if (BCE_PIPE_LPRIO) __builtin_amdgcn_s_setprio(BCE_PIPE_LPRIO);
     // loader w owns sequences i = w, w + NL, ... (slot i % R); k counts its own tiles
-#if BCE_PIPE_PROF
-    unsigned long long lp_t = __builtin_amdgcn_s_memtime(), lp[4] = {0, 0, 0, 0};
-#define LPROF(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); lp[k] += t_ - lp_t; lp_t = t_; } while (0)
-#else
-#define LPROF(k) do {} while (0)
-#endif
     const int64_t Nf4 = a.n_signals & ~3ll, Nf2 = a.n_signals & ~1ll;
     const int64_t clamp_s = (Nf4 - 4 > 0) ? Nf4 - 4 : 0;  // host: n_signals >= 4
     const int64_t clamp_p = (Nf2 - 2 > 0) ? Nf2 - 2 : 0;
@@ -1292,7 +886,7 @@ void consensus_pipe_kernel(ConsArgs a) {
       for (int k = 0; k < TS / kWave; ++k) {
         const int i = k * kWave + lane;
         const double p = sProb[s][d + ((i < nb) ? i : 0)];
-        const unsigned long long m = (BCE_ABLATE & 32) ? 0ull : ballot(i < nb && (p < 0.0 || p > 1.0));
+        const unsigned long long m = ballot(i < nb && (p < 0.0 || p > 1.0));
         sBad[s][2 * k] = (uint32_t)m;
         sBad[s][2 * k + 1] = (uint32_t)(m >> 32);
       }
@@ -1300,9 +894,6 @@ void consensus_pipe_kernel(ConsArgs a) {
     };
     auto publish = [&](int seq, int64_t t) {
       const int s = seq % R;
-#if BCE_PIPE_DBG
-      if (lane == 0 && blockIdx.x == 0) printf("[L] publish seq %d tile %ld slot %d\n", seq, (long)t, s);
-#endif
       // every lane stores the same words: no lane-0-only region inside the loop (the
       // structurizer splits loops around such regions and breaks wave-uniform state)
       sTile[s] = t;
@@ -1313,9 +904,6 @@ void consensus_pipe_kernel(ConsArgs a) {
     int64_t pend_t = -1, pend_B = 0, pend_E = 0;
     for (int64_t i = w, k = 0; i < my_tiles + C; i += NL, ++k) {
       const int s = (int)(i % R);
-#if BCE_PIPE_DBG
-      if (lane == 0 && blockIdx.x == 0) printf("[L] i %ld / %ld\n", (long)i, (long)(my_tiles + C));
-#endif
       // wait for the release of sequence i - R (publish what is in flight first)
       if (i >= R) {
         const int need = (int)(i - R) + 1;
@@ -1329,14 +917,13 @@ void consensus_pipe_kernel(ConsArgs a) {
           int spins = 0;
           while (ldsflag(&sFree[s]) < need) {
             __builtin_amdgcn_s_sleep(2);
-            if (++spins > kSpinCap) {  // never expected: bounded so a bug cannot hang the GPU,
+            if (++spins > a.spin_cap) {  // never expected: bounded so a bug cannot hang the GPU,
               raise_fault(a.fault, kFaultSpinLoader);  // and reported (bce_fault_check)
               return;
             }
           }
         }
       }
-      LPROF(0);  // waiting for a free slot (incl. publishing what was in flight)
       if (i >= my_tiles) {  // end markers: one per compute wave
         if (pending >= 0) {
           __builtin_amdgcn_s_waitcnt(0x0F70);
@@ -1403,13 +990,10 @@ void consensus_pipe_kernel(ConsArgs a) {
         const int d = tb + lane;
         dma_b32(og + ((d < ndw) ? d : 0), &sOffs[s][tb]);
       }
-      LPROF(1);  // issuing this tile's DMA
       if (pending >= 0) {  // the previous tile has landed once only this one is in flight
         __builtin_amdgcn_s_waitcnt((NDMA & 15) | (7 << 4) | (15 << 8) | ((NDMA >> 4) << 14));
-        LPROF(2);  // waiting for the previous tile to land
         finish(pending % R, pend_B, pend_E);
         publish(pending, pend_t);
-        LPROF(3);  // validation + publish
       }
       pending = (int)i;
       pend_t = t;
@@ -1421,22 +1005,11 @@ void consensus_pipe_kernel(ConsArgs a) {
       finish(pending % R, pend_B, pend_E);
       publish(pending, pend_t);
     }
-#if BCE_PIPE_PROF
-    if (lane == 0)
-      for (int q = 0; q < 4; ++q) atomicAdd(&g_pipe_prof[8 + q], lp[q]);
-#endif
-#undef LPROF
     return;
   }
 
   // ================================ compute waves =====================================
   const int cw = w - NL;
-#if BCE_PIPE_PROF
-  unsigned long long pr_t = __builtin_amdgcn_s_memtime(), pr[6] = {0, 0, 0, 0, 0, 0};
-#define PROF_MARK(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); pr[k] += t_ - pr_t; pr_t = t_; } while (0)
-#else
-#define PROF_MARK(k) do {} while (0)
-#endif
   const unsigned smax = (unsigned)(a.n_sources > 0 ? a.n_sources - 1 : 0);
   const double2* const tab = (a.n_sources > 0) ? a.relconf : kColdRow;
   const int64_t Nf4 = a.n_signals & ~3ll, Nf2 = a.n_signals & ~1ll;
@@ -1446,31 +1019,19 @@ void consensus_pipe_kernel(ConsArgs a) {
     const int tk = __hip_atomic_fetch_add(&sNext, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     const int seq = __builtin_amdgcn_readfirstlane(tk) >> 6;
     const int s = seq % R;
-#if BCE_PIPE_DBG
-    if (lane == 0 && blockIdx.x == 0) printf("[C%d] grab seq %d\n", w, seq);
-#endif
     int spins = 0;
     while (ldsflag(&sReady[s]) != seq + 1) {
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > kSpinCap) {  // never expected: bounded so a bug cannot hang the GPU,
+      if (++spins > a.spin_cap) {  // never expected: bounded so a bug cannot hang the GPU,
         raise_fault(a.fault, kFaultSpinCompute);  // and reported (bce_fault_check)
         return;
       }
     }
-    PROF_MARK(0);  // waiting for a loaded slot
     const int64_t tile0 = sTile[s];
     const int64_t tile = ((int64_t)__builtin_amdgcn_readfirstlane((int)(tile0 >> 32)) << 32) |
                          (uint32_t)__builtin_amdgcn_readfirstlane((int)tile0);  // uniform
-#if BCE_PIPE_DBG
-    if (lane == 0 && blockIdx.x == 0) printf("[C%d] seq %d ready, tile %ld\n", w, seq, (long)tile);
-#endif
     if (tile < 0) {
       __hip_atomic_store(&sFree[s], seq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-#if BCE_PIPE_PROF
-      if (lane_id() == 0)
-        for (int k = 0; k < 5; ++k) atomicAdd(&g_pipe_prof[k], pr[k]);
-      if (lane_id() == 0) atomicAdd(&g_pipe_prof[5], 1ull);
-#endif
       break;
     }
     uint32_t* const iS = sSid[s];
@@ -1495,6 +1056,10 @@ void consensus_pipe_kernel(ConsArgs a) {
       off = ((int64_t)iO[2 * ln + 1] << 32) | iO[2 * ln];
       n = (int)((((int64_t)iO[2 * ln + 3] << 32) | iO[2 * ln + 2]) - off);
     }
+    if (ballot(n < 0 || n > G)) {  // longer than the launch's max_len: report, skip
+      raise_fault(a.fault, kFaultTooLong);
+      if (n < 0 || n > G) n = 0;
+    }
     const int rs = (int)(off - B);
     const int rsi = rs + (int)(B - Bs);
     const int rsp = rs + (int)(B - Bp);
@@ -1513,7 +1078,7 @@ void consensus_pipe_kernel(ConsArgs a) {
     }
 #pragma unroll
     for (int t = 0; t < G; ++t) key[t] = (t < n) ? ((key[t] << LOGG) | (unsigned)t) : kSent32;
-    if constexpr (!(BCE_ABLATE & 1)) oem_sort<G>(key);
+    oem_sort<G>(key);
     // run boundaries: bit t of nq = (sid_t != sid_t+1); sentinels sort last and never
     // equal a sid, so lst = nq | top bit, fst = nq << 1 | 1, both masked to t < n
     unsigned nq = 0;
@@ -1525,13 +1090,11 @@ void consensus_pipe_kernel(ConsArgs a) {
     asm volatile("" : "+v"(fb), "+v"(lb), "+v"(vb));
     wave_sync_lds();  // every lane has its sids: rows become usid staging
 
-    PROF_MARK(1);  // keys + sort
     double2 ring[NG];
 #pragma unroll
     for (int t = 0; t < NG; ++t) {
       const unsigned ix = min(key[t] >> LOGG, smax);
-      if constexpr (!(BCE_ABLATE & 2)) ring[t] = tab[ix];
-      else ring[t] = make_double2(0.5, 0.25 + ix);
+      ring[t] = tab[ix];
     }
     double pq[PA];
 #pragma unroll
@@ -1558,7 +1121,7 @@ void consensus_pipe_kernel(ConsArgs a) {
       const double2 rc = ring[t % NG];
       if (t + NG < G) {
         const unsigned ix = min(key[t + NG < G ? t + NG : t] >> LOGG, smax);
-        if constexpr (!(BCE_ABLATE & 2)) ring[t % NG] = tab[ix];
+        ring[t % NG] = tab[ix];
       }
       const double wt = rc.x, cf = rc.y;
       const bool kv = __builtin_amdgcn_ubfe(vb, t, 1) != 0u;
@@ -1594,7 +1157,6 @@ void consensus_pipe_kernel(ConsArgs a) {
       __builtin_amdgcn_sched_barrier(0);
     }
 
-    PROF_MARK(2);  // walk
     // ---- per-market results --------------------------------------------------------------
     if (has) {
       const bool null_ = (total == 0.0);  // core.py:131-133
@@ -1616,12 +1178,11 @@ void consensus_pipe_kernel(ConsArgs a) {
     }
     wave_sync_lds();
 
-    PROF_MARK(3);  // per-market results
     // ---- per-unique outputs from the in-place staging ------------------------------------
     // lane = (market q, slot pair k2), batches of CB iterations: the three dependent LDS
     // round trips (info -> packed usid -> weight cell / present bit) are issued for the
     // whole batch before any result is used, and no load sits under a branch.
-    if (!(BCE_ABLATE & 8)) {
+    {
       const int dB = (int)(B - Bs), dP = (int)(B - Bp);
       auto copy_out = [&](auto npl) {
         constexpr int NPL = decltype(npl)::value;  // 2: slot pairs (16-B stores), 1: single slots
@@ -1680,18 +1241,9 @@ void consensus_pipe_kernel(ConsArgs a) {
             const double n1 = (tot > 0.0) ? w1[b] / tot : 0.0;  // (cold bit: core.py:167-170)
             const int64_t pos = B + r[b] + k2;
             if (v1[b]) {
-#if BCE_PIPE_NTS
-              // streaming outputs are never re-read by this launch: nontemporal stores
-              typedef unsigned v2u __attribute__((ext_vector_type(2)));
-              typedef double v2d __attribute__((ext_vector_type(2)));
-              __builtin_nontemporal_store((v2u){x0, x1}, reinterpret_cast<v2u*>(a.usid + pos));
-              __builtin_nontemporal_store((v2d){w0[b], w1[b]}, reinterpret_cast<v2d*>(a.weight + pos));
-              __builtin_nontemporal_store((v2d){n0, n1}, reinterpret_cast<v2d*>(a.nweight + pos));
-#else
               *reinterpret_cast<uint2*>(a.usid + pos) = make_uint2(x0, x1);
               *reinterpret_cast<double2*>(a.weight + pos) = make_double2(w0[b], w1[b]);
               *reinterpret_cast<double2*>(a.nweight + pos) = make_double2(n0, n1);
-#endif
             } else if (v0[b]) {
               a.usid[pos] = (int32_t)x0;
               a.weight[pos] = w0[b];
@@ -1707,10 +1259,6 @@ void consensus_pipe_kernel(ConsArgs a) {
         copy_out(std::integral_constant<int, 1>{});
     }
     wave_sync_lds();  // every read of the slot has returned
-    PROF_MARK(4);  // copy-out
-#if BCE_PIPE_DBG
-    if (lane == 0 && blockIdx.x == 0) printf("[C%d] seq %d done\n", w, seq);
-#endif
     __hip_atomic_store(&sFree[s], seq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
 }
@@ -2032,7 +1580,7 @@ __device__ __forceinline__ void wide_sort(unsigned (&key)[R], unsigned* sX, int 
 template <int NW, int R>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 8))) void consensus_wide_kernel(ConsArgs a) {
   using Cfg = WideCfg<NW, R>;
-  constexpr int NT = Cfg::NT, P = Cfg::P, IB = Cfg::IB, XROW = Cfg::XROW;
+  constexpr int NT = Cfg::NT, P = Cfg::P, IB = Cfg::IB;
   constexpr unsigned QMASK = (unsigned)P - 1u;
   __shared__ __attribute__((aligned(16))) double sRegA[Cfg::A_DBL];
   __shared__ __attribute__((aligned(16))) double sRegB[Cfg::B_DBL];
@@ -2050,12 +1598,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 8)))
   const int lane = lane_id();
   const int wv = t >> 6;
   const unsigned smax = (unsigned)(a.n_sources > 0 ? a.n_sources - 1 : 0);
-#if BCE_PIPE_PROF
-  unsigned long long pr_t = __builtin_amdgcn_s_memtime(), pr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#define WPROF(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); pr[k] += t_ - pr_t; pr_t = t_; } while (0)
-#else
 #define WPROF(k) do {} while (0)
-#endif
 
   // Market metadata for this workgroup's next 64 markets (li = base + G*k on lane k) is
   // loaded in one vector batch, so picking a market is a readlane, never a scalar-load
@@ -2096,9 +1639,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 8)))
   if (blockIdx.x < a.n_list) fetch(blockIdx.x);
 
   for (int64_t li = blockIdx.x; li < a.n_list; li += gridDim.x) {
-#if BCE_PIPE_PROF
-    pr[7] += 1;
-#endif
     const int32_t m = pm;
     const int64_t off = poff;
     const int n = pn;
@@ -2369,10 +1909,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 8)))
         a.nweight[off + jj] = (total > 0.0) ? sP[(jj)] / total : 0.0;
     WPROF(6);
   }
-#if BCE_PIPE_PROF
-  if (lane == 0 && wv < 2)
-    for (int k = 0; k < 8; ++k) atomicAdd(&g_pipe_prof[wv * 8 + k], pr[k]);
-#endif
 #undef WPROF
 }
 
@@ -2392,8 +1928,7 @@ int launch_seg(const ConsArgs& a, hipStream_t st) {
   static int per_cu = 0;
   if (!per_cu) {
     int nb = 0;
-    if (BCE_SEG_GRID_PER_CU > 0) nb = BCE_SEG_GRID_PER_CU;
-    else if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, consensus_seg_kernel<G, TM>, 64, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, consensus_seg_kernel<G, TM>, 64, 0) !=
                  hipSuccess || nb <= 0)
       nb = 8;
     per_cu = nb;
@@ -2411,8 +1946,7 @@ int launch_lpm(const ConsArgs& a, hipStream_t st) {
   static int per_cu = 0;
   if (!per_cu) {
     int nb = 0;
-    if (BCE_SEG_GRID_PER_CU > 0) nb = BCE_SEG_GRID_PER_CU;
-    else if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, consensus_lpm_kernel<G>, 64, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, consensus_lpm_kernel<G>, 64, 0) !=
                  hipSuccess || nb <= 0)
       nb = 4;
     per_cu = nb;
@@ -2447,30 +1981,6 @@ int launch_pipe(const ConsArgs& a, hipStream_t st) {
 }
 
 template <int G>
-int launch_stream(const ConsArgs& a, hipStream_t st) {
-  constexpr int TM = 64, WPB = BCE_STREAM_WPB, CH = (G < BCE_STREAM_CH) ? G : BCE_STREAM_CH;
-  const int64_t tiles = (a.n_list + TM - 1) / TM;
-  if (tiles == 0) return BCE_OK;
-  static int per_cu = 0;
-  if (!per_cu) {
-    int nb = 0;
-    if (BCE_SEG_GRID_PER_CU > 0) nb = BCE_SEG_GRID_PER_CU;
-    else if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, consensus_stream_kernel<G, TM, WPB, CH>, 64 * WPB, 0) !=
-                 hipSuccess || nb <= 0)
-      nb = 1;
-    per_cu = nb;
-    if (getenv("BCE_DEBUG_LAUNCH"))
-      fprintf(stderr, "[bce] consensus_stream_kernel<%d,%d,%d,%d>: %d blocks/CU x %d CUs\n", G, TM, WPB, CH, nb,
-              cu_count());
-  }
-  const int64_t blocks = (tiles + WPB - 1) / WPB;
-  const int64_t cap = (int64_t)cu_count() * per_cu;
-  const int grid = (int)(blocks < cap ? blocks : cap);
-  hipLaunchKernelGGL((consensus_stream_kernel<G, TM, WPB, CH>), dim3(grid), dim3(64 * WPB), 0, st, a);
-  return check_launch("consensus_stream_kernel");
-}
-
-template <int G>
 int launch_flat(const ConsArgs& a, hipStream_t st) {
   constexpr int TM = BCE_FLAT_TM, WPB = BCE_FLAT_WPB;
   const int64_t tiles = (a.n_list + TM - 1) / TM;
@@ -2478,8 +1988,7 @@ int launch_flat(const ConsArgs& a, hipStream_t st) {
   static int per_cu = 0;
   if (!per_cu) {
     int nb = 0;
-    if (BCE_SEG_GRID_PER_CU > 0) nb = BCE_SEG_GRID_PER_CU;
-    else if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, consensus_flat_kernel<G, TM, WPB>, 64 * WPB, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, consensus_flat_kernel<G, TM, WPB>, 64 * WPB, 0) !=
                  hipSuccess || nb <= 0)
       nb = 2;
     per_cu = nb;
@@ -2493,34 +2002,27 @@ int launch_flat(const ConsArgs& a, hipStream_t st) {
   return check_launch("consensus_flat_kernel");
 }
 
+// Markets with n <= 64 (a.list == NULL: contiguous CSR; else a planned market list).
+//   contiguous, 16 < n <= 32, S <= kTabMaxSources   consensus_tab32_kernel (table in LDS)
+//   contiguous, n <= 32, S <= 16384, all outputs     consensus_pipe_kernel<G> (loader + compute waves)
+//   contiguous, n <= 32, otherwise                   consensus_flat_kernel<G>
+//   market list, n <= 32                             consensus_lpm_kernel<G> (lane per market)
+//   33 <= n <= 64                                    consensus_seg_kernel<64, 8>
 int launch_seg_for_len(int max_len, const ConsArgs& a, hipStream_t st) {
-  if (a.list == nullptr && max_len > 16 && max_len <= 32 && a.n_sources <= kTabMaxSources)
-    return launch_tab32(a, st);
-  if (BCE_FLAT == 3 && a.list == nullptr && max_len <= 32 && a.n_sources <= 32 * kBitsLds && a.n_signals >= 4 &&
-      a.usid && a.weight && a.nweight) {
-    if (max_len <= 8) return launch_pipe<8>(a, st);
-    if (max_len <= 16) return launch_pipe<16>(a, st);
-    return launch_pipe<32>(a, st);
-  }
-  if (BCE_FLAT == 2 && a.list == nullptr && max_len <= 32 && a.n_sources <= 32 * kBitsLds) {
-    if (max_len <= 8) return launch_stream<8>(a, st);
-    if (max_len <= 16) return launch_stream<16>(a, st);
-    return launch_stream<32>(a, st);
-  }
-  if (BCE_FLAT && a.list == nullptr && max_len <= 32 && a.n_sources <= (1 << kPackSlot)) {
+  if (a.list == nullptr && max_len <= 32) {
+    if (max_len > 16 && a.n_sources <= kTabMaxSources) return launch_tab32(a, st);
+    if (a.n_sources <= 32 * kBitsLds && a.n_signals >= 4 && a.usid && a.weight && a.nweight) {
+      if (max_len <= 8) return launch_pipe<8>(a, st);
+      if (max_len <= 16) return launch_pipe<16>(a, st);
+      return launch_pipe<32>(a, st);
+    }
     if (max_len <= 8) return launch_flat<8>(a, st);
     if (max_len <= 16) return launch_flat<16>(a, st);
     return launch_flat<32>(a, st);
   }
-  if (BCE_USE_LPM) {
-    if (max_len <= 8) return launch_lpm<8>(a, st);
-    if (max_len <= 16) return launch_lpm<16>(a, st);
-    if (max_len <= 32) return launch_lpm<32>(a, st);
-  } else {
-    if (max_len <= 8) return launch_seg<8, 64>(a, st);
-    if (max_len <= 16) return launch_seg<16, 32>(a, st);
-    if (max_len <= 32) return launch_seg<32, BCE_SEG32_TM>(a, st);
-  }
+  if (max_len <= 8) return launch_lpm<8>(a, st);
+  if (max_len <= 16) return launch_lpm<16>(a, st);
+  if (max_len <= 32) return launch_lpm<32>(a, st);
   return launch_seg<64, 8>(a, st);
 }
 
@@ -2556,7 +2058,7 @@ int launch_wide(const ConsArgs& a, hipStream_t st) {
 int launch_wide_for_len(int64_t max_len, const ConsArgs& a, hipStream_t st) {
   const int ib = max_len <= 128 ? 7 : max_len <= 256 ? 8 : max_len <= 512 ? 9 : max_len <= 1024 ? 10
                : max_len <= 2048 ? 11 : 12;
-  if (BCE_WIDE && a.mode == BCE_MODE_EXACT && (int64_t)a.n_sources <= (1ll << (32 - ib))) {
+  if (a.mode == BCE_MODE_EXACT && (int64_t)a.n_sources <= (1ll << (32 - ib))) {
     switch (ib) {
       case 7: return launch_wide<1, 2>(a, st);
       case 8: return launch_wide<1, 4>(a, st);
@@ -2649,6 +2151,7 @@ extern "C" int bce_consensus_csr(const int64_t* offsets, int64_t n_markets, cons
   a.n_unique = n_unique; a.err_idx = err_idx; a.usid = usid; a.weight = weight; a.nweight = nweight;
   a.mode = mode;
   a.fault = fault_word();
+  a.spin_cap = spin_cap();
   if (a.n_list == 0) return BCE_OK;
   int64_t L = max_len;
   if (L <= 0) {  // unknown: measure on device (synchronises)
@@ -2744,6 +2247,7 @@ extern "C" int bce_consensus_planned(const int64_t* offsets, int64_t n_markets, 
   base.total_weight = total_weight; base.n_unique = n_unique; base.err_idx = err_idx;
   base.usid = usid; base.weight = weight; base.nweight = nweight; base.mode = mode;
   base.fault = fault_word();
+  base.spin_cap = spin_cap();
   const bool seg_ok = n_sources <= (1 << 25);
   for (int b = 0; b < BCE_NBINS; ++b) {
     ConsArgs a = base;
@@ -2798,14 +2302,6 @@ __global__ __launch_bounds__(256) void validate_kernel(const int64_t* offsets, i
 }
 }  // namespace bce
 
-#if BCE_PIPE_PROF
-extern "C" int bce_pipe_prof_read(unsigned long long* host16) {
-  BCE_HIP(hipMemcpyFromSymbol(host16, HIP_SYMBOL(bce::g_pipe_prof), 16 * sizeof(unsigned long long)));
-  unsigned long long z[16] = {0};
-  BCE_HIP(hipMemcpyToSymbol(HIP_SYMBOL(bce::g_pipe_prof), z, sizeof z));
-  return BCE_OK;
-}
-#endif
 
 extern "C" int bce_validate_csr(const int64_t* offsets, int64_t n_markets, const double* prob,
                                 int32_t* err_idx, void* stream) {

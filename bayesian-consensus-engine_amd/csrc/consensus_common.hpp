@@ -30,7 +30,8 @@ struct ConsArgs {
   int32_t mode;
   void* scratch;      // long kernel, global variant
   int64_t scratch_stride;  // elements (keys) per workgroup slice
-  int* fault;         // device word: set to a BCE_FAULT_* code by a wave that gave up
+  int* fault;         // device word: set to a kFault* code by a wave that gave up
+  int spin_cap;       // bounded waits of the persistent pipe kernel (polls before giving up)
 };
 
 // Device fault codes (bce_fault_check reports them).
@@ -139,6 +140,8 @@ __device__ __forceinline__ void dma_b32(const void* g, const void* lds) {
 // ---- host side -------------------------------------------------------------------------
 // The device fault word of the current device (allocated once, zeroed).
 int* fault_word();
+// Polls a persistent wave makes before it gives up (bce_debug_set_spin_cap; default 2^22).
+int spin_cap();
 
 // LDS-table kernel (consensus_tab.hip): contiguous markets with n <= 32 and
 // n_sources <= kTabMaxSources.

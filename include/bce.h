@@ -79,6 +79,10 @@ int bce_device_count(void);
  * of failing silently.  BCE_OK when clean, else BCE_EHIP with the reason in
  * bce_last_error(). */
 int bce_fault_check(void* stream);
+/* Test hook: polls a persistent wave makes before giving up (<= 0 restores the default,
+ * 2^22).  A tiny cap makes the pipe kernel's waves give up at once, which exercises the
+ * fault path above; results of such a launch are garbage. */
+int bce_debug_set_spin_cap(int cap);
 
 /* ---- consensus: core.compute_consensus (core.py:63-179) + validation -------------
  *

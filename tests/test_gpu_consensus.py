@@ -134,8 +134,8 @@ def _compare_vec(out, exp, offsets):
     assert M == len(u)
 
 
-def test_stream_kernel_many_tiles_per_wave():
-    """> 64 tiles per wave: exercises the streamed kernel's bounds-batch refresh."""
+def test_many_tiles_per_wave():
+    """6M tiny markets (> 64 tiles per wave of the persistent short-market kernels)."""
     rng = np.random.default_rng(11)
     M, S = 6_000_000, 1000
     lens = rng.integers(0, 3, M)
@@ -174,3 +174,114 @@ def test_short_ragged_unaligned(maxlen, S, M, seed):
     g = dict(offsets=off, sid=sid, prob=prob, rel=rel, conf=conf, present=present)
     exp = orc.consensus_csr(off, sid, prob, rel, conf, present)
     _compare_vec(_run(g, max_len=maxlen), exp, off)
+
+
+def _c2_like(M, S, seed, L=32, base=0):
+    rng = np.random.default_rng(seed)
+    sid = rng.integers(0, S, M * L).astype(np.int32)
+    prob = rng.random(M * L)
+    prob[rng.random(M * L) < 0.003] = 1.5
+    off = np.arange(0, M * L + 1, L, dtype=np.int64) + base
+    sid = np.concatenate([np.zeros(base, np.int32), sid])
+    prob = np.concatenate([np.zeros(base), prob])
+    rel = rng.uniform(0.1, 1.0, S)
+    conf = rng.random(S)
+    present = (rng.random(S) < 0.9).astype(np.uint8)
+    rel[present == 0] = 0.5
+    conf[present == 0] = 0.25
+    return dict(offsets=off, sid=sid, prob=prob, rel=rel, conf=conf, present=present)
+
+
+@pytest.mark.parametrize("S", [10000, 10112, 12000, 16384, 20000, 100000])
+def test_c2_shape_every_table_size(S):
+    """n = 32 contiguous markets: LDS-table kernel (S <= 10112), pipe kernel (S <= 16384),
+    flat kernel (larger tables) -- all bit-exact, all eight outputs."""
+    g = _c2_like(20000, S, S)
+    exp = orc.consensus_csr(g["offsets"], g["sid"], g["prob"], g["rel"], g["conf"], g["present"])
+    _compare_vec(_run(g, max_len=32), exp, g["offsets"])
+
+
+@pytest.mark.parametrize("S,L,base", [(10000, 32, 0), (10000, 32, 4), (10000, 32, 1), (12000, 32, 0),
+                                      (30000, 32, 0), (5000, 16, 0), (40000, 8, 3)])
+def test_compact_mode(S, L, base):
+    """unique_outputs=False (usid/weight/nweight NULL): per-market outputs only, on every
+    contiguous short-market kernel; offset views with aligned and unaligned bases."""
+    from bayesian_engine import batch
+    g = _c2_like(9000, S, S + L, L=L, base=base)
+    exp = orc.consensus_csr(g["offsets"], g["sid"], g["prob"], g["rel"], g["conf"], g["present"])
+    table = batch.SourceTable.from_arrays(_dev(g["rel"]), _dev(g["conf"]), _dev(g["present"]))
+    r = batch.consensus(_dev(g["offsets"]), _dev(g["sid"], np.int32), _dev(g["prob"]), table, max_len=L,
+                        unique_outputs=False)
+    torch.cuda.synchronize()
+    assert r.usid is None and r.weight is None and r.nweight is None
+    for k in ("n_unique", "err_idx"):
+        assert np.array_equal(getattr(r, k).cpu().numpy(), exp[k]), k
+    for k in ("consensus", "confidence", "total_weight"):
+        assert np.array_equal(getattr(r, k).cpu().numpy(), exp[k], equal_nan=True), k
+
+
+def test_tab_kernel_mixed_regular_and_ragged_tiles():
+    """Mostly 32-signal markets with a few short ones and empty ones scattered: regular
+    tiles take the transposed path, the others the per-lane path, same results."""
+    rng = np.random.default_rng(21)
+    M, S = 30000, 9000
+    lens = np.full(M, 32)
+    lens[rng.integers(0, M, 40)] = rng.integers(0, 32, 40)
+    off = np.zeros(M + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    n = int(off[-1])
+    sid = rng.integers(0, S, n).astype(np.int32)
+    prob = rng.random(n)
+    rel, conf = rng.uniform(0, 1, S), rng.random(S)
+    present = (rng.random(S) < 0.8).astype(np.uint8)
+    g = dict(offsets=off, sid=sid, prob=prob, rel=rel, conf=conf, present=present)
+    exp = orc.consensus_csr(off, sid, prob, rel, conf, present)
+    _compare_vec(_run(g, max_len=32), exp, off)
+
+
+@pytest.mark.parametrize("S", [1, 2, 7, 40])
+def test_tab_kernel_heavy_duplicates(S):
+    """Tiny tables: nearly every market is all duplicates (many averaging / compaction
+    rounds per wave, runs of up to 32)."""
+    g = _c2_like(6000, S, 100 + S)
+    exp = orc.consensus_csr(g["offsets"], g["sid"], g["prob"], g["rel"], g["conf"], g["present"])
+    _compare_vec(_run(g, max_len=32), exp, g["offsets"])
+
+
+def test_fault_word_reports_bad_sid_and_long_market():
+    from bayesian_engine import _native as N, batch
+    g = _c2_like(3000, 500, 5)
+    table = batch.SourceTable.from_arrays(_dev(g["rel"]), _dev(g["conf"]), _dev(g["present"]))
+    N.check_faults()  # clean
+    sid = g["sid"].copy()
+    sid[777] = 500  # == n_sources
+    batch.consensus(_dev(g["offsets"]), _dev(sid, np.int32), _dev(g["prob"]), table, max_len=32)
+    with pytest.raises(N.BCEError, match="n_sources"):
+        N.check_faults()
+    N.check_faults()  # the word was cleared
+    off = g["offsets"].copy()
+    off[10] += 5  # market 9 has 37 signals, launched as max_len 32
+    batch.consensus(_dev(off), _dev(g["sid"], np.int32), _dev(g["prob"]), table, max_len=32)
+    with pytest.raises(N.BCEError, match="max_len"):
+        N.check_faults()
+
+
+def test_pipe_kernel_spin_cap_reports_fault():
+    """A persistent wave that exhausts its bounded wait records a fault instead of silently
+    leaving its tiles unwritten (forced with a tiny cap on the pipe kernel, S = 12000)."""
+    from bayesian_engine import _native as N, batch
+    L = N.lib()
+    g = _c2_like(50000, 12000, 9)
+    table = batch.SourceTable.from_arrays(_dev(g["rel"]), _dev(g["conf"]), _dev(g["present"]))
+    args = (_dev(g["offsets"]), _dev(g["sid"], np.int32), _dev(g["prob"]), table)
+    N.check_faults()
+    try:
+        N.check(L.bce_debug_set_spin_cap(1))
+        batch.consensus(*args, max_len=32)
+        with pytest.raises(N.BCEError, match="timed out"):
+            N.check_faults()
+    finally:
+        L.bce_debug_set_spin_cap(0)
+    exp = orc.consensus_csr(g["offsets"], g["sid"], g["prob"], g["rel"], g["conf"], g["present"])
+    _compare_vec(_run(g, max_len=32), exp, g["offsets"])
+    N.check_faults()
