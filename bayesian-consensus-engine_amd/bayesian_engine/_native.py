@@ -61,9 +61,9 @@ _SIGS = {
     "bce_outcome_update": (C.c_int, [_i64, _vp, _vp, _vp, _vp, _vp, _i64, _f64, _f64, _vp]),
     "bce_replay_step": (C.c_int, [_i64, _vp, _vp, _vp, _vp, _vp, _i64, _f64, _f64, _f64, _f64, _vp, _vp]),
     "bce_tiebreak_csr": (C.c_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp,
-                                   _vp, _vp, _vp, _vp, _vp, _vp]),
-    "bce_tiebreak_csr_long": (C.c_int, [_vp, _i64, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
-                                        _vp, _vp, _vp, _vp, _vp, _vp]),
+                                   _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "bce_tiebreak_csr_long": (C.c_int, [_vp, _i64, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
+                                        _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "bce_agreement_stats": (C.c_int, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "bce_reestimate_consensus": (C.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp]),
     "bce_reestimate_agreement": (C.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp]),

@@ -85,7 +85,7 @@ class SourceTable:
         for i, n in enumerate(names):
             if n in sr:
                 present[i] = 1
-                d = sr.get(n) or {}
+                d = sr.get(n, {})  # a None value raises AttributeError, as core.py:110-111 does
                 r = d.get("reliability", DEFAULT_RELIABILITY)
                 c = d.get("confidence", DEFAULT_CONFIDENCE)
                 acc = 0.0
@@ -304,11 +304,15 @@ class TieBreakResult:
     g_density: torch.Tensor
     g_avgconf: torch.Tensor
     g_maxrel: torch.Tensor
+    g_of: torch.Tensor      # int32[N]: each signal's group ordinal (first-seen order)
 
 
 def tiebreak(offsets: torch.Tensor, pred: torch.Tensor, conf: torch.Tensor, weight: torch.Tensor,
              rel: torch.Tensor, *, precision: int = 6, offsets_host: Optional[np.ndarray] = None) -> TieBreakResult:
-    """DeterministicTieBreaker(precision).resolve for every CSR market (tiebreak.py:73-152)."""
+    """DeterministicTieBreaker(precision).resolve for every CSR market (tiebreak.py:73-152).
+
+    Any market length (> 4096 agents sort in a global scratch slice).  ``precision`` as
+    CPython round(): exact for -15..22, below -308 and above 323 (BCEError otherwise)."""
     L = N.require_gpu()
     M = offsets.numel() - 1
     Nsig = pred.numel()
@@ -318,14 +322,13 @@ def tiebreak(offsets: torch.Tensor, pred: torch.Tensor, conf: torch.Tensor, weig
     r = TieBreakResult(torch.empty(M, **f64), torch.empty(M, **i32), torch.empty(M, **i32),
                        torch.empty(M, **f64), torch.empty(max(Nsig, 1), **f64),
                        torch.empty(max(Nsig, 1), **i32), torch.empty(max(Nsig, 1), **f64),
-                       torch.empty(max(Nsig, 1), **f64), torch.empty(max(Nsig, 1), **f64))
+                       torch.empty(max(Nsig, 1), **f64), torch.empty(max(Nsig, 1), **f64),
+                       torch.empty(max(Nsig, 1), **i32))
     offh = offsets_host if offsets_host is not None else offsets.cpu().numpy()
     lens = np.diff(offh)
     long_ = np.nonzero(lens > 64)[0]
-    if len(long_) and lens.max() > 4096:
-        raise N.BCEError("tiebreak: markets longer than 4096 agents are not supported by this build")
     outs = (N.ptr(r.winner), N.ptr(r.label), N.ptr(r.n_groups), N.ptr(r.variance), N.ptr(r.g_key),
-            N.ptr(r.g_count), N.ptr(r.g_density), N.ptr(r.g_avgconf), N.ptr(r.g_maxrel))
+            N.ptr(r.g_count), N.ptr(r.g_density), N.ptr(r.g_avgconf), N.ptr(r.g_maxrel), N.ptr(r.g_of))
     ins = (N.ptr(pred), N.ptr(conf), N.ptr(weight), N.ptr(rel))
     st = N.stream(dev)
     if len(long_) == 0:
@@ -338,8 +341,8 @@ def tiebreak(offsets: torch.Tensor, pred: torch.Tensor, conf: torch.Tensor, weig
         N.check(L.bce_tiebreak_csr(N.ptr(offsets), M, N.ptr(sl), len(short), *ins, 64, int(precision), *outs, st),
                 "bce_tiebreak_csr")
     ll = torch.from_numpy(long_.astype(np.int32)).to(dev)
-    N.check(L.bce_tiebreak_csr_long(N.ptr(offsets), M, N.ptr(ll), len(long_), int(precision), *ins, *outs, st),
-            "bce_tiebreak_csr_long")
+    N.check(L.bce_tiebreak_csr_long(N.ptr(offsets), M, N.ptr(ll), len(long_), int(precision), *ins,
+                                    int(lens[long_].max()), *outs, st), "bce_tiebreak_csr_long")
     return r
 
 

@@ -1,145 +1,178 @@
-"""Drop-in for ``bayesian_engine.cli`` (reference src/bayesian_engine/cli.py:1-178).
+"""``bayesian-engine`` command line -- a caller of the hot path (reference
+src/bayesian_engine/cli.py:1-178 defines the surface this keeps).
 
-Same argparse surface (global --db/--dry-run/--input; subcommands consensus,
-report-outcome, list-sources; no subcommand = legacy consensus), same JSON on stdout
-(``json.dumps(indent=2)``) and the same error text on stderr / exit code 1.  It is a
-caller of the hot path: validation, consensus, decay and outcome updates run in the
-HIP engine through the drop-in modules.
+Kept from the reference, byte for byte: the argparse surface (global --db/--dry-run/--input;
+subcommands consensus, report-outcome, list-sources; no subcommand = the legacy consensus
+path that never consults the store), the JSON on stdout (``json.dumps(indent=2)``), the
+error text on stderr and exit status 1.  The reference quirk that a global ``--input``
+placed before ``consensus`` is replaced by the subcommand's own default (cli.py:138) holds
+too, because the subcommand declares its own ``--input``.
+
+Added: ``consensus-batch`` -- a JSONL file of payloads, one engine launch for the batch
+(SURVEY.md §8(f) f2), printing per line what ``consensus`` prints for that payload alone.
+
+Structure: every consensus flavour goes through :func:`_consensus`; the store-backed
+commands share :func:`_with_store`; the parser is built from the :data:`COMMANDS` table.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import sys
-from typing import Any
+from typing import Any, Callable, Dict, Iterable, List, Optional, Tuple
 
 from .core import ValidationError, compute_consensus, validate_input_payload
 from .reliability import SQLiteReliabilityStore
 
 
-def _load_input(input_path: str | None) -> dict[str, Any]:
-    if input_path:
-        with open(input_path, "r", encoding="utf-8") as f:
-            return json.load(f)
+def _emit(obj: Any) -> None:
+    print(json.dumps(obj, indent=2))
+
+
+def _fail(message: str, cause: Optional[BaseException] = None) -> None:
+    print(message, file=sys.stderr)
+    raise SystemExit(1) from cause
+
+
+def _read_payload(path: Optional[str]) -> Dict[str, Any]:
+    """--input file, else JSON on a non-terminal stdin (cli.py:14-22)."""
+    if path:
+        with open(path, "r", encoding="utf-8") as fh:
+            return json.load(fh)
     if sys.stdin.isatty():
         raise ValidationError("Input required: provide --input <file> or JSON via stdin")
     return json.load(sys.stdin)
 
 
-def _cmd_consensus(args: argparse.Namespace) -> None:
+def _store_reliability(db: str, payload: Dict[str, Any]) -> Dict[str, Dict[str, float]]:
+    """Every signal's source looked up (decayed) in the store: cli.py:35-44."""
+    market_id = payload["marketId"]
+    table: Dict[str, Dict[str, float]] = {}
+    with SQLiteReliabilityStore(db) as store:
+        for signal in payload.get("signals", []):
+            sid = signal.get("sourceId")
+            if sid:
+                rec = store.get_reliability(sid, market_id, apply_decay=True)
+                table[sid] = {"reliability": rec.reliability, "confidence": rec.confidence}
+    return table
+
+
+def _consensus(args: argparse.Namespace, use_store: bool) -> None:
+    """Load -> validate -> (store lookup) -> compute -> print, shared by the legacy path
+    (use_store=False: the reference ignores --db there, cli.py:163-174) and ``consensus``."""
     try:
-        payload = _load_input(args.input)
+        payload = _read_payload(args.input)
         validate_input_payload(payload)
-        source_reliability = None
-        if args.db:
-            with SQLiteReliabilityStore(args.db) as store:
-                source_reliability = {}
-                for signal in payload.get("signals", []):
-                    source_id = signal.get("sourceId")
-                    if source_id:
-                        rec = store.get_reliability(source_id, payload["marketId"], apply_decay=True)
-                        source_reliability[source_id] = {"reliability": rec.reliability,
-                                                         "confidence": rec.confidence}
-        result = compute_consensus(payload["signals"], source_reliability)
+        reliability = _store_reliability(args.db, payload) if (use_store and args.db) else None
+        result = compute_consensus(payload["signals"], reliability)
         if args.dry_run:
             result["diagnostics"]["dryRun"] = True
-        print(json.dumps(result, indent=2))
+        _emit(result)
     except (json.JSONDecodeError, ValidationError) as exc:
-        print(f"Validation error: {exc}", file=sys.stderr)
-        raise SystemExit(1) from exc
+        _fail(f"Validation error: {exc}", exc)
 
 
-def _cmd_consensus_batch(args: argparse.Namespace) -> None:
-    """Build-defined: a JSONL file of payloads, one consensus launch for all.
-    Prints, per line, exactly what ``consensus`` prints for that payload alone (results on
-    stdout, ``Validation error: ...`` on stderr); exit 1 if any line failed.  Sources are
-    cold (no ``--db`` lookup), as in the legacy path."""
+def _consensus_batch(args: argparse.Namespace) -> None:
     from .jsonl import consensus_jsonl
 
     if args.input:
-        with open(args.input, "r", encoding="utf-8") as f:
-            lines = f.readlines()
+        with open(args.input, "r", encoding="utf-8") as fh:
+            lines = fh.readlines()
     else:
         lines = sys.stdin.readlines()
     failed = False
     for ok, text in consensus_jsonl(lines, dry_run=args.dry_run):
         print(text, file=sys.stdout if ok else sys.stderr)
-        failed |= not ok
+        failed = failed or not ok
     if failed:
         raise SystemExit(1)
 
 
-def _cmd_report_outcome(args: argparse.Namespace) -> None:
-    if not args.db:
-        print("Error: --db is required for report-outcome", file=sys.stderr)
-        raise SystemExit(1)
-    try:
-        with SQLiteReliabilityStore(args.db) as store:
-            result = store.update_reliability(source_id=args.source_id, market_id=args.market_id,
-                                              outcome_correct=args.correct, dry_run=args.dry_run)
-        output = {"sourceId": result.source_id, "marketId": result.market_id, "reliability": result.reliability,
-                  "confidence": result.confidence, "updatedAt": result.updated_at, "dryRun": args.dry_run}
-        print(json.dumps(output, indent=2))
-    except Exception as exc:  # noqa: BLE001  -- reference behaviour (cli.py:79-81)
-        print(f"Error: {exc}", file=sys.stderr)
-        raise SystemExit(1) from exc
+def _with_store(command: str, body: Callable[[argparse.Namespace, SQLiteReliabilityStore], Any]):
+    """report-outcome / list-sources: --db required, any failure -> 'Error: ...', rc 1."""
+
+    def run(args: argparse.Namespace) -> None:
+        if not args.db:
+            _fail(f"Error: --db is required for {command}")
+        try:
+            with SQLiteReliabilityStore(args.db) as store:
+                out = body(args, store)
+            _emit(out)
+        except Exception as exc:  # noqa: BLE001 -- the reference catches everything (cli.py:79-81)
+            _fail(f"Error: {exc}", exc)
+
+    return run
 
 
-def _cmd_list_sources(args: argparse.Namespace) -> None:
-    if not args.db:
-        print("Error: --db is required for list-sources", file=sys.stderr)
-        raise SystemExit(1)
-    try:
-        with SQLiteReliabilityStore(args.db) as store:
-            sources = store.list_sources(market_id=args.market_id)
-        output = {"sources": [{"sourceId": s.source_id, "marketId": s.market_id, "reliability": s.reliability,
-                               "confidence": s.confidence, "updatedAt": s.updated_at} for s in sources],
-                  "count": len(sources)}
-        print(json.dumps(output, indent=2))
-    except Exception as exc:  # noqa: BLE001
-        print(f"Error: {exc}", file=sys.stderr)
-        raise SystemExit(1) from exc
+def _record(rec, *, dry_run: Optional[bool] = None) -> Dict[str, Any]:
+    d = {"sourceId": rec.source_id, "marketId": rec.market_id, "reliability": rec.reliability,
+         "confidence": rec.confidence, "updatedAt": rec.updated_at}
+    if dry_run is not None:
+        d["dryRun"] = dry_run
+    return d
 
 
-def main() -> None:
+def _report_outcome(args, store):
+    rec = store.update_reliability(source_id=args.source_id, market_id=args.market_id,
+                                   outcome_correct=args.correct, dry_run=args.dry_run)
+    return _record(rec, dry_run=args.dry_run)
+
+
+def _list_sources(args, store):
+    rows = store.list_sources(market_id=args.market_id)
+    return {"sources": [_record(r) for r in rows], "count": len(rows)}
+
+
+Arg = Tuple[Tuple[str, ...], Dict[str, Any]]
+
+GLOBAL_ARGS: List[Arg] = [
+    (("--db",), dict(type=str, help="Path to SQLite database file (default: in-memory)")),
+    (("--dry-run",), dict(action="store_true", help="Compute without persisting changes (zero DB writes)")),
+    (("--input",), dict(type=str, help="Path to JSON input file (for consensus command)")),
+]
+
+# name -> (help, arguments, handler)
+COMMANDS: Dict[str, Tuple[str, List[Arg], Callable[[argparse.Namespace], None]]] = {
+    "consensus": ("Compute consensus from signals",
+                  [(("--input",), dict(help="Path to JSON input file"))],
+                  lambda a: _consensus(a, use_store=True)),
+    "consensus-batch": ("Compute consensus for a JSONL batch of payloads",
+                        [(("--input",), dict(help="Path to JSONL input file (one payload per line)"))],
+                        _consensus_batch),
+    "report-outcome": ("Report outcome and update reliability",
+                       [(("--source-id",), dict(required=True, help="Source identifier")),
+                        (("--market-id",), dict(required=True, help="Market identifier")),
+                        (("--correct",), dict(action="store_true", help="Outcome was correct"))],
+                       _with_store("report-outcome", _report_outcome)),
+    "list-sources": ("List sources with reliability data",
+                     [(("--market-id",), dict(help="Filter by market ID"))],
+                     _with_store("list-sources", _list_sources)),
+}
+
+
+def _add(parser: argparse.ArgumentParser, specs: Iterable[Arg]) -> None:
+    for flags, kw in specs:
+        parser.add_argument(*flags, **kw)
+
+
+def build_parser() -> argparse.ArgumentParser:
     parser = argparse.ArgumentParser(prog="bayesian-engine",
                                      description="Bayesian-weighted consensus engine with reliability tracking")
-    parser.add_argument("--db", type=str, help="Path to SQLite database file (default: in-memory)")
-    parser.add_argument("--dry-run", action="store_true", help="Compute without persisting changes (zero DB writes)")
-    parser.add_argument("--input", type=str, help="Path to JSON input file (for consensus command)")
-    subparsers = parser.add_subparsers(dest="command", help="Available commands")
-    consensus_parser = subparsers.add_parser("consensus", help="Compute consensus from signals")
-    consensus_parser.add_argument("--input", help="Path to JSON input file")
-    consensus_parser.set_defaults(func=_cmd_consensus)
-    batch_parser = subparsers.add_parser("consensus-batch", help="Compute consensus for a JSONL batch of payloads")
-    batch_parser.add_argument("--input", help="Path to JSONL input file (one payload per line)")
-    batch_parser.set_defaults(func=_cmd_consensus_batch)
-    outcome_parser = subparsers.add_parser("report-outcome", help="Report outcome and update reliability")
-    outcome_parser.add_argument("--source-id", required=True, help="Source identifier")
-    outcome_parser.add_argument("--market-id", required=True, help="Market identifier")
-    outcome_parser.add_argument("--correct", action="store_true", help="Outcome was correct")
-    outcome_parser.set_defaults(func=_cmd_report_outcome)
-    list_parser = subparsers.add_parser("list-sources", help="List sources with reliability data")
-    list_parser.add_argument("--market-id", help="Filter by market ID")
-    list_parser.set_defaults(func=_cmd_list_sources)
-    args = parser.parse_args()
+    _add(parser, GLOBAL_ARGS)
+    sub = parser.add_subparsers(dest="command", help="Available commands")
+    for name, (help_text, specs, handler) in COMMANDS.items():
+        p = sub.add_parser(name, help=help_text)
+        _add(p, specs)
+        p.set_defaults(func=handler)
+    return parser
+
+
+def main(argv: Optional[List[str]] = None) -> None:
+    args = build_parser().parse_args(argv)
     if args.command is None:
-        _cmd_consensus_legacy(args)
+        _consensus(args, use_store=False)  # legacy path (cli.py:156-158)
     else:
         args.func(args)
-
-
-def _cmd_consensus_legacy(args: argparse.Namespace) -> None:
-    try:
-        payload = _load_input(args.input)
-        validate_input_payload(payload)
-        result = compute_consensus(payload["signals"])
-        if args.dry_run:
-            result["diagnostics"]["dryRun"] = True
-        print(json.dumps(result, indent=2))
-    except (json.JSONDecodeError, ValidationError) as exc:
-        print(f"Validation error: {exc}", file=sys.stderr)
-        raise SystemExit(1) from exc
 
 
 if __name__ == "__main__":

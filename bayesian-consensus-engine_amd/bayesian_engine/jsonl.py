@@ -182,9 +182,11 @@ def parse_batch(lines: Iterable[str]) -> Tuple[List[Any], List[Optional[str]], L
         try:
             payload = json.loads(line)
             p, te = check_structure(payload)
-        except (json.JSONDecodeError, ValidationError) as exc:
+        except (json.JSONDecodeError, ValidationError, TypeError) as exc:
+            # a JSON scalar (5, null, true) is not a payload: the reference's single-payload
+            # CLI dies on it with this TypeError; the batch reports it for that line only
             payloads.append(None)
-            errors.append(f"Validation error: {exc}")
+            errors.append(f"TypeError: {exc}" if isinstance(exc, TypeError) else f"Validation error: {exc}")
             probs.append([])
             type_errors.append(None)
             continue

@@ -71,12 +71,25 @@ class DeterministicTieBreaker:
             )
         return self.resolve_many([agents])[0]
 
+    def _group_keys(self, agents, fkeys, g_of) -> list:
+        """The reference's dict keys, round(first member's prediction, precision): the
+        kernel's float key, or -- when that first member's prediction is an int -- the
+        same value as an int (round(int, n) is an int; tiebreak.py:54)."""
+        keys = [float(k) for k in fkeys]
+        seen = set()
+        for agent, g in zip(agents, g_of):
+            g = int(g)
+            if g in seen:
+                continue
+            seen.add(g)
+            if isinstance(agent.prediction, int):
+                keys[g] = round(agent.prediction, self.precision)
+        return keys
+
     def resolve_many(self, markets: Sequence[Sequence[AgentSignal]]) -> List[Tuple[float, TieBreakDiagnostics]]:
         """resolve() for every market in one kernel launch (empty markets raise)."""
         if any(len(m) == 0 for m in markets):
             raise ValueError("Cannot resolve tie with empty agent list")
-        if not (0 <= int(self.precision) <= 15):
-            raise NotImplementedError("the GPU tie-breaker supports precision 0..15")
         N.require_gpu()
         dev = N.device()
         lens = np.array([len(m) for m in markets], np.int64)
@@ -89,7 +102,7 @@ class DeterministicTieBreaker:
         r = batch.tiebreak(T(off), T(cols[:, 0]), T(cols[:, 1]), T(cols[:, 2]), T(cols[:, 3]),
                            precision=int(self.precision), offsets_host=off)
         host = {k: getattr(r, k).cpu().numpy() for k in ("winner", "label", "n_groups", "variance", "g_key",
-                                                          "g_count", "g_density", "g_avgconf", "g_maxrel")}
+                                                          "g_count", "g_density", "g_avgconf", "g_maxrel", "g_of")}
         out = []
         for m, agents in enumerate(markets):
             if len(agents) == 1:
@@ -97,15 +110,17 @@ class DeterministicTieBreaker:
                 continue
             a = int(off[m])
             ng = int(host["n_groups"][m])
+            keys = self._group_keys(agents, host["g_key"][a:a + ng], host["g_of"][a:a + len(agents)])
             groups = {}
-            for g in range(a, a + ng):
-                groups[float(host["g_key"][g])] = {
+            for j, g in enumerate(range(a, a + ng)):
+                groups[keys[j]] = {
                     "count": int(host["g_count"][g]),
                     "weight_density": round(float(host["g_density"][g]), 4),
                     "avg_confidence": round(float(host["g_avgconf"][g]), 4),
                     "max_reliability": round(float(host["g_maxrel"][g]), 4),
                 }
-            winner = float(host["winner"][m])
+            wf = float(host["winner"][m])
+            winner = next((k for j, k in enumerate(keys) if host["g_key"][a + j] == wf or (wf != wf and k != k)), wf)
             out.append((winner, TieBreakDiagnostics(
                 method="prioritized_weight_density",
                 groups=groups,

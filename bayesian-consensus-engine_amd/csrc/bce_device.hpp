@@ -90,7 +90,7 @@ __device__ __forceinline__ unsigned bitonic_sort_seg(unsigned key, int l) {
 __device__ __forceinline__ double py_min(double a, double b) { return (b < a) ? b : a; }
 __device__ __forceinline__ double py_max(double a, double b) { return (b > a) ? b : a; }
 
-// CPython round(x, nd) for 0 <= nd <= 15: the correctly rounded decimal (half-even on
+// CPython round(x, nd) for 0 <= nd <= 22 (10^nd exact): the correctly rounded decimal (half-even on
 // the exact binary value) converted back to the nearest double.  x*10^nd is split
 // exactly (hi + lo via the fma error term), the nearest integer k of hi+lo is found with
 // ties-to-even, and k/10^nd is one IEEE division (k < 2^53 is exact) == strtod of the
@@ -112,6 +112,28 @@ __device__ __forceinline__ double py_round_nd(double x, double scale, double thr
   double r = k / scale;
   if (r == 0.0) r = copysign(0.0, x);
   return r;
+}
+
+// CPython round(x, nd) for -15 <= nd < 0 (P = 10^-nd, exact): the correctly rounded
+// (half-even) multiple of P, converted back with one rounding.  k0 = rint(x / P) is at most
+// one off; the remainder r = x - k0 * P is exact under the FMA (|r| <= |x| with x's
+// granularity, or an integer < 2^53 for integer-valued x), so |r| against P / 2 decides k
+// exactly.  For |x| >= 2^53 * P the nearest multiple is within ulp(x) / 4: the answer is x.
+__device__ __forceinline__ double py_round_neg(double x, double P) {
+  if (!(fabs(x) < 9007199254740992.0 * P)) return x;  // also NaN / inf
+  const double k0 = rint(x / P);
+  const double r = __builtin_fma(-k0, P, x);  // exact
+  const double h = 0.5 * P;
+  double k = k0;
+  if (fabs(r) > h) {
+    k = k0 + (r > 0.0 ? 1.0 : -1.0);
+  } else if (fabs(r) == h) {
+    const double k1 = k0 + (r > 0.0 ? 1.0 : -1.0);
+    k = (fmod(k0, 2.0) == 0.0) ? k0 : k1;
+  }
+  double out = k * P;
+  if (out == 0.0) out = copysign(0.0, x);
+  return out;
 }
 
 __device__ __forceinline__ double py_round6(double x) {

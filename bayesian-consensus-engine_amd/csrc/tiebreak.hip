@@ -31,9 +31,22 @@ struct TbArgs {
   double* g_density;
   double* g_avgconf;
   double* g_maxrel;
-  double rscale;   // 10^ndigits
+  int32_t* g_of;   // nullable: per agent, the ordinal of its group (dict insertion order)
+  double rscale;   // 10^ndigits (ndigits >= 0) or 10^-ndigits (ndigits < 0)
   double rthresh;  // see py_round_nd
+  int rmode;       // 0: py_round_nd, 1: py_round_neg, 2: identity (nd > 323), 3: signed zero (nd < -308)
 };
+
+// round(prediction, precision) of tiebreak.py:54 for every precision CPython accepts that
+// this build restates exactly (see tb_round_mode on the host)
+__device__ __forceinline__ double tb_round(double x, const TbArgs& a) {
+  switch (a.rmode) {
+    case 0: return py_round_nd(x, a.rscale, a.rthresh);
+    case 1: return py_round_neg(x, a.rscale);
+    case 2: return x;
+    default: return (x != x || fabs(x) == __builtin_inf()) ? x : copysign(0.0, x);
+  }
+}
 
 __device__ __forceinline__ bool key_eq(double a, double b) { return a == b; }  // -0.0 == 0.0
 
@@ -86,10 +99,11 @@ __global__ __launch_bounds__(256) void tiebreak_wave_kernel(TbArgs a, const int3
         if (a.g_density) a.g_density[off] = w;
         if (a.g_avgconf) a.g_avgconf[off] = c;
         if (a.g_maxrel) a.g_maxrel[off] = r;
+        if (a.g_of) a.g_of[off] = 0;
       }
       continue;
     }
-    const double key = py_round_nd(p, a.rscale, a.rthresh);
+    const double key = tb_round(p, a);
     // leader = first index with an equal key (dict insertion order)
     int leader = lane;
     for (int j = 0; j < n; ++j) {
@@ -143,6 +157,7 @@ __global__ __launch_bounds__(256) void tiebreak_wave_kernel(TbArgs a, const int3
       a.n_groups[m] = ng;
       a.variance[m] = vs / (double)n;
     }
+    if (a.g_of && v) a.g_of[off + lane] = __popcll(lm & ((leader == 0) ? 0ull : (~0ull >> (64 - leader))));
     if (is_leader) {
       const int64_t g = off + __popcll(lm & below);
       if (a.g_key) a.g_key[g] = key;
@@ -154,18 +169,26 @@ __global__ __launch_bounds__(256) void tiebreak_wave_kernel(TbArgs a, const int3
   }
 }
 
-// 64 < n <= 4096: one workgroup per market.  (rounded key, index) pairs are bitonic-
-// sorted in LDS, so every group is a run whose members appear in input order; the run
-// head owns the group (its first member is the dict-insertion leader).
+// n > 64: one workgroup per market.  (rounded key, index) pairs are bitonic-sorted in
+// LDS (n <= 4096) or in the workgroup's slice of a global scratch buffer (any length:
+// the reference has no limit), so every group is a run whose members appear in input
+// order; the run head owns the group (its first member is the dict-insertion leader).
 constexpr int kTbThreads = 256;
 constexpr int kTbMax = 4096;
 constexpr unsigned long long kNanKey = 0xFFFFFFFFFFFFF000ull;
 
+template <bool IN_LDS>
 __global__ __launch_bounds__(kTbThreads) void tiebreak_block_kernel(TbArgs a, const int32_t* list,
-                                                                    int64_t n_list) {
-  __shared__ unsigned long long sk[kTbMax];  // ordered key bits
-  __shared__ int32_t sIdx[kTbMax];           // original index
-  __shared__ int32_t sRank[kTbMax];          // leader flag, then first-seen rank
+                                                                    int64_t n_list, void* scratch,
+                                                                    int64_t stride) {
+  __shared__ unsigned long long lk[IN_LDS ? kTbMax : 1];
+  __shared__ int32_t lIdx[IN_LDS ? kTbMax : 1];
+  __shared__ int32_t lRank[IN_LDS ? kTbMax : 1];
+  // global slice: keys (8 B), indices, ranks (4 B each) of `stride` entries per workgroup
+  unsigned long long* const sk =
+      IN_LDS ? lk : reinterpret_cast<unsigned long long*>(scratch) + (int64_t)blockIdx.x * 2 * stride;
+  int32_t* const sIdx = IN_LDS ? lIdx : reinterpret_cast<int32_t*>(sk + stride);
+  int32_t* const sRank = IN_LDS ? lRank : sIdx + stride;
   __shared__ double cD[kTbThreads], cM[kTbThreads], cK[kTbThreads];
   __shared__ int32_t cI[kTbThreads];
   __shared__ int32_t sW[kTbThreads / 64 + 1];
@@ -184,7 +207,7 @@ __global__ __launch_bounds__(kTbThreads) void tiebreak_block_kernel(TbArgs a, co
     for (int i = tid; i < P; i += kTbThreads) {
       unsigned long long kk = ~0ull;
       if (i < n) {
-        double k = py_round_nd(a.pred[off + i], a.rscale, a.rthresh);
+        double k = tb_round(a.pred[off + i], a);
         if (k == 0.0) k = 0.0;  // -0.0 and 0.0 share one dict slot
         unsigned long long b = (unsigned long long)__double_as_longlong(k);
         kk = (b >> 63) ? ~b : (b | 0x8000000000000000ull);  // total order on doubles
@@ -249,6 +272,7 @@ __global__ __launch_bounds__(kTbThreads) void tiebreak_block_kernel(TbArgs a, co
       for (int q = t; q < n; ++q) {
         if (q > t && (sk[q] == kNanKey || sk[q] != sk[t])) break;
         const int iq = sIdx[q];
+        if (a.g_of) a.g_of[off + iq] = sRank[i0];
         tot += a.weight[off + iq];
         cs += a.conf[off + iq];
         ++cnt;
@@ -257,7 +281,7 @@ __global__ __launch_bounds__(kTbThreads) void tiebreak_block_kernel(TbArgs a, co
         if (sk[t] == kNanKey) break;
       }
       const double dens = tot / (double)cnt;
-      const double key = py_round_nd(a.pred[off + i0], a.rscale, a.rthresh);
+      const double key = tb_round(a.pred[off + i0], a);
       const int64_t g = off + sRank[i0];
       if (a.g_key) a.g_key[g] = key;
       if (a.g_count) a.g_count[g] = cnt;
@@ -324,7 +348,7 @@ __global__ __launch_bounds__(kTbThreads) void tiebreak_block_kernel(TbArgs a, co
 
 using namespace bce;
 
-static double round_scale(int nd) {
+static double pow10_exact(int nd) {
   double s = 1.0;
   for (int i = 0; i < nd; ++i) s *= 10.0;  // exact for nd <= 22
   return s;
@@ -335,13 +359,32 @@ static double round_thresh(int nd) {
   const int E = (int)floor(52.0 - y) + 1;
   return ldexp(1.0, E);
 }
+// CPython float.__round__(x, nd): nd > 323 returns x, nd < -308 returns 0.0 * x
+// (NDIGITS_MAX / NDIGITS_MIN of floatobject.c); in between the correctly rounded decimal.
+// Restated exactly here for -15 <= nd <= 22 (10^|nd| exact, remainders exact).
+static int tb_round_mode(int nd, double* scale, double* thresh) {
+  *scale = 1.0;
+  *thresh = 0.0;
+  if (nd > 323) return 2;
+  if (nd < -308) return 3;
+  if (nd >= 0 && nd <= 22) {
+    *scale = pow10_exact(nd);
+    *thresh = round_thresh(nd);
+    return 0;
+  }
+  if (nd < 0 && nd >= -15) {
+    *scale = pow10_exact(-nd);
+    return 1;
+  }
+  return -1;
+}
 
 extern "C" int bce_tiebreak_csr(const int64_t* offsets, int64_t n_markets, const int32_t* market_list,
                                 int64_t n_list, const double* pred, const double* conf,
                                 const double* weight, const double* rel, int32_t max_len,
                                 int32_t ndigits, double* winner, int32_t* label, int32_t* n_groups,
                                 double* variance, double* g_key, int32_t* g_count, double* g_density,
-                                double* g_avgconf, double* g_maxrel, void* stream) {
+                                double* g_avgconf, double* g_maxrel, int32_t* g_of, void* stream) {
   BCE_REQUIRE(n_markets >= 0, "tiebreak: n_markets < 0");
   const int64_t nl = market_list ? n_list : n_markets;
   if (nl == 0) return BCE_OK;
@@ -349,9 +392,15 @@ extern "C" int bce_tiebreak_csr(const int64_t* offsets, int64_t n_markets, const
               "tiebreak: NULL argument");
   BCE_REQUIRE(max_len > 0 && max_len <= 64,
               "tiebreak: max_len must be in 1..64 (longer markets: bce_tiebreak_csr_long)");
-  BCE_REQUIRE(ndigits >= 0 && ndigits <= 15, "tiebreak: ndigits must be in [0, 15]");
+  double rs = 1.0, rt = 0.0;
+  const int rmode = tb_round_mode(ndigits, &rs, &rt);
+  if (rmode < 0) {
+    set_error("tiebreak: precision %d is outside what this build restates exactly "
+              "(-15..22, below -308, above 323)", ndigits);
+    return BCE_EUNSUPPORTED;
+  }
   TbArgs a{offsets, n_markets, pred, conf, weight, rel, winner, label, n_groups, variance,
-           g_key, g_count, g_density, g_avgconf, g_maxrel, round_scale(ndigits), round_thresh(ndigits)};
+           g_key, g_count, g_density, g_avgconf, g_maxrel, g_of, rs, rt, rmode};
   int64_t blocks = (nl + 3) / 4;
   const int64_t cap = (int64_t)cu_count() * 16;
   if (blocks > cap) blocks = cap;
@@ -363,21 +412,44 @@ extern "C" int bce_tiebreak_csr(const int64_t* offsets, int64_t n_markets, const
 extern "C" int bce_tiebreak_csr_long(const int64_t* offsets, int64_t n_markets, const int32_t* list,
                                      int64_t n_list, int32_t ndigits, const double* pred,
                                      const double* conf, const double* weight, const double* rel,
-                                     double* winner, int32_t* label, int32_t* n_groups,
-                                     double* variance, double* g_key, int32_t* g_count,
-                                     double* g_density, double* g_avgconf, double* g_maxrel,
-                                     void* stream) {
+                                     int64_t max_len, double* winner, int32_t* label,
+                                     int32_t* n_groups, double* variance, double* g_key,
+                                     int32_t* g_count, double* g_density, double* g_avgconf,
+                                     double* g_maxrel, int32_t* g_of, void* stream) {
   BCE_REQUIRE(n_list >= 0 && (n_list == 0 || list), "tiebreak_long: bad list");
   if (n_list == 0) return BCE_OK;
   BCE_REQUIRE(offsets && pred && conf && weight && rel && winner && label && n_groups && variance,
               "tiebreak_long: NULL argument");
-  BCE_REQUIRE(ndigits >= 0 && ndigits <= 15, "tiebreak: ndigits must be in [0, 15]");
+  BCE_REQUIRE(max_len > 0 && max_len < (1ll << 31), "tiebreak_long: max_len out of range");
+  double rs = 1.0, rt = 0.0;
+  const int rmode = tb_round_mode(ndigits, &rs, &rt);
+  if (rmode < 0) {
+    set_error("tiebreak: precision %d is outside what this build restates exactly "
+              "(-15..22, below -308, above 323)", ndigits);
+    return BCE_EUNSUPPORTED;
+  }
   TbArgs a{offsets, n_markets, pred, conf, weight, rel, winner, label, n_groups, variance,
-           g_key, g_count, g_density, g_avgconf, g_maxrel, round_scale(ndigits), round_thresh(ndigits)};
+           g_key, g_count, g_density, g_avgconf, g_maxrel, g_of, rs, rt, rmode};
+  hipStream_t st = as_stream(stream);
+  if (max_len <= kTbMax) {
+    int64_t blocks = n_list;
+    const int64_t cap = (int64_t)cu_count() * 2;
+    if (blocks > cap) blocks = cap;
+    hipLaunchKernelGGL(tiebreak_block_kernel<true>, dim3((int)blocks), dim3(kTbThreads), 0, st, a, list,
+                       n_list, nullptr, (int64_t)0);
+    return check_launch("tiebreak_block_kernel<lds>");
+  }
+  // any longer market: sort in a global scratch slice per workgroup (16 B per entry)
+  int64_t P = 1;
+  while (P < max_len) P <<= 1;
   int64_t blocks = n_list;
-  const int64_t cap = (int64_t)cu_count() * 2;
+  const int64_t cap = (int64_t)cu_count();
   if (blocks > cap) blocks = cap;
-  hipLaunchKernelGGL(tiebreak_block_kernel, dim3((int)blocks), dim3(kTbThreads), 0,
-                     as_stream(stream), a, list, n_list);
-  return check_launch("tiebreak_block_kernel");
+  void* scratch = nullptr;
+  BCE_HIP(hipMallocAsync(&scratch, (size_t)(blocks * 16 * P), st));
+  hipLaunchKernelGGL(tiebreak_block_kernel<false>, dim3((int)blocks), dim3(kTbThreads), 0, st, a, list, n_list,
+                     scratch, P);
+  const int rc = check_launch("tiebreak_block_kernel<global>");
+  BCE_HIP(hipFreeAsync(scratch, st));
+  return rc;
 }

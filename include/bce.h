@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define BCE_ABI_VERSION 1
+#define BCE_ABI_VERSION 2
 
 enum bce_status {
     BCE_OK = 0,
@@ -199,22 +199,28 @@ int bce_namespace_resolve(int64_t n, const double* rel0, const double* conf0, co
  * label (enum bce_tb_label; -1 for an empty market = the reference's ValueError),
  * n_groups, variance (unrounded population variance of conf, tiebreak.py:104-106).
  * Per group, first-seen order, at CSR offsets: key, count, weight density, avg conf,
- * max reliability (tiebreak.py:58-71).  Group pointers may be NULL.  ndigits is the
- * DeterministicTieBreaker precision (0..15).
+ * max reliability (tiebreak.py:58-71); per signal (nullable g_of) the ordinal of its group,
+ * which lets a caller rebuild the reference's dict keys with their Python types (an int
+ * prediction keys its group with an int).  Group pointers may be NULL.  ndigits is the
+ * DeterministicTieBreaker precision: CPython round(x, ndigits) restated exactly for
+ * -15 <= ndigits <= 22, ndigits < -308 (signed zero) and ndigits > 323 (x itself); other
+ * values return BCE_EUNSUPPORTED.
  * bce_tiebreak_csr: markets market_list[0..n_list) (NULL = all), every length <= max_len
- * <= 64 (one wave per market).  bce_tiebreak_csr_long: 64 < n <= 4096 (one workgroup per
- * market, LDS-sorted). */
+ * <= 64 (one wave per market).  bce_tiebreak_csr_long: markets of any length >= 1, max_len
+ * >= every listed market's length (one workgroup per market; sorted in LDS up to 4096
+ * agents, beyond that in a global scratch slice the library allocates on `stream`). */
 int bce_tiebreak_csr(const int64_t* offsets, int64_t n_markets, const int32_t* market_list,
                      int64_t n_list, const double* pred, const double* conf, const double* weight,
                      const double* rel, int32_t max_len, int32_t ndigits, double* winner,
                      int32_t* label, int32_t* n_groups, double* variance, double* g_key,
                      int32_t* g_count, double* g_density, double* g_avgconf, double* g_maxrel,
-                     void* stream);
+                     int32_t* g_of, void* stream);
 int bce_tiebreak_csr_long(const int64_t* offsets, int64_t n_markets, const int32_t* list,
                           int64_t n_list, int32_t ndigits, const double* pred, const double* conf,
-                          const double* weight, const double* rel, double* winner, int32_t* label,
-                          int32_t* n_groups, double* variance, double* g_key, int32_t* g_count,
-                          double* g_density, double* g_avgconf, double* g_maxrel, void* stream);
+                          const double* weight, const double* rel, int64_t max_len, double* winner,
+                          int32_t* label, int32_t* n_groups, double* variance, double* g_key,
+                          int32_t* g_count, double* g_density, double* g_avgconf, double* g_maxrel,
+                          int32_t* g_of, void* stream);
 
 /* ---- agreement statistics: CrossMarketAggregator.summarize_sources counts -----------
  * (market.py:279-304).  outcome[m]: -1 skip (unresolved), 0 false, 1 true.

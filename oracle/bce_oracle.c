@@ -186,6 +186,7 @@ typedef struct {
 /* tiebreak.py:73-152 */
 int orc_tiebreak_csr(const int64_t* offsets, int64_t n_markets, const double* pred,
                      const double* conf, const double* weight, const double* rel,
+                     const double* keys, /* nullable: round(pred, 6); else the caller's round() */
                      double* winner, int32_t* label, int32_t* n_groups, double* variance,
                      double* g_key, int32_t* g_count, double* g_total, double* g_avgconf,
                      double* g_maxrel) {
@@ -210,7 +211,7 @@ int orc_tiebreak_csr(const int64_t* offsets, int64_t n_markets, const double* pr
         }
         int64_t ng = 0;
         for (int64_t i = 0; i < n; ++i) { /* _group_by_prediction: dict in first-seen order */
-            const double k = orc_round_decimal(pred[a + i], 6);
+            const double k = keys ? keys[a + i] : orc_round_decimal(pred[a + i], 6);
             int64_t j = 0;
             while (j < ng && !(g[j].key == k)) ++j;
             if (j == ng) {

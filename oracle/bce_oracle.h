@@ -69,6 +69,7 @@ double orc_round_decimal(double x, int ndigits);
  * key, count, total_weight, avg_conf, max_rel.  Empty market: n_groups = -1. */
 int orc_tiebreak_csr(const int64_t* offsets, int64_t n_markets, const double* pred,
                      const double* conf, const double* weight, const double* rel,
+                     const double* keys,
                      double* winner, int32_t* label, int32_t* n_groups, double* variance,
                      double* g_key, int32_t* g_count, double* g_total, double* g_avgconf,
                      double* g_maxrel);

@@ -118,14 +118,18 @@ def agreement_stats(offsets, sid, prob, outcome, n_sources):
     return correct, total
 
 
-def tiebreak_csr(offsets, pred, conf, weight, rel):
+def tiebreak_csr(offsets, pred, conf, weight, rel, keys=None):
+    """tiebreak.py:73-152 per market; group keys round(pred, 6), or ``keys`` (the caller's
+    own round(pred, precision) for other precisions)."""
     offsets = np.ascontiguousarray(offsets, np.int64)
     pred, conf, weight, rel = (np.ascontiguousarray(x, np.float64) for x in (pred, conf, weight, rel))
+    keys = None if keys is None else np.ascontiguousarray(keys, np.float64)
     M, N = len(offsets) - 1, len(pred)
     out = dict(winner=np.zeros(M), label=np.zeros(M, np.int32), n_groups=np.zeros(M, np.int32),
                variance=np.zeros(M), g_key=np.zeros(N), g_count=np.zeros(N, np.int32),
                g_total=np.zeros(N), g_avgconf=np.zeros(N), g_maxrel=np.zeros(N))
     rc = lib().orc_tiebreak_csr(_p(offsets), C.c_int64(M), _p(pred), _p(conf), _p(weight), _p(rel),
+                                _p(keys) if keys is not None else C.c_void_p(0),
                                 *[_p(out[k]) for k in ("winner", "label", "n_groups", "variance", "g_key",
                                                         "g_count", "g_total", "g_avgconf", "g_maxrel")])
     if rc != 0:

@@ -433,3 +433,88 @@ def test_cli_dry_run_and_db_reliability():
         p = _cli(["--db", db, "consensus"], stdin=json.dumps(payload))
         w = {x["sourceId"]: x["weight"] for x in json.loads(p.stdout)["sourceWeights"]}
         assert w["agent-a"] > w["agent-b"]
+
+
+def _tb_inputs(lens, seed):
+    rng = np.random.default_rng(seed)
+    off = np.zeros(len(lens) + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    n = int(off[-1])
+    kind = rng.integers(0, 6, n)
+    pred = rng.random(n)
+    pred = np.where(kind == 1, rng.integers(0, 9, n) / 8.0, pred)                        # exact binary grid
+    pred = np.where(kind == 2, (rng.integers(-2000, 2000, n) + 0.5) * 10.0 ** rng.integers(-6, 4, n), pred)  # near-ties
+    pred = np.where(kind == 3, rng.normal(0, 1e9, n), pred)                              # large magnitudes
+    pred = np.where(kind == 4, rng.integers(-300, 300, n) * 50.0, pred)                  # multiples of 50
+    pred[rng.random(n) < 0.02] = -0.0
+    conf, weight, rel = rng.random(n), rng.choice([0.5, 1.0, 2.0], n), rng.choice([0.5, 0.9], n)
+    return off, pred, conf, weight, rel
+
+
+def _tb_check(r, exp, off):
+    assert np.array_equal(r.winner.cpu().numpy(), exp["winner"])
+    assert np.array_equal(r.label.cpu().numpy(), exp["label"])
+    assert np.array_equal(r.n_groups.cpu().numpy(), exp["n_groups"])
+    np.testing.assert_allclose(r.variance.cpu().numpy(), exp["variance"], rtol=1e-12)
+    gk, gc, gd, gm = (r.g_key.cpu().numpy(), r.g_count.cpu().numpy(), r.g_density.cpu().numpy(),
+                      r.g_maxrel.cpu().numpy())
+    for m in range(len(off) - 1):
+        a, g = int(off[m]), int(exp["n_groups"][m])
+        sl = slice(a, a + g)
+        assert np.array_equal(gk[sl], exp["g_key"][sl]), m
+        assert np.array_equal(gc[sl], exp["g_count"][sl]), m
+        assert np.array_equal(gd[sl], exp["g_total"][sl] / exp["g_count"][sl]), m
+        assert np.array_equal(gm[sl], exp["g_maxrel"][sl]), m
+
+
+@pytest.mark.parametrize("precision", [0, 2, 6, 10, 17, 22, -1, -2, -7, -15, 400, -400])
+def test_tiebreak_any_precision_vs_python_round(precision):
+    """Group keys are CPython round(pred, precision) (tiebreak.py:54) for any precision the
+    reference accepts that the build restates: the oracle groups by Python's own round()."""
+    import torch
+    from bayesian_engine import batch
+    from oracle import oracle as orc
+    lens = np.array([40, 64, 2, 100, 700, 3], np.int64)
+    off, pred, conf, weight, rel = _tb_inputs(lens, 100 + precision)
+    keys = np.array([round(float(x), precision) for x in pred], np.float64)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    r = batch.tiebreak(T(off), T(pred), T(conf), T(weight), T(rel), precision=precision, offsets_host=off)
+    exp = orc.tiebreak_csr(off, pred, conf, weight, rel, keys=keys)
+    _tb_check(r, exp, off)
+
+
+def test_tiebreak_unsupported_precision_raises():
+    import torch
+    from bayesian_engine import _native as N, batch
+    off, pred, conf, weight, rel = _tb_inputs(np.array([5, 6], np.int64), 3)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    with pytest.raises(N.BCEError, match="precision 30"):
+        batch.tiebreak(T(off), T(pred), T(conf), T(weight), T(rel), precision=30, offsets_host=off)
+
+
+def test_tiebreak_markets_longer_than_4096_vs_oracle():
+    """The reference has no length limit: 5000 and 12000 agents sort in a global scratch
+    slice (4097 and shorter markets in the same batch)."""
+    import torch
+    from bayesian_engine import batch
+    from oracle import oracle as orc
+    lens = np.array([5000, 70, 12000, 4097, 1, 64], np.int64)
+    off, pred, conf, weight, rel = _tb_inputs(lens, 77)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    for precision in (6, 2, 0, 10):
+        keys = np.array([round(float(x), precision) for x in pred], np.float64)
+        r = batch.tiebreak(T(off), T(pred), T(conf), T(weight), T(rel), precision=precision, offsets_host=off)
+        exp = orc.tiebreak_csr(off, pred, conf, weight, rel, keys=keys)
+        _tb_check(r, exp, off)
+
+
+def test_tiebreak_int_predictions_keep_int_keys():
+    """round(int, 6) is an int: the reference's group keys and winner are ints then."""
+    from bayesian_engine.tiebreak import AgentSignal, DeterministicTieBreaker
+    agents = [AgentSignal("a", 1, 0.9, 2.0, 0.9), AgentSignal("b", 0, 0.5, 1.0, 0.5),
+              AgentSignal("c", 1.0, 0.7, 1.0, 0.6), AgentSignal("d", 0.25, 0.5, 1.0, 0.4)]
+    pred, diag = DeterministicTieBreaker().resolve(agents)
+    assert pred == 1 and type(pred) is int
+    assert [type(k) for k in diag.groups] == [int, int, float]
+    pred2, diag2 = DeterministicTieBreaker(precision=-1).resolve(agents)
+    assert list(diag2.groups) == [0] and type(pred2) is int  # every prediction rounds to the tens: 0

@@ -67,3 +67,17 @@ def test_iso_to_us_many_matches_per_value():
     good = [v for v in vals if isinstance(v, str) and v.endswith("+00:00") and "02-30" not in v and "-13-" not in v]
     assert iso_to_us_many(good).tolist() == [iso_to_us(v) for v in good]
     assert iso_to_us_many([]).tolist() == []
+
+
+def test_parse_batch_scalar_lines_do_not_abort_the_batch():
+    """A JSON scalar line (5, null, true) is reported for that line only; the payloads
+    around it are still parsed (the reference's single CLI dies on it with this TypeError)."""
+    from bayesian_engine.jsonl import parse_batch
+    ok = json.dumps({"schemaVersion": "1.0.0", "marketId": "m", "signals": [{"sourceId": "a", "probability": 0.5}]})
+    payloads, errors, probs, _ = parse_batch([ok, "5", "null", "true", ok, '"text"'])
+    assert len(payloads) == 6
+    assert errors[0] is None and errors[4] is None and probs[4] == [0.5]
+    assert errors[1] == "TypeError: argument of type 'int' is not iterable"
+    assert errors[2] == "TypeError: argument of type 'NoneType' is not iterable"
+    assert errors[3] == "TypeError: argument of type 'bool' is not iterable"
+    assert errors[5] == "Validation error: schemaVersion is required"

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_device_count():
     lib = N.load_library()
-    assert lib.bce_abi_version() == 1
+    assert lib.bce_abi_version() == 2
     assert lib.bce_device_count() >= 0
 
 
