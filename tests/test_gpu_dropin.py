@@ -475,7 +475,7 @@ def test_tiebreak_any_precision_vs_python_round(precision):
     from bayesian_engine import batch
     from oracle import oracle as orc
     lens = np.array([40, 64, 2, 100, 700, 3], np.int64)
-    off, pred, conf, weight, rel = _tb_inputs(lens, 100 + precision)
+    off, pred, conf, weight, rel = _tb_inputs(lens, 1000 + precision)
     keys = np.array([round(float(x), precision) for x in pred], np.float64)
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
     r = batch.tiebreak(T(off), T(pred), T(conf), T(weight), T(rel), precision=precision, offsets_host=off)
