@@ -4,10 +4,9 @@ RCCL/xGMI (backend "nccl"; "gloo" for CPU tests).
 * Markets (configs 2/3) shard with ZERO communication: contiguous market ranges split at
   equal signal counts (prefix sum of the CSR offsets), source table replicated (e1).
 * Sources (config 4) shard by an owner hash; the only exchange is the per-source outcome
-  flags produced by market shards, combined with one all-reduce (e2).  Flags are combined
-  as a bitwise OR of (participates, correct) bits packed in uint8 -- expressed as a SUM
-  all-reduce over disjoint contributions (each (source, step) outcome is produced by
-  exactly one market shard), which RCCL implements natively.
+  flags produced by market shards, combined with one SUM all-reduce (e2) whose packing
+  keeps the participate and correct counts apart, so a source flagged by two shards in
+  one step is detected (:class:`FlagCollision`) instead of being silently mis-read.
 """
 from __future__ import annotations
 
@@ -38,17 +37,35 @@ def owner_of(source_ids: np.ndarray, world: int) -> np.ndarray:
     return (h % np.uint64(max(world, 1))).astype(np.int32)
 
 
+class FlagCollision(ValueError):
+    """Two market shards resolved an outcome for the same source in one step."""
+
+
 def combine_flags(local_flags: torch.Tensor) -> torch.Tensor:
-    """All-reduce per-source outcome flags produced by disjoint market shards (e2).
+    """All-reduce per-source outcome flags produced by market shards (e2).
 
     ``local_flags`` uint8[S]: bit0 participates, bit1 correct, zero where this rank's
-    markets produced no outcome.  Contributions are disjoint, so SUM == OR.
+    markets produced no outcome.  ``outcome_update`` applies at most one outcome per
+    source per call, as the reference's one ``update_reliability`` call per outcome does
+    (reliability.py:185-233), so two shards flagging one source in the same step is an
+    error, not something to OR together: the caller must split that step in two.
+
+    One SUM all-reduce over int32 words that keep the two bits apart (participation count
+    in the low 16 bits, correct count above), then a collision check on the counts.
+    Raises :class:`FlagCollision` naming the first colliding sources.
     """
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return local_flags
-    t = local_flags.to(torch.int32) if local_flags.device.type == "cpu" else local_flags
+    f = local_flags.to(torch.int32)
+    t = (f & 1) | (((f >> 1) & 1) << 16)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return t.to(torch.uint8)
+    part = t & 0xFFFF
+    bad = torch.nonzero(part > 1).flatten()
+    if bad.numel():
+        raise FlagCollision(f"{bad.numel()} source(s) got outcomes from more than one market shard in "
+                            f"one step (first: {bad[:8].tolist()}); split the step")
+    corr = (t >> 16) > 0
+    return (part | (corr.to(torch.int32) << 1)).to(torch.uint8)
 
 
 def allreduce_counts(correct: torch.Tensor, total: torch.Tensor) -> None:

@@ -57,12 +57,27 @@ def _worker(rank, world, port, q):
     mine = np.arange(S) % world == rank
     flags[torch.from_numpy(mine)] = 1
     comb = combine_flags(flags)
+    # correct bit from one shard only survives the combine; participation does too
+    f2 = torch.zeros(S, dtype=torch.uint8)
+    f2[torch.from_numpy(mine)] = 1 | (2 * (rank == 0))
+    comb2 = combine_flags(f2)
+    exp2 = torch.from_numpy(np.where(np.arange(S) % world == 0, 3, 1).astype(np.uint8))
+    # two shards flagging the same source in one step must not be read as "not participating"
+    from bayesian_engine.sharding import FlagCollision
+    f3 = torch.zeros(S, dtype=torch.uint8)
+    f3[7] = 1  # both ranks
+    try:
+        combine_flags(f3)
+        collided = False
+    except FlagCollision as exc:
+        collided = "[7]" in str(exc)
     if rank == 0:
         full = orc.consensus_csr(off, sid, prob, rel, conf, present)
         call, tall = orc.agreement_stats(off, sid, prob, outcome, S)
         q.put(dict(parts=parts, full_cons=full["consensus"].tolist(), full_nu=full["n_unique"].tolist(),
                    counts_ok=bool(np.array_equal(ct.numpy(), call) and np.array_equal(tt.numpy(), tall)),
-                   flags_ok=bool(torch.all(comb == 1).item())))
+                   flags_ok=bool(torch.all(comb == 1).item()) and bool(torch.equal(comb2, exp2)),
+                   collided=collided))
     dist.destroy_process_group()
 
 
@@ -85,3 +100,4 @@ def test_two_rank_gloo_sharding():
         nu += n
     assert cons == res["full_cons"] and nu == res["full_nu"]
     assert res["counts_ok"] and res["flags_ok"]
+    assert res["collided"], "a source flagged by two shards in one step must raise FlagCollision"
