@@ -12,8 +12,9 @@
 //                              market, rows staged per market by LDS-DMA.
 //  consensus_seg_kernel<64,8>  33 <= n <= 64: cooperative lane-per-signal phase (bitonic
 //                              sort, ballots) then lane-per-market ordered sums from LDS.
-//  consensus_wide_kernel<NW,R> 64 < n <= 4096: one workgroup per market, register bitonic
-//                              network over packed (sid, index) keys, exact chains.
+//  consensus_wide_kernel       64 < n <= 4096 (consensus_wide.hip): one workgroup per
+//                              market, register bitonic network over packed (sid, index)
+//                              keys, exact chains or BCE_MODE_FAST fixed-order trees.
 //  consensus_long_kernel<LDS>  fallback for long markets (LDS or global-scratch sort),
 //                              BCE_MODE_FAST fixed-order trees.
 // Every kernel sums in the reference's order in BCE_MODE_EXACT (bit-exact outputs).
@@ -40,9 +41,6 @@
 #endif
 #ifndef BCE_FLAT_WPB
 #define BCE_FLAT_WPB 2
-#endif
-#ifndef BCE_WIDE_HR
-#define BCE_WIDE_HR 4  // wide kernel: rounds of NT uniques computed into registers at once
 #endif
 
 namespace bce {
@@ -1471,446 +1469,6 @@ __global__ __launch_bounds__(kLongThreads) void consensus_long_kernel(ConsArgs a
   }
 }
 
-// ------------------------------------------------------------------------------------
-// wide markets (64 < n <= 4096), exact mode: one workgroup of NW waves per market
-// ------------------------------------------------------------------------------------
-// The P = 64*NW*R (sid, input index) keys of a market are packed into 32 bits
-// (sid << IB | index, IB = log2 P; needs n_sources <= 2^(32-IB)) and sorted in registers:
-// thread t holds sorted positions q = t*R + r.  Flip-form bitonic network: stages inside a
-// thread are min/max pairs, lane exchanges use DPP / ds_swizzle / bpermute plus one
-// compare and a lane-mask select, the few stages that cross waves go through LDS.
-// After the sort (core.py:103 sorted ids, ties in input order core.py:115):
-//   * probabilities are permuted into sorted order in LDS (row-xor swizzle, no padding),
-//   * run leaders (first position of each sid) get their compact unique index j from a
-//     workgroup prefix count,
-//   * per chunk of CH uniques, the compute waves sum each run in input order (core.py:116),
-//     gather relconf[sid] once (core.py:111-112), write usid/weight and stage
-//     (w, avg*w, c*w); wave 0 carries the three left-to-right chains (core.py:120,136,142)
-//     on lanes 0..2 one chunk behind (with NW > 1 it does nothing else),
-//   * w[j] is kept in the dead sorted-prob slots for normalizedWeight (core.py:151).
-// The next market's sid/prob are loaded into registers as soon as the current ones are
-// consumed, so their HBM latency hides behind the whole market.
-// LDS: region A = input-order probs, then leaders + the two chain chunk buffers;
-// region B = sort exchange rows, then the sorted probs, then w[j].
-constexpr int ilog2c(int x) { return x <= 1 ? 0 : 1 + ilog2c(x >> 1); }
-
-template <int NW, int R>
-struct WideCfg {
-  static constexpr int NT = 64 * NW;
-  static constexpr int P = NT * R;
-  static constexpr int IB = ilog2c(P);
-  static constexpr int XROW = R + 4;                        // padded exchange row (u32)
-  // region A (doubles): input-order probs [P], then leaders (u32 [P]) + round buffers
-  // [2][3][NT] + 64 doubles the chain's two-batches-ahead reads may touch
-  static constexpr int A_DBL = (P > P / 2 + 6 * NT + 64) ? P : P / 2 + 6 * NT + 64;
-  // region B (doubles): exchange rows, then sorted probs (linear in q) + 64 doubles the
-  // run sums' batch-ahead reads may touch
-  static constexpr int B_DBL = ((P > NT * XROW / 2) ? P : NT * XROW / 2) + 64;
-};
-
-// v from lane ^ M (whole wave) for the masks the flip-form sort uses.
-template <int M>
-__device__ __forceinline__ unsigned lane_xor(unsigned v) {
-  if constexpr (M == 1) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
-  else if constexpr (M == 2) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // 2,3,0,1
-  else if constexpr (M == 3) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x1B, 0xF, 0xF, false);  // 3,2,1,0
-  else if constexpr (M == 7) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false); // row_half_mirror
-  else if constexpr (M == 15) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false);  // row_mirror
-  else if constexpr (M < 32) return (unsigned)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (M << 10));  // bitmask xor
-  else return (unsigned)__shfl_xor((int)v, M);  // 32, 63: ds_bpermute
-}
-
-// One stage of the flip-form bitonic network over P = 64*NW*R keys, position q = t*R + r:
-// the first stage of merge K pairs q with q ^ (K-1), the others pair q with q ^ J, and the
-// lower position always keeps the minimum -- no direction bits anywhere.
-template <int NW, int R, int K, int J>
-__device__ __forceinline__ void wide_stage(unsigned (&key)[R], unsigned* sX, int t, int lane) {
-  constexpr bool flip = (J == K / 2);
-  constexpr int XROW = R + 4;
-  if constexpr (flip ? (K <= R) : (J < R)) {  // inside a thread: min/max pairs
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int r2 = flip ? (r ^ (K - 1)) : (r | J);
-      if (flip ? (r < r2) : ((r & J) == 0)) {
-        const unsigned x = key[r], y = key[r2];
-        key[r] = x < y ? x : y;
-        key[r2] = x < y ? y : x;
-      }
-    }
-  } else if constexpr (flip ? (K <= 64 * R) : (J < 64 * R)) {  // across lanes
-    constexpr int MK = flip ? (K / R - 1) : (J / R);
-    const bool lower = (lane & (flip ? (K / R / 2) : MK)) == 0;
-    unsigned y[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) y[r] = lane_xor<MK>(key[flip ? R - 1 - r : r]);
-#pragma unroll
-    for (int r = 0; r < R; ++r) key[r] = ((key[r] < y[r]) == lower) ? key[r] : y[r];
-  } else {  // across waves, through LDS rows
-    constexpr int MT = flip ? (K / R - 1) : (J / R);
-    const bool lower = (t & (flip ? (K / R / 2) : MT)) == 0;
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < R; r += 4)
-      *reinterpret_cast<uint4*>(sX + t * XROW + r) = make_uint4(key[r], key[r + 1], key[r + 2], key[r + 3]);
-    __syncthreads();
-    unsigned y[R];
-#pragma unroll
-    for (int r = 0; r < R; r += 4) {
-      const uint4 y4 = *reinterpret_cast<const uint4*>(sX + (t ^ MT) * XROW + r);
-      y[r] = y4.x;
-      y[r + 1] = y4.y;
-      y[r + 2] = y4.z;
-      y[r + 3] = y4.w;
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const unsigned yr = y[flip ? R - 1 - r : r];
-      key[r] = ((key[r] < yr) == lower) ? key[r] : yr;
-    }
-  }
-  if constexpr (J > 1) wide_stage<NW, R, K, J / 2>(key, sX, t, lane);
-}
-
-template <int NW, int R, int K = 2>
-__device__ __forceinline__ void wide_sort(unsigned (&key)[R], unsigned* sX, int t, int lane) {
-  wide_stage<NW, R, K, K / 2>(key, sX, t, lane);
-  if constexpr (K < 64 * NW * R) wide_sort<NW, R, 2 * K>(key, sX, t, lane);
-}
-
-template <int NW, int R>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 8))) void consensus_wide_kernel(ConsArgs a) {
-  using Cfg = WideCfg<NW, R>;
-  constexpr int NT = Cfg::NT, P = Cfg::P, IB = Cfg::IB;
-  constexpr unsigned QMASK = (unsigned)P - 1u;
-  __shared__ __attribute__((aligned(16))) double sRegA[Cfg::A_DBL];
-  __shared__ __attribute__((aligned(16))) double sRegB[Cfg::B_DBL];
-  __shared__ unsigned sLast[NW];
-  __shared__ int sCnt[NW];
-  __shared__ int sErr;
-  __shared__ double sTot[4];
-  double* const lP = sRegA;                                    // [P] input order
-  unsigned* const sLead = reinterpret_cast<unsigned*>(sRegA);  // [u] sid<<IB | q0
-  double* const sWAC = sRegA + P / 2;                          // [2][3][NT]
-  unsigned* const sX = reinterpret_cast<unsigned*>(sRegB);     // [NT][XROW]
-  double* const sP = sRegB;                                    // (q)
-
-  const int t = threadIdx.x;
-  const int lane = lane_id();
-  const int wv = t >> 6;
-  const unsigned smax = (unsigned)(a.n_sources > 0 ? a.n_sources - 1 : 0);
-#define WPROF(k) do {} while (0)
-
-  // Market metadata for this workgroup's next 64 markets (li = base + G*k on lane k) is
-  // loaded in one vector batch, so picking a market is a readlane, never a scalar-load
-  // stall; its sid/prob are loaded into registers one market ahead.
-  const int64_t G = gridDim.x;
-  int32_t vm = 0;
-  int64_t voff = 0;
-  int vn = 0;
-  auto refill = [&](int64_t base) {
-    const int64_t li = base + G * lane;
-    vm = (li < a.n_list) ? (a.list ? a.list[li] : (int32_t)li) : 0;
-    voff = (li < a.n_list) ? a.offsets[vm] : 0;
-    vn = (li < a.n_list) ? (int)(a.offsets[vm + 1] - voff) : 0;
-  };
-  int32_t pm = 0;
-  int64_t poff = 0;
-  int pn = 0;
-  unsigned ps[R];
-  double pp[R];
-  auto fetch = [&](int64_t li) {
-    const int k = (int)(((li - blockIdx.x) / G) & 63);
-    if (k == 0) refill(li);
-    pm = __builtin_amdgcn_readlane(vm, k);
-    poff = ((int64_t)__builtin_amdgcn_readlane((int)(voff >> 32), k) << 32) |
-           (uint32_t)__builtin_amdgcn_readlane((int)voff, k);
-    pn = __builtin_amdgcn_readlane(vn, k);
-    // raw buffer loads: one descriptor per market (records = its n signals, so the
-    // hardware zero-fills i >= n) and the chunk offset c*NT in the scalar offset -- no
-    // per-chunk 64-bit addresses held in registers
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(a.sid + poff), 0, pn * 4, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc((void*)(a.prob + poff), 0, pn * 8, 0x00020000);
-#pragma unroll
-    for (int c = 0; c < R; ++c) {
-      ps[c] = __builtin_amdgcn_raw_buffer_load_b32(rs, t * 4, c * NT * 4, 0);
-      pp[c] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rp, t * 8, c * NT * 8, 0));
-    }
-  };
-  if (blockIdx.x < a.n_list) fetch(blockIdx.x);
-
-  for (int64_t li = blockIdx.x; li < a.n_list; li += gridDim.x) {
-    const int32_t m = pm;
-    const int64_t off = poff;
-    const int n = pn;
-
-    // ---- keys (index i = c*NT + t) + input-order probs; range check (core.py:59-60) ----
-    if (t == 0) sErr = 0x7fffffff;
-    unsigned key[R];
-    int myerr = 0x7fffffff;
-#pragma unroll
-    for (int c = 0; c < R; ++c) {
-      const int i = c * NT + t;
-      const double p = pp[c];
-      key[c] = (i < n) ? ((ps[c] < smax ? ps[c] : smax) << IB) | (unsigned)i : 0xFFFFFFFFu;
-      lP[i] = p;
-      if ((p < 0.0 || p > 1.0) && myerr == 0x7fffffff) myerr = i;
-    }
-    // next market's loads: in flight through all of this one (vmcnt is in order, so a load
-    // issued later in the market would make the first gather wait for them)
-    if (li + G < a.n_list) fetch(li + G);
-    __syncthreads();  // sErr init (and the previous market's readers of every region)
-    if (myerr != 0x7fffffff) atomicMin(&sErr, myerr);
-    WPROF(0);
-
-    // ---- bitonic sort (core.py:103 order; ties in input order by the index bits) ---------
-    wide_sort<NW, R>(key, sX, t, lane);
-    if (NW > 1) __syncthreads();  // exchange rows dead before the sorted probs land
-    WPROF(1);
-
-    // ---- sorted probs, run leaders, compact unique index ---------------------------------
-    if (lane == 63) sLast[wv] = key[R - 1];
-    // (thread rows are 8R bytes apart: the 16-B writes conflict, once per market; every
-    // later read is linear in q with immediate offsets)
-#pragma unroll
-    for (int r = 0; r < R; r += 2) {
-      const int q = t * R + r;
-      const double p0 = (q < n) ? lP[key[r] & QMASK] : 0.0;
-      const double p1 = (q + 1 < n) ? lP[key[r + 1] & QMASK] : 0.0;
-      *reinterpret_cast<double2*>(sP + t * R + r) = make_double2(p0, p1);
-    }
-    const unsigned prev_in_wave = (unsigned)__shfl_up((int)key[R - 1], 1);
-    __syncthreads();  // (1) sorted probs + sLast visible; lP dead
-    const unsigned prev_key = (lane > 0) ? prev_in_wave : (wv > 0 ? sLast[wv - 1] : 0u);
-    unsigned lead = 0;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int q = t * R + r;
-      const unsigned ps0 = ((r == 0) ? prev_key : key[r - 1]) >> IB;
-      const bool is = (q < n) && (q == 0 || (key[r] >> IB) != ps0);
-      lead |= is ? (1u << r) : 0u;
-    }
-    const int cnt = __popc(lead);
-    int incl = cnt;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int y = __shfl_up(incl, d);
-      if (lane >= d) incl += y;
-    }
-    if (lane == 63) sCnt[wv] = incl;
-    __syncthreads();  // (2)
-    int base = incl - cnt, u = 0;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) {
-      const int cw = sCnt[w];
-      if (w < wv) base += cw;
-      u += cw;
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      if (lead & (1u << r)) {
-        const int jj = base + __popc(lead & ((1u << r) - 1u));
-        sLead[jj] = (key[r] & ~QMASK) | (unsigned)(t * R + r);
-      }
-    }
-    __syncthreads();  // (3) leaders visible
-    WPROF(2);
-
-    // ---- per-unique products: thread t owns uniques j = t + NT*i ----------------------
-    // Up to HR rounds of NT uniques are computed into registers at once (all relconf
-    // gathers in flight together), then staged round by round through two LDS buffers
-    // while wave 0 carries the three left-to-right chains on lanes 0..2.
-    constexpr int HR = (R < BCE_WIDE_HR) ? R : BCE_WIDE_HR;
-    double acc = 0.0;  // wave 0: lane 0 = total weight, 1 = sum avg*w, 2 = sum c*w
-    const int nr = (u + NT - 1) / NT;
-    for (int h = 0; h < nr; h += HR) {
-      double2 rc[HR];
-      int q0s[HR], q1s[HR];
-      unsigned sids[HR], pw[HR];
-#pragma unroll
-      for (int i = 0; i < HR; ++i) {  // every global load of the half in flight together
-        const int jj = (h + i) * NT + t;
-        q0s[i] = q1s[i] = 0;
-        sids[i] = pw[i] = 0;
-        if (jj < u) {
-          const unsigned lv = sLead[jj];
-          q0s[i] = (int)(lv & QMASK);
-          sids[i] = lv >> IB;  // <= smax by construction of the key
-          q1s[i] = (jj + 1 < u) ? (int)(sLead[jj + 1] & QMASK) : n;
-          rc[i] = (a.n_sources > 0) ? a.relconf[sids[i]] : kColdRow[0];  // empty table: all cold
-          pw[i] = (a.n_sources > 0) ? a.pbits[sids[i] >> 5] : 0u;
-        }
-      }
-      double vw[HR], va[HR], vc[HR];
-#pragma unroll
-      for (int i = 0; i < HR; ++i) {
-        const int jj = (h + i) * NT + t;
-        vw[i] = va[i] = vc[i] = 0.0;
-        if (jj < u) {
-          // builtin sum() from 0 over the run in input order (core.py:116); terms past
-          // the run add +0.0, exact since the sum starts at +0.0 and so is never -0.0
-          const int q0 = q0s[i], len = q1s[i] - q0s[i];
-          const double* rp = sP + q0;
-          double x[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) x[e] = rp[e];
-          double sum = 0.0;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) sum += (e < len) ? x[e] : 0.0;
-          if (len > 4) {  // long (hot-source) run: 16 terms per step, the next 16 in flight
-            int e0 = 4;
-            double xa[8], xb[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) xa[e] = rp[e0 + e];
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) xb[e] = rp[e0 + 8 + e];
-            __builtin_amdgcn_sched_barrier(0);
-            for (; e0 + 16 <= len; e0 += 16) {
-#pragma unroll
-              for (int e = 0; e < 8; ++e) sum += xa[e];
-#pragma unroll
-              for (int e = 0; e < 8; ++e) xa[e] = rp[e0 + 16 + e];
-              __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-              for (int e = 0; e < 8; ++e) sum += xb[e];
-#pragma unroll
-              for (int e = 0; e < 8; ++e) xb[e] = rp[e0 + 24 + e];
-              __builtin_amdgcn_sched_barrier(0);
-            }
-#pragma unroll
-            for (int e = 0; e < 8; ++e) sum += (e0 + e < len) ? xa[e] : 0.0;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) sum += (e0 + 8 + e < len) ? xb[e] : 0.0;
-          }
-          const double avg = (len > 1) ? sum / (double)len : sum;
-          const double w = rc[i].x;  // core.py:111,119
-          vw[i] = w;
-          va[i] = avg * w;       // core.py:136
-          vc[i] = rc[i].y * w;   // core.py:142
-        }
-      }
-      WPROF(3);
-#pragma unroll
-      for (int i = 0; i < HR; ++i) {
-        if (h + i < nr) {
-          double* const buf = sWAC + ((h + i) & 1) * 3 * NT;
-          buf[t] = vw[i];
-          buf[NT + t] = va[i];
-          buf[2 * NT + t] = vc[i];
-          __syncthreads();  // round staged; every sorted-prob read of this half is done
-          WPROF(4);
-          const int jj = (h + i) * NT + t;
-          if (jj < u) sP[(jj)] = vw[i];  // slot jj is only read by uniques <= jj
-          if (wv == 0) {
-            // Full 16-term steps run in asm: two 8-term batches in fixed registers, each
-            // reloaded right after its adds, so one batch's LDS latency hides under the
-            // other's dependent adds (the compiler would copy loop-carried batch registers
-            // behind an lgkmcnt(0)).  The < 16-term tail is added in C++ with masked
-            // terms adding +0.0 -- exact, because these chains never hold -0.0.
-            __builtin_amdgcn_s_setprio(2);  // the chain is the critical path: win VALU arbitration
-            const int ce = (u - (h + i) * NT < NT) ? u - (h + i) * NT : NT;
-            const double* src = buf + (lane % 3) * NT;
-            const int nfull = ce & ~15;
-            if (nfull) {
-              unsigned addr = (unsigned)(uintptr_t)src;
-              int steps = nfull >> 4;
-              asm volatile(
-                  "ds_read_b128 v[96:99], %[ad] offset:0\n"
-                  "ds_read_b128 v[100:103], %[ad] offset:16\n"
-                  "ds_read_b128 v[104:107], %[ad] offset:32\n"
-                  "ds_read_b128 v[108:111], %[ad] offset:48\n"
-                  "ds_read_b128 v[112:115], %[ad] offset:64\n"
-                  "ds_read_b128 v[116:119], %[ad] offset:80\n"
-                  "ds_read_b128 v[120:123], %[ad] offset:96\n"
-                  "ds_read_b128 v[124:127], %[ad] offset:112\n"
-                  "1:\n"
-                  "s_waitcnt lgkmcnt(7)\n"
-                  "v_add_f64 %[acc], %[acc], v[96:97]\n"
-                  "v_add_f64 %[acc], %[acc], v[98:99]\n"
-                  "s_waitcnt lgkmcnt(6)\n"
-                  "v_add_f64 %[acc], %[acc], v[100:101]\n"
-                  "v_add_f64 %[acc], %[acc], v[102:103]\n"
-                  "s_waitcnt lgkmcnt(5)\n"
-                  "v_add_f64 %[acc], %[acc], v[104:105]\n"
-                  "v_add_f64 %[acc], %[acc], v[106:107]\n"
-                  "s_waitcnt lgkmcnt(4)\n"
-                  "v_add_f64 %[acc], %[acc], v[108:109]\n"
-                  "v_add_f64 %[acc], %[acc], v[110:111]\n"
-                  "ds_read_b128 v[96:99], %[ad] offset:128\n"
-                  "ds_read_b128 v[100:103], %[ad] offset:144\n"
-                  "ds_read_b128 v[104:107], %[ad] offset:160\n"
-                  "ds_read_b128 v[108:111], %[ad] offset:176\n"
-                  "s_waitcnt lgkmcnt(7)\n"
-                  "v_add_f64 %[acc], %[acc], v[112:113]\n"
-                  "v_add_f64 %[acc], %[acc], v[114:115]\n"
-                  "s_waitcnt lgkmcnt(6)\n"
-                  "v_add_f64 %[acc], %[acc], v[116:117]\n"
-                  "v_add_f64 %[acc], %[acc], v[118:119]\n"
-                  "s_waitcnt lgkmcnt(5)\n"
-                  "v_add_f64 %[acc], %[acc], v[120:121]\n"
-                  "v_add_f64 %[acc], %[acc], v[122:123]\n"
-                  "s_waitcnt lgkmcnt(4)\n"
-                  "v_add_f64 %[acc], %[acc], v[124:125]\n"
-                  "v_add_f64 %[acc], %[acc], v[126:127]\n"
-                  "ds_read_b128 v[112:115], %[ad] offset:192\n"
-                  "ds_read_b128 v[116:119], %[ad] offset:208\n"
-                  "ds_read_b128 v[120:123], %[ad] offset:224\n"
-                  "ds_read_b128 v[124:127], %[ad] offset:240\n"
-                  "v_add_u32 %[ad], 0x80, %[ad]\n"
-                  "s_sub_u32 %[st], %[st], 1\n"
-                  "s_cmp_lg_u32 %[st], 0\n"
-                  "s_cbranch_scc1 1b\n"
-                  "s_waitcnt lgkmcnt(0)\n"
-                  : [acc] "+v"(acc), [ad] "+v"(addr), [st] "+s"(steps)
-                  :
-                  : "memory", "scc", "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104",
-                    "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", "v114", "v115",
-                    "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123", "v124", "v125", "v126",
-                    "v127");
-            }
-            if (nfull < ce) {
-              double xt[16];
-#pragma unroll
-              for (int e = 0; e < 16; ++e) xt[e] = src[nfull + e];
-#pragma unroll
-              for (int e = 0; e < 16; ++e) acc += (nfull + e < ce) ? xt[e] : 0.0;
-            }
-            __builtin_amdgcn_s_setprio(0);
-          }
-          WPROF(5);
-        }
-      }
-      // per-unique outputs after the chain rounds, so no store is pending under them
-#pragma unroll
-      for (int i = 0; i < HR; ++i) {
-        const int jj = (h + i) * NT + t;
-        if (jj < u) {
-          const int64_t p = off + jj;
-          if (a.usid)
-            a.usid[p] = (int32_t)sids[i] | (((pw[i] >> (sids[i] & 31)) & 1u) ? 0 : (int32_t)0x80000000);
-          if (a.weight) a.weight[p] = vw[i];
-        }
-      }
-      WPROF(3);
-    }
-    if (wv == 0 && lane < 3) sTot[lane] = acc;
-    __syncthreads();  // totals + w[j] visible
-    const double total = sTot[0];
-    if (t == 0) {
-      const bool null_ = (n == 0) || (total == 0.0);
-      a.consensus[m] = null_ ? 0.0 : sTot[1] / total;
-      a.confidence[m] = null_ ? 0.0 : sTot[2] / total;
-      a.total_weight[m] = total;
-      a.n_unique[m] = u;
-      if (a.err_idx) a.err_idx[m] = (sErr == 0x7fffffff) ? -1 : sErr;
-    }
-    if (a.nweight)  // core.py:151
-      for (int jj = t; jj < u; jj += NT)
-        a.nweight[off + jj] = (total > 0.0) ? sP[(jj)] / total : 0.0;
-    WPROF(6);
-  }
-#undef WPROF
-}
 
 }  // namespace bce
 
@@ -2034,40 +1592,11 @@ int launch_long_lds(const ConsArgs& a, hipStream_t st) {
   return check_launch("consensus_long_kernel<lds>");
 }
 
-template <int NW, int R>
-int launch_wide(const ConsArgs& a, hipStream_t st) {
-  if (a.n_list == 0) return BCE_OK;
-  static int per_cu = 0;
-  if (!per_cu) {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, consensus_wide_kernel<NW, R>, 64 * NW, 0) != hipSuccess ||
-        nb <= 0)
-      nb = 1;
-    per_cu = nb;
-    if (getenv("BCE_DEBUG_LAUNCH"))
-      fprintf(stderr, "[bce] consensus_wide_kernel<%d,%d>: %d blocks/CU x %d CUs\n", NW, R, nb, cu_count());
-  }
-  const int64_t cap = (int64_t)cu_count() * per_cu;
-  const int grid = (int)(a.n_list < cap ? a.n_list : cap);
-  hipLaunchKernelGGL((consensus_wide_kernel<NW, R>), dim3(grid), dim3(64 * NW), 0, st, a);
-  return check_launch("consensus_wide_kernel");
-}
-
-// Markets with 64 < n <= 4096: the register-sort kernel when the packed 32-bit key fits
-// (exact mode), else the LDS-sort kernel.
+// Markets with 64 < n <= 4096: the register-sort kernel (consensus_wide.hip) when the
+// packed 32-bit (sid, index) key fits, else the LDS-sort kernel.
 int launch_wide_for_len(int64_t max_len, const ConsArgs& a, hipStream_t st) {
-  const int ib = max_len <= 128 ? 7 : max_len <= 256 ? 8 : max_len <= 512 ? 9 : max_len <= 1024 ? 10
-               : max_len <= 2048 ? 11 : 12;
-  if (a.mode == BCE_MODE_EXACT && (int64_t)a.n_sources <= (1ll << (32 - ib))) {
-    switch (ib) {
-      case 7: return launch_wide<1, 2>(a, st);
-      case 8: return launch_wide<1, 4>(a, st);
-      case 9: return launch_wide<1, 8>(a, st);
-      case 10: return launch_wide<1, 16>(a, st);
-      case 11: return launch_wide<2, 16>(a, st);
-      default: return launch_wide<4, 16>(a, st);
-    }
-  }
+  const int ib = wide_key_bits(max_len);
+  if ((int64_t)a.n_sources <= (1ll << (32 - ib))) return launch_wide_ib(ib, a, st);
   return launch_long_lds(a, st);
 }
 

@@ -1,6 +1,6 @@
 // consensus_common.hpp -- declarations shared by the consensus translation units
 // (consensus.hip: list / long-market kernels, launchers and the C ABI; consensus_tab.hip:
-// the LDS-table kernel for contiguous short markets).
+// the LDS-table kernel for contiguous short markets; consensus_wide.hip: 64 < n <= 4096).
 #pragma once
 #pragma clang fp contract(off)
 
@@ -147,5 +147,10 @@ int spin_cap();
 // n_sources <= kTabMaxSources.
 constexpr int kTabMaxSources = 10112;  // 16 B per source + the bitmask fit the 160 KiB LDS
 int launch_tab32(const ConsArgs& a, hipStream_t st);
+
+// Register-sort kernel (consensus_wide.hip) for 64 < n <= 4096: ib = log2 of the key's
+// index field (7..12, wide_key_bits(max_len)); needs n_sources <= 2^(32 - ib).
+int wide_key_bits(int64_t max_len);
+int launch_wide_ib(int ib, const ConsArgs& a, hipStream_t st);
 
 }  // namespace bce

@@ -1,0 +1,621 @@
+// consensus_wide.hip -- core.compute_consensus (core.py:63-179) for markets with
+// 64 < n <= 4096 signals: one workgroup of NW waves per market, P = 64*NW*R keys.
+//
+// Per market (core.py:103 sorted source ids, core.py:115-116 duplicates averaged in input
+// order, core.py:111-112 table lookups, core.py:119-151 weights and ordered sums):
+//   1. keys (sid << IB | input index, 32 bits; needs n_sources <= 2^(32-IB)) from the sid
+//      registers loaded one market ahead; the next market's sids are issued right away.
+//   2. register bitonic network (flip form): stages inside a thread are min/max pairs, lane
+//      exchanges use DPP / ds_swizzle / ds_bpermute, the few stages that cross waves go
+//      through LDS rows (region B).
+//   3. input-order probabilities (loaded during the previous market) land in region A, are
+//      range-checked (core.py:59-60), read back in sorted order into registers and written
+//      over region A in place; run leaders get their unique index from a workgroup prefix
+//      count and land in region B (sid << IB | first sorted position).
+//   4. per unique j (thread t owns j = t + NT*i): the run's probabilities summed in input
+//      order (builtin sum, core.py:116; FAST: runs longer than kWaveRun by the whole wave
+//      in a fixed order), one {rel, conf} row + present bit gathered,
+//      products w, avg*w, conf*w (core.py:119,136,142); usid / weight written.
+//        FAST  (BCE_MODE_FAST): per-thread partial sums in round order, then a fixed
+//              butterfly over the wave and a wave-ordered sum over the workgroup --
+//              deterministic, within the north-star 1e-9 of the reference order.
+//        EXACT: rounds of NT products staged through two LDS buffers; wave 0 carries the
+//              three left-to-right chains (core.py:120,136,142) on lanes 0..2.
+//      w[j] is parked in the dead sorted-probability slot j for normalizedWeight.
+//   5. the next market's probabilities are issued, then per-market outputs and
+//      normalizedWeight = w / total (core.py:151).
+// LDS: region A = P doubles (+ read-ahead pad), region B = max(sort exchange rows,
+// leaders [+ the exact chain buffers]).  FAST at P = 4096 fits three workgroups per CU.
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "consensus_common.hpp"
+
+#pragma clang fp contract(off)
+
+#ifndef BCE_WIDE_HR
+#define BCE_WIDE_HR 2  // rounds of NT uniques whose gathers are in flight together
+#endif
+#ifndef BCE_WIDE_WPE
+#define BCE_WIDE_WPE 2  // min waves per SIMD (register budget)
+#endif
+#ifndef BCE_WIDE_EARLY
+#define BCE_WIDE_EARLY 1  // next market's probabilities issued with its sids (1) or after the gathers (0)
+#endif
+#ifndef BCE_WIDE_MAP
+#define BCE_WIDE_MAP 1  // (NW, R) per key-bit width: 0 = R 16 from P 1024, 1 = R 8 from P 1024, 2 = R 4 from P 1024
+#endif
+#ifndef BCE_WIDE_PROF
+#define BCE_WIDE_PROF 0  // experiment builds only (tools/wide_variants.py): per-phase s_memtime
+#endif
+
+namespace bce {
+namespace {
+
+#if BCE_WIDE_PROF
+__device__ unsigned long long g_wide_prof[8];
+#define WMARK(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); prof[k] += t_ - prof_t; prof_t = t_; } while (0)
+#else
+#define WMARK(k) do {} while (0)
+#endif
+
+constexpr int ilog2c(int x) { return x <= 1 ? 0 : 1 + ilog2c(x >> 1); }
+constexpr int kWaveRun = 48;  // FAST: duplicate runs longer than this are summed wave-wide
+
+template <int NW, int R, bool FAST>
+struct WideCfg {
+  static constexpr int NT = 64 * NW;
+  static constexpr int P = NT * R;
+  static constexpr int IB = ilog2c(P);
+  static constexpr int XROW = R + 4;  // padded exchange row (u32)
+  static constexpr int HR = (R < BCE_WIDE_HR) ? R : BCE_WIDE_HR;
+  // register budget: workgroups of >= 4 waves get 4 waves per SIMD (<= 128 VGPRs), so two
+  // LDS-sized workgroups share a CU
+  static constexpr int WPE = (NW >= 4 && BCE_WIDE_WPE < 4) ? 4 : BCE_WIDE_WPE;
+  static constexpr int A_DBL = P + 64;  // + the run sums' read-ahead
+  // region B (u32): sort exchange rows, then leaders [P] (+ exact: chain buffers
+  // [2][3][NT] doubles + the chain's read-ahead)
+  static constexpr int LEAD_U32 = FAST ? P : P + 2 * (6 * NT + 32);
+  static constexpr int B_U32 = (NT * XROW > LEAD_U32) ? NT * XROW : LEAD_U32;
+};
+
+// v from lane ^ M (whole wave) for the masks the flip-form sort uses.
+template <int M>
+__device__ __forceinline__ unsigned lane_xor(unsigned v) {
+  if constexpr (M == 1) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
+  else if constexpr (M == 2) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // 2,3,0,1
+  else if constexpr (M == 3) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x1B, 0xF, 0xF, false);  // 3,2,1,0
+  else if constexpr (M == 7) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false); // row_half_mirror
+  else if constexpr (M == 15) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false);  // row_mirror
+  else if constexpr (M < 32) return (unsigned)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (M << 10));  // bitmask xor
+  else return (unsigned)__shfl_xor((int)v, M);  // 32, 63: ds_bpermute
+}
+
+// One stage of the flip-form bitonic network over P = 64*NW*R keys, position q = t*R + r:
+// the first stage of merge K pairs q with q ^ (K-1), the others pair q with q ^ J, and the
+// lower position always keeps the minimum -- no direction bits anywhere.
+template <int NW, int R, int K, int J>
+__device__ __forceinline__ void wide_stage(unsigned (&key)[R], unsigned* sX, int t, int lane) {
+  constexpr bool flip = (J == K / 2);
+  constexpr int XROW = R + 4;
+  if constexpr (flip ? (K <= R) : (J < R)) {  // inside a thread: min/max pairs
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int r2 = flip ? (r ^ (K - 1)) : (r | J);
+      if (flip ? (r < r2) : ((r & J) == 0)) {
+        const unsigned x = key[r], y = key[r2];
+        key[r] = x < y ? x : y;
+        key[r2] = x < y ? y : x;
+      }
+    }
+  } else if constexpr (flip ? (K <= 64 * R) : (J < 64 * R)) {  // across lanes
+    constexpr int MK = flip ? (K / R - 1) : (J / R);
+    const bool lower = (lane & (flip ? (K / R / 2) : MK)) == 0;
+    unsigned y[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) y[r] = lane_xor<MK>(key[flip ? R - 1 - r : r]);
+#pragma unroll
+    for (int r = 0; r < R; ++r) key[r] = ((key[r] < y[r]) == lower) ? key[r] : y[r];
+  } else {  // across waves, through LDS rows
+    constexpr int MT = flip ? (K / R - 1) : (J / R);
+    const bool lower = (t & (flip ? (K / R / 2) : MT)) == 0;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R; r += 4)
+      *reinterpret_cast<uint4*>(sX + t * XROW + r) = make_uint4(key[r], key[r + 1], key[r + 2], key[r + 3]);
+    __syncthreads();
+    unsigned y[R];
+#pragma unroll
+    for (int r = 0; r < R; r += 4) {
+      const uint4 y4 = *reinterpret_cast<const uint4*>(sX + (t ^ MT) * XROW + r);
+      y[r] = y4.x;
+      y[r + 1] = y4.y;
+      y[r + 2] = y4.z;
+      y[r + 3] = y4.w;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const unsigned yr = y[flip ? R - 1 - r : r];
+      key[r] = ((key[r] < yr) == lower) ? key[r] : yr;
+    }
+  }
+  if constexpr (J > 1) wide_stage<NW, R, K, J / 2>(key, sX, t, lane);
+}
+
+template <int NW, int R, int K = 2>
+__device__ __forceinline__ void wide_sort(unsigned (&key)[R], unsigned* sX, int t, int lane) {
+  wide_stage<NW, R, K, K / 2>(key, sX, t, lane);
+  if constexpr (K < 64 * NW * R) wide_sort<NW, R, 2 * K>(key, sX, t, lane);
+}
+
+// Fixed xor butterfly: every lane ends with the same, run-independent sum.
+__device__ __forceinline__ double wave_sum_fixed(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = v + __shfl_xor(v, o);
+  return v;
+}
+
+// builtin sum() from 0 over a run of len sorted probabilities in input order (core.py:116);
+// terms past the run add +0.0, exact since the sum starts at +0.0 and is never -0.0.
+__device__ __forceinline__ double run_sum(const double* rp, int len) {
+  double x[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) x[e] = rp[e];
+  double sum = 0.0;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) sum += (e < len) ? x[e] : 0.0;
+  if (len > 4) {  // long (hot-source) run: 8 terms per step, the next 8 in flight
+    int e0 = 4;
+    double xa[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) xa[e] = rp[e0 + e];
+    for (; e0 + 8 <= len; e0 += 8) {
+      double xb[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) xb[e] = rp[e0 + 8 + e];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sum += xa[e];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) xa[e] = xb[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sum += (e0 + e < len) ? xa[e] : 0.0;
+  }
+  return (len > 1) ? sum / (double)len : sum;
+}
+
+template <int NW, int R, bool FAST>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg<NW, R, FAST>::WPE, 8))) void consensus_wide_kernel(ConsArgs a) {
+  using Cfg = WideCfg<NW, R, FAST>;
+  constexpr int NT = Cfg::NT, P = Cfg::P, IB = Cfg::IB, HR = Cfg::HR;
+  constexpr unsigned QMASK = (unsigned)P - 1u;
+  constexpr int kNoErr = 0x7fffffff;
+  __shared__ __attribute__((aligned(16))) double sA[Cfg::A_DBL];
+  __shared__ __attribute__((aligned(16))) unsigned sB[Cfg::B_U32];
+  __shared__ unsigned sLast[NW];
+  __shared__ int sCnt[NW];
+  __shared__ int sErr;
+  __shared__ double sTot[3 * NW];
+  unsigned* const sX = sB;                                            // sort exchange rows
+  unsigned* const sLead = sB;                                         // [u] sid<<IB | q0
+  double* const sWAC = reinterpret_cast<double*>(sB + P);             // exact: [2][3][NT]
+
+  const int t = threadIdx.x;
+  const int lane = lane_id();
+  const int wv = t >> 6;
+  const unsigned smax = (unsigned)(a.n_sources > 0 ? a.n_sources - 1 : 0);
+#if BCE_WIDE_PROF
+  unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prof_t = __builtin_amdgcn_s_memtime();
+#endif
+
+  // Market metadata for this workgroup's next 64 markets (li = base + G*k on lane k) is
+  // loaded in one vector batch, so picking a market is a readlane, never a scalar-load
+  // stall.  A market's sids are loaded one market ahead, its probabilities while the
+  // previous market finishes (buffer loads: records = n signals, so i >= n reads 0).
+  const int64_t G = gridDim.x;
+  int32_t vm = 0;
+  int64_t voff = 0;
+  int vn = 0;
+  auto refill = [&](int64_t base) {
+    const int64_t li = base + G * lane;
+    vm = (li < a.n_list) ? (a.list ? a.list[li] : (int32_t)li) : 0;
+    voff = (li < a.n_list) ? a.offsets[vm] : 0;
+    vn = (li < a.n_list) ? (int)(a.offsets[vm + 1] - voff) : 0;
+  };
+  int32_t nm = 0;
+  int64_t noff = 0;
+  int nn = 0;
+  auto meta = [&](int64_t li) {
+    const int k = (int)(((li - blockIdx.x) / G) & 63);
+    if (k == 0) refill(li);
+    nm = __builtin_amdgcn_readlane(vm, k);
+    noff = ((int64_t)__builtin_amdgcn_readlane((int)(voff >> 32), k) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)voff, k);
+    nn = __builtin_amdgcn_readlane(vn, k);
+  };
+  unsigned ps[R];
+  double pp[R];
+  auto load_sids = [&]() {
+    const int cnt = nn < P ? nn : P;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(a.sid + noff), 0, cnt * 4, 0x00020000);
+#pragma unroll
+    for (int c = 0; c < R; ++c) ps[c] = __builtin_amdgcn_raw_buffer_load_b32(rs, t * 4, c * NT * 4, 0);
+  };
+  auto load_probs = [&]() {
+    const int cnt = nn < P ? nn : P;
+    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc((void*)(a.prob + noff), 0, cnt * 8, 0x00020000);
+#pragma unroll
+    for (int c = 0; c < R; ++c)
+      pp[c] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rp, t * 8, c * NT * 8, 0));
+  };
+  if (blockIdx.x < a.n_list) {
+    meta(blockIdx.x);
+    load_sids();
+    load_probs();
+  }
+
+  for (int64_t li = blockIdx.x; li < a.n_list; li += G) {
+    const int32_t m = nm;
+    const int64_t off = noff;
+    const int n = nn;
+
+    // ---- 1. keys; next market's metadata + sids ------------------------------------
+    unsigned key[R];
+    bool badsid = false;
+#pragma unroll
+    for (int c = 0; c < R; ++c) {
+      const int i = c * NT + t;
+      const unsigned s = ps[c];
+      badsid |= (i < n) && (s > smax);
+      key[c] = (i < n) ? ((s < smax ? s : smax) << IB) | (unsigned)i : 0xFFFFFFFFu;
+    }
+    if (ballot(badsid)) raise_fault(a.fault, kFaultSid);
+    int myerr = kNoErr;
+    if constexpr (BCE_WIDE_EARLY) {  // input-order probs into region A before the next loads
+      if constexpr (NW > 1) __syncthreads();  // the previous market's readers of region A are done
+#pragma unroll
+      for (int c = 0; c < R; ++c) {
+        const int i = c * NT + t;
+        const double p = pp[c];
+        sA[i] = p;
+        if ((i < n) && (p < 0.0 || p > 1.0) && myerr == kNoErr) myerr = i;  // core.py:59-60
+      }
+    }
+    const bool has_next = li + G < a.n_list;
+    if (has_next) {
+      meta(li + G);
+      load_sids();
+      if constexpr (BCE_WIDE_EARLY) load_probs();
+    }
+    if (n > P) {  // longer than this launch's max_len: left unprocessed, reported
+      raise_fault(a.fault, kFaultTooLong);
+      if (!BCE_WIDE_EARLY && has_next) load_probs();
+      continue;
+    }
+    if (t == 0) sErr = kNoErr;
+    WMARK(0);
+
+    // ---- 2. sort (core.py:103 order; ties in input order by the index bits) ----------
+    wide_sort<NW, R>(key, sX, t, lane);
+    WMARK(1);
+
+    // ---- 3. input-order probs + range check, sorted probs in place, leaders ----------
+    if constexpr (!BCE_WIDE_EARLY) {
+#pragma unroll
+      for (int c = 0; c < R; ++c) {
+        const int i = c * NT + t;
+        const double p = pp[c];
+        sA[i] = p;
+        if ((i < n) && (p < 0.0 || p > 1.0) && myerr == kNoErr) myerr = i;  // core.py:59-60
+      }
+    }
+    if (lane == 63) sLast[wv] = key[R - 1];
+    __syncthreads();  // (a) input-order probs + sLast visible; exchange rows dead
+    if (myerr != kNoErr) atomicMin(&sErr, myerr);
+    double x[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int q = t * R + r;
+      x[r] = (q < n) ? sA[key[r] & QMASK] : 0.0;
+    }
+    const unsigned prev_in_wave = (unsigned)__shfl_up((int)key[R - 1], 1);
+    const unsigned prev_key = (lane > 0) ? prev_in_wave : (wv > 0 ? sLast[wv - 1] : 0u);
+    unsigned lead = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int q = t * R + r;
+      const unsigned ps0 = ((r == 0) ? prev_key : key[r - 1]) >> IB;
+      const bool is = (q < n) && (q == 0 || (key[r] >> IB) != ps0);
+      lead |= is ? (1u << r) : 0u;
+    }
+    const int cnt = __popc(lead);
+    int incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int y = __shfl_up(incl, d);
+      if (lane >= d) incl += y;
+    }
+    if (lane == 63) sCnt[wv] = incl;
+    __syncthreads();  // (b) every read of the input-order probs done; counts visible
+#pragma unroll
+    for (int r = 0; r < R; r += 2)
+      *reinterpret_cast<double2*>(sA + t * R + r) = make_double2(x[r], x[r + 1]);
+    int base = incl - cnt, u = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const int cw = sCnt[w];
+      if (w < wv) base += cw;
+      u += cw;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (lead & (1u << r)) {
+        const int jj = base + __popc(lead & ((1u << r) - 1u));
+        sLead[jj] = (key[r] & ~QMASK) | (unsigned)(t * R + r);
+      }
+    }
+    __syncthreads();  // (c) sorted probs + leaders visible
+    WMARK(2);
+
+    // ---- 4. per-unique products --------------------------------------------------------
+    const int nr = (u + NT - 1) / NT;
+    double acc = 0.0;                     // exact: wave 0 lanes 0..2 carry the chains
+    double pw = 0.0, pa = 0.0, pc = 0.0;  // fast: this thread's partial sums
+    for (int h = 0; h < nr; h += HR) {
+      double2 rc[HR];
+      int q0s[HR], q1s[HR];
+      unsigned sids[HR], pwd[HR];
+#pragma unroll
+      for (int i = 0; i < HR; ++i) {  // every gather of the group in flight together
+        const int jj = (h + i) * NT + t;
+        q0s[i] = q1s[i] = 0;
+        sids[i] = pwd[i] = 0;
+        rc[i] = make_double2(0.5, 0.25);  // DEFAULT_RELIABILITY / _CONFIDENCE (empty table)
+        if (jj < u) {
+          const unsigned lv = sLead[jj];
+          q0s[i] = (int)(lv & QMASK);
+          sids[i] = lv >> IB;  // <= smax by construction of the key
+          q1s[i] = (jj + 1 < u) ? (int)(sLead[jj + 1] & QMASK) : n;
+          if (a.n_sources > 0) {
+            rc[i] = a.relconf[sids[i]];
+            pwd[i] = a.pbits[sids[i] >> 5];
+          }
+        }
+      }
+      double vw[HR], va[HR], vc[HR];
+#pragma unroll
+      for (int i = 0; i < HR; ++i) {
+        const int jj = (h + i) * NT + t;
+        const int len = q1s[i] - q0s[i];
+        double avg = 0.0;
+        if constexpr (FAST) {
+          // runs longer than kWaveRun (hot sources) are summed by the whole wave in a fixed
+          // order instead of by their own lane, so one hot source does not hold the wave
+          avg = (jj < u && len <= kWaveRun) ? run_sum(sA + q0s[i], len) : 0.0;
+          unsigned long long lm = ballot(jj < u && len > kWaveRun);
+          while (lm) {
+            const int L = __builtin_ctzll(lm);
+            lm &= lm - 1;
+            const int lq0 = __builtin_amdgcn_readlane(q0s[i], L), llen = __builtin_amdgcn_readlane(len, L);
+            double part = 0.0;
+            for (int e = lane; e < llen; e += 64) part += sA[lq0 + e];
+            part = wave_sum_fixed(part);
+            if (lane == L) avg = part / (double)llen;
+          }
+        } else if (jj < u) {
+          avg = run_sum(sA + q0s[i], len);
+        }
+        vw[i] = va[i] = vc[i] = 0.0;
+        if (jj < u) {
+          const double w = rc[i].x;  // core.py:111,119
+          vw[i] = w;
+          va[i] = avg * w;        // core.py:136
+          vc[i] = rc[i].y * w;    // core.py:142
+        }
+      }
+      WMARK(3);
+      if constexpr (FAST) {
+#pragma unroll
+        for (int i = 0; i < HR; ++i) {  // round order: fixed per thread
+          pw += vw[i];
+          pa += va[i];
+          pc += vc[i];
+        }
+        __syncthreads();  // every sorted-prob read of this group done
+#pragma unroll
+        for (int i = 0; i < HR; ++i) {
+          const int jj = (h + i) * NT + t;
+          if (jj < u) sA[jj] = vw[i];  // later groups read only slots > jj
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < HR; ++i) {
+          if (h + i < nr) {
+            double* const buf = sWAC + ((h + i) & 1) * 3 * NT;
+            buf[t] = vw[i];
+            buf[NT + t] = va[i];
+            buf[2 * NT + t] = vc[i];
+            __syncthreads();  // round staged; every sorted-prob read of this group is done
+            WMARK(4);
+            const int jj = (h + i) * NT + t;
+            if (jj < u) sA[jj] = vw[i];  // slot jj is only read by uniques <= jj
+            if (wv == 0) {
+              // Full 8-term steps run in asm: two 4-term batches in fixed registers, each
+              // reloaded right after its adds, so one batch's LDS latency hides under the
+              // other's dependent adds (the compiler would copy loop-carried batch registers
+              // behind an lgkmcnt(0)).  The < 8-term tail is added in C++ with masked terms
+              // adding +0.0 -- exact, because these chains never hold -0.0.
+              __builtin_amdgcn_s_setprio(2);  // the chain is the critical path
+              const int ce = (u - (h + i) * NT < NT) ? u - (h + i) * NT : NT;
+              const double* src = buf + (lane % 3) * NT;
+              const int nfull = ce & ~7;
+              if (nfull) {
+                unsigned addr = (unsigned)(uintptr_t)src;
+                int steps = nfull >> 3;
+                asm volatile(
+                    "ds_read_b128 v[112:115], %[ad] offset:0\n"
+                    "ds_read_b128 v[116:119], %[ad] offset:16\n"
+                    "ds_read_b128 v[120:123], %[ad] offset:32\n"
+                    "ds_read_b128 v[124:127], %[ad] offset:48\n"
+                    "1:\n"
+                    "s_waitcnt lgkmcnt(3)\n"
+                    "v_add_f64 %[acc], %[acc], v[112:113]\n"
+                    "v_add_f64 %[acc], %[acc], v[114:115]\n"
+                    "s_waitcnt lgkmcnt(2)\n"
+                    "v_add_f64 %[acc], %[acc], v[116:117]\n"
+                    "v_add_f64 %[acc], %[acc], v[118:119]\n"
+                    "ds_read_b128 v[112:115], %[ad] offset:64\n"
+                    "ds_read_b128 v[116:119], %[ad] offset:80\n"
+                    "s_waitcnt lgkmcnt(3)\n"
+                    "v_add_f64 %[acc], %[acc], v[120:121]\n"
+                    "v_add_f64 %[acc], %[acc], v[122:123]\n"
+                    "s_waitcnt lgkmcnt(2)\n"
+                    "v_add_f64 %[acc], %[acc], v[124:125]\n"
+                    "v_add_f64 %[acc], %[acc], v[126:127]\n"
+                    "ds_read_b128 v[120:123], %[ad] offset:96\n"
+                    "ds_read_b128 v[124:127], %[ad] offset:112\n"
+                    "v_add_u32 %[ad], 64, %[ad]\n"
+                    "s_sub_u32 %[st], %[st], 1\n"
+                    "s_cmp_lg_u32 %[st], 0\n"
+                    "s_cbranch_scc1 1b\n"
+                    "s_waitcnt lgkmcnt(0)\n"
+                    : [acc] "+v"(acc), [ad] "+v"(addr), [st] "+s"(steps)
+                    :
+                    : "memory", "scc", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120",
+                      "v121", "v122", "v123", "v124", "v125", "v126", "v127");
+              }
+              if (nfull < ce) {
+                double xt[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) xt[e] = src[nfull + e];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) acc += (nfull + e < ce) ? xt[e] : 0.0;
+              }
+              __builtin_amdgcn_s_setprio(0);
+            }
+            WMARK(5);
+          }
+        }
+      }
+      // per-unique outputs after the group's LDS work, so no store is pending under it
+#pragma unroll
+      for (int i = 0; i < HR; ++i) {
+        const int jj = (h + i) * NT + t;
+        if (jj < u) {
+          const int64_t p = off + jj;
+          if (a.usid)
+            a.usid[p] = (int32_t)sids[i] | (((pwd[i] >> (sids[i] & 31)) & 1u) ? 0 : (int32_t)0x80000000);
+          if (a.weight) a.weight[p] = vw[i];
+        }
+      }
+      WMARK(3);
+    }
+
+    // ---- 5. next market's probabilities; totals, per-market outputs, nweight ---------
+    if (!BCE_WIDE_EARLY && has_next) load_probs();
+    if constexpr (FAST) {
+      pw = wave_sum_fixed(pw);
+      pa = wave_sum_fixed(pa);
+      pc = wave_sum_fixed(pc);
+      if (lane == 0) {
+        sTot[3 * wv] = pw;
+        sTot[3 * wv + 1] = pa;
+        sTot[3 * wv + 2] = pc;
+      }
+    } else {
+      if (wv == 0 && lane < 3) sTot[lane] = acc;
+    }
+    __syncthreads();  // totals + w[j] visible
+    double tw = sTot[0], ta = sTot[1], tc = sTot[2];
+    if constexpr (FAST) {
+#pragma unroll
+      for (int w = 1; w < NW; ++w) {
+        tw += sTot[3 * w];
+        ta += sTot[3 * w + 1];
+        tc += sTot[3 * w + 2];
+      }
+    }
+    if (t == 0) {
+      const bool null_ = (n == 0) || (tw == 0.0);
+      a.consensus[m] = null_ ? 0.0 : ta / tw;
+      a.confidence[m] = null_ ? 0.0 : tc / tw;
+      a.total_weight[m] = tw;
+      a.n_unique[m] = u;
+      if (a.err_idx) a.err_idx[m] = (sErr == kNoErr) ? -1 : sErr;
+    }
+    if (a.nweight)  // core.py:151
+      for (int jj = t; jj < u; jj += NT) a.nweight[off + jj] = (tw > 0.0) ? sA[jj] / tw : 0.0;
+    WMARK(6);
+  }
+#if BCE_WIDE_PROF
+  if (lane_id() == 0)
+    for (int k = 0; k < 7; ++k) atomicAdd(&g_wide_prof[k], prof[k]);
+#endif
+}
+
+template <int NW, int R, bool FAST>
+int launch_wide(const ConsArgs& a, hipStream_t st) {
+  if (a.n_list == 0) return BCE_OK;
+  static int per_cu = 0;
+  if (!per_cu) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, consensus_wide_kernel<NW, R, FAST>, 64 * NW, 0) !=
+            hipSuccess ||
+        nb <= 0)
+      nb = 1;
+    per_cu = nb;
+    if (getenv("BCE_DEBUG_LAUNCH"))
+      fprintf(stderr, "[bce] consensus_wide_kernel<%d,%d,%s>: %d blocks/CU x %d CUs\n", NW, R,
+              FAST ? "fast" : "exact", nb, cu_count());
+  }
+  const int64_t cap = (int64_t)cu_count() * per_cu;
+  const int grid = (int)(a.n_list < cap ? a.n_list : cap);
+  hipLaunchKernelGGL((consensus_wide_kernel<NW, R, FAST>), dim3(grid), dim3(64 * NW), 0, st, a);
+  return check_launch("consensus_wide_kernel");
+}
+
+template <bool FAST>
+int launch_wide_mode(int ib, const ConsArgs& a, hipStream_t st) {
+  switch (ib) {
+    case 7: return launch_wide<1, 2, FAST>(a, st);
+    case 8: return launch_wide<1, 4, FAST>(a, st);
+#if BCE_WIDE_MAP == 0
+    case 9: return launch_wide<1, 8, FAST>(a, st);
+    case 10: return launch_wide<1, 16, FAST>(a, st);
+    case 11: return launch_wide<2, 16, FAST>(a, st);
+    default: return launch_wide<4, 16, FAST>(a, st);
+#elif BCE_WIDE_MAP == 1
+    case 9: return launch_wide<1, 8, FAST>(a, st);
+    case 10: return launch_wide<2, 8, FAST>(a, st);
+    case 11: return launch_wide<4, 8, FAST>(a, st);
+    default: return launch_wide<8, 8, FAST>(a, st);
+#else
+    case 9: return launch_wide<2, 4, FAST>(a, st);
+    case 10: return launch_wide<4, 4, FAST>(a, st);
+    case 11: return launch_wide<8, 4, FAST>(a, st);
+    default: return launch_wide<16, 4, FAST>(a, st);
+#endif
+  }
+}
+
+}  // namespace
+
+#if BCE_WIDE_PROF
+extern "C" int bce_wide_prof_read(unsigned long long* host8) {
+  BCE_HIP(hipMemcpyFromSymbol(host8, HIP_SYMBOL(g_wide_prof), 8 * sizeof(unsigned long long)));
+  unsigned long long z[8] = {0};
+  BCE_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_wide_prof), z, sizeof z));
+  return BCE_OK;
+}
+#endif
+
+int wide_key_bits(int64_t max_len) {
+  return max_len <= 128 ? 7 : max_len <= 256 ? 8 : max_len <= 512 ? 9 : max_len <= 1024 ? 10 : max_len <= 2048 ? 11
+                                                                                                                 : 12;
+}
+
+int launch_wide_ib(int ib, const ConsArgs& a, hipStream_t st) {
+  return (a.mode == BCE_MODE_FAST) ? launch_wide_mode<true>(ib, a, st) : launch_wide_mode<false>(ib, a, st);
+}
+
+}  // namespace bce

@@ -164,12 +164,12 @@ def _cpu_c5(P, args, m_sample=1024):
 
 
 # ---------------------------------------------------------------------------------------
-def _c3(args, world, rank, barrier, max_over, sum_over):
-    from bayesian_engine import batch
+def make_c3(world=1, rank=0, total=100_000_000, S=1_000_000):
+    """Config 3: ragged CSR with log-uniform lengths on [1, 4096] and Zipf(1.1)
+    sources over S ranks; this rank's market shard.  Returns (M, offsets, sid, prob, table
+    arrays (rel, conf, present) as interned on the host)."""
     from bayesian_engine.sharding import shard_markets
 
-    total = 100_000_000
-    S = 1_000_000
     rng = np.random.default_rng(3)
     lens = np.floor(np.exp(rng.uniform(0, np.log(4097), size=total // 400))).astype(np.int64)
     cs = np.cumsum(lens)
@@ -192,14 +192,24 @@ def _c3(args, world, rank, barrier, max_over, sum_over):
         bad = bad[z[bad] > S]
     sid = perm[z - 1]
     prob = r2.random(n)
-    dev = torch.device("cuda", torch.cuda.current_device())
-    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
     rt = np.random.default_rng(34)
     rel, conf = rt.uniform(0.1, 1.0, S), rt.random(S)
     present = (rt.random(S) < 0.9).astype(np.uint8)
     rel_h, conf_h = np.where(present == 1, rel, 0.5), np.where(present == 1, conf, 0.25)
+    return M, off, sid, prob, (rel_h, conf_h, present)
+
+
+def _c3(args, world, rank, barrier, max_over, sum_over):
+    from bayesian_engine import batch
+
+    S = 1_000_000
+    total = 100_000_000
+    M, off, sid, prob, table_host = make_c3(world, rank, total, S)
+    n = int(off[-1])
+    rel_h, conf_h, present = table_host
+    dev = torch.device("cuda", torch.cuda.current_device())
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
     table = batch.SourceTable.from_arrays(T(rel_h), T(conf_h), T(present))
-    table_host = (rel_h, conf_h, present)
     d_off, d_sid, d_prob = T(off), T(sid), T(prob)
     plan = batch.Plan.build(off, dev)
     res = batch._alloc(len(off) - 1, n, dev, True, True)
