@@ -446,7 +446,11 @@ def aggregate(group_offsets: torch.Tensor, members: torch.Tensor, consensus: tor
 
 def reestimate(P: torch.Tensor, iters: int, w0: float = 0.5, w: Optional[torch.Tensor] = None,
                keep_history: bool = False):
-    """Config 5: ``iters`` rounds of consensus <-> reliability on agent-major P [A, M]."""
+    """Config 5: ``iters`` rounds of consensus <-> reliability on agent-major P [A, M].
+
+    Each round reads P once: the consensus pass records every cell's vote as one bit and the
+    agreement pass counts from those bits (bce_reestimate_consensus_votes /
+    bce_reestimate_agreement_votes; A*ceil(M/64)*8 bytes of scratch)."""
     L = N.require_gpu()
     A, M = P.shape
     dev = P.device
@@ -457,15 +461,19 @@ def reestimate(P: torch.Tensor, iters: int, w0: float = 0.5, w: Optional[torch.T
     nul = torch.empty(max(M, 1), dtype=torch.uint8, device=dev)
     agree = torch.zeros(A, dtype=torch.int64, device=dev)
     resolved = torch.zeros(1, dtype=torch.int64, device=dev)
+    K = max((M + 63) // 64, 1)
+    votes = torch.empty((K, A), dtype=torch.int64, device=dev)
+    words = torch.empty((2, K), dtype=torch.int64, device=dev)  # cvote, ok
     hist = []
     st = N.stream(dev)
     for _ in range(iters):
-        N.check(L.bce_reestimate_consensus(N.ptr(P, row_strided=True), A, M, ld, N.ptr(w), N.ptr(cons), N.ptr(nul), st),
-                "bce_reestimate_consensus")
+        N.check(L.bce_reestimate_consensus_votes(N.ptr(P, row_strided=True), A, M, ld, N.ptr(w), N.ptr(cons),
+                                                 N.ptr(nul), N.ptr(votes), N.ptr(words[0]), N.ptr(words[1]), st),
+                "bce_reestimate_consensus_votes")
         agree.zero_()
         resolved.zero_()
-        N.check(L.bce_reestimate_agreement(N.ptr(P, row_strided=True), A, M, ld, N.ptr(cons), N.ptr(nul), N.ptr(agree),
-                                           N.ptr(resolved), st), "bce_reestimate_agreement")
+        N.check(L.bce_reestimate_agreement_votes(N.ptr(votes), A, M, N.ptr(words[0]), N.ptr(words[1]),
+                                                 N.ptr(agree), N.ptr(resolved), st), "bce_reestimate_agreement_votes")
         N.check(L.bce_reestimate_weights(A, N.ptr(agree), N.ptr(resolved), N.ptr(w), st),
                 "bce_reestimate_weights")
         if keep_history:

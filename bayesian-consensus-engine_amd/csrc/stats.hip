@@ -9,6 +9,11 @@
 //   reestimate_agreement   config 5 pass 2: per-agent count of markets whose binary vote
 //                          matches the consensus vote (market.py:298-304), ballot+popcount
 //                          over (agent tile x market tile) blocks, LDS-collected counts.
+//   reestimate_consensus_votes / reestimate_agreement_votes
+//                          the single-read iteration: pass 1 also records every cell's vote
+//                          (P >= 0.5) as one bit, 64 markets per word, plus the consensus
+//                          votes and resolved masks per word; pass 2 then counts agreement
+//                          from the bits (A*M/8 bytes) instead of re-reading P (8*A*M).
 #include "bce_device.hpp"
 #include "bce_internal.hpp"
 
@@ -136,6 +141,94 @@ __global__ __launch_bounds__(256) void reestimate_agreement_kernel(const double*
                                            (unsigned long long)cntS[tid]);
 }
 
+// Pass 1 with votes.  Lane per market column m = 256*block + tid, so wave w of a block
+// covers the 64 markets of vote word k = 4*block + w.  Agents are streamed kVoteRows rows
+// at a time (coalesced 512-B row segments); the rows' vote ballots are spread over lanes
+// 0..kVoteRows-1 and stored as contiguous bytes of vote_bits[k][a ..].  Every lane also
+// carries the total weight in agent order (core.py:107-120: the same for every column,
+// and free beside the stream), so no separate reduction launch is needed.
+constexpr int kVoteRows = 16;
+__global__ __launch_bounds__(256) void reestimate_consensus_votes_kernel(
+    const double* __restrict__ P, int64_t A, int64_t M, int64_t ld, const double* __restrict__ w,
+    double* __restrict__ cons, uint8_t* __restrict__ null_out, unsigned long long* __restrict__ vote_bits,
+    unsigned long long* __restrict__ cvote_words, unsigned long long* __restrict__ ok_words) {
+  const int lane = lane_id();
+  const int64_t m = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t k = m >> 6;
+  if ((k << 6) >= M) return;  // whole wave past the last market (wave-uniform)
+  const bool in = m < M;
+  double ws = 0.0, total = 0.0;
+  const double* col = P + (in ? m : 0);
+  unsigned long long* vb = vote_bits + k * A;
+  int64_t a = 0;
+  for (; a + kVoteRows <= A; a += kVoteRows) {
+    double v[kVoteRows];
+#pragma unroll
+    for (int q = 0; q < kVoteRows; ++q) v[q] = in ? col[(a + q) * ld] : 0.0;
+    unsigned long long mine = 0;
+#pragma unroll
+    for (int q = 0; q < kVoteRows; ++q) {
+      const double wq = w[a + q];
+      ws += (0.0 + v[q]) * wq;  // avg of one signal = 0 + p (core.py:116,136)
+      total += wq;
+      const unsigned long long b = ballot(in && v[q] >= 0.5);  // market.py:298-299
+      mine = (lane == q) ? b : mine;
+    }
+    if (lane < kVoteRows) vb[a + lane] = mine;
+  }
+  for (; a < A; ++a) {
+    const double v = in ? col[a * ld] : 0.0;
+    ws += (0.0 + v) * w[a];
+    total += w[a];
+    const unsigned long long b = ballot(in && v >= 0.5);
+    if (lane == 0) vb[a] = b;
+  }
+  const bool isnull = (total == 0.0);
+  const double c = isnull ? 0.0 : ws / total;
+  if (in) {
+    cons[m] = c;
+    null_out[m] = isnull ? 1 : 0;
+  }
+  const unsigned long long okw = ballot(in && !isnull);
+  const unsigned long long cvw = ballot(in && !isnull && c >= 0.5);
+  if (lane == 0) {
+    ok_words[k] = okw;
+    cvote_words[k] = cvw;
+  }
+}
+
+// Pass 2 from the vote bits: lane per agent, a block's 4 waves = 256 agents, blockIdx.y =
+// a slice of the vote words; agree[a] += popc(ok & ~(vote ^ cvote)) per word.  The first
+// agent block also counts the resolved markets of its slice.  (Exact, order-free.)
+constexpr int kVoteUnroll = 8;
+__global__ __launch_bounds__(256) void reestimate_agreement_votes_kernel(
+    const unsigned long long* __restrict__ vote_bits, int64_t A, int64_t K,
+    const unsigned long long* __restrict__ cvote_words, const unsigned long long* __restrict__ ok_words,
+    long long* __restrict__ agree, long long* __restrict__ resolved) {
+  const int64_t a = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t per = (K + gridDim.y - 1) / gridDim.y;
+  const int64_t k0 = blockIdx.y * per;
+  const int64_t k1 = (K < k0 + per) ? K : k0 + per;
+  const bool in = a < A;
+  const unsigned long long* col = vote_bits + (in ? a : 0);
+  long long acc = 0;
+  int64_t k = k0;
+  for (; k + kVoteUnroll <= k1; k += kVoteUnroll) {
+    unsigned long long x[kVoteUnroll];
+#pragma unroll
+    for (int q = 0; q < kVoteUnroll; ++q) x[q] = in ? col[(k + q) * A] : 0ull;
+#pragma unroll
+    for (int q = 0; q < kVoteUnroll; ++q) acc += __popcll(ok_words[k + q] & ~(x[q] ^ cvote_words[k + q]));
+  }
+  for (; k < k1; ++k) acc += __popcll(ok_words[k] & ~((in ? col[k * A] : 0ull) ^ cvote_words[k]));
+  if (in && acc) atomicAdd(reinterpret_cast<unsigned long long*>(&agree[a]), (unsigned long long)acc);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    long long r = 0;
+    for (int64_t q = k0; q < k1; ++q) r += __popcll(ok_words[q]);
+    if (r) atomicAdd(reinterpret_cast<unsigned long long*>(resolved), (unsigned long long)r);
+  }
+}
+
 __global__ void reestimate_weights_kernel(int64_t A, const long long* agree, const long long* resolved,
                                           double* w) {
   for (int64_t a = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; a < A;
@@ -202,4 +295,41 @@ extern "C" int bce_reestimate_weights(int64_t A, const int64_t* agreement, const
                      as_stream(stream), A, reinterpret_cast<const long long*>(agreement),
                      reinterpret_cast<const long long*>(resolved), w);
   return check_launch("reestimate_weights_kernel");
+}
+
+extern "C" int bce_reestimate_consensus_votes(const double* P, int64_t A, int64_t M, int64_t ld,
+                                              const double* w, double* consensus, uint8_t* null_out,
+                                              uint64_t* vote_bits, uint64_t* cvote_words,
+                                              uint64_t* ok_words, void* stream) {
+  BCE_REQUIRE(A > 0 && M >= 0 && ld >= M, "reestimate_votes: bad shape");
+  if (M == 0) return BCE_OK;
+  BCE_REQUIRE(P && w && consensus && null_out && vote_bits && cvote_words && ok_words,
+              "reestimate_votes: NULL argument");
+  hipLaunchKernelGGL(reestimate_consensus_votes_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0,
+                     as_stream(stream), P, A, M, ld, w, consensus, null_out,
+                     reinterpret_cast<unsigned long long*>(vote_bits), reinterpret_cast<unsigned long long*>(cvote_words),
+                     reinterpret_cast<unsigned long long*>(ok_words));
+  return check_launch("reestimate_consensus_votes_kernel");
+}
+
+extern "C" int bce_reestimate_agreement_votes(const uint64_t* vote_bits, int64_t A, int64_t M,
+                                              const uint64_t* cvote_words, const uint64_t* ok_words,
+                                              int64_t* agreement, int64_t* resolved, void* stream) {
+  BCE_REQUIRE(A > 0 && M >= 0, "reestimate_agreement_votes: bad shape");
+  if (M == 0) return BCE_OK;
+  BCE_REQUIRE(vote_bits && cvote_words && ok_words && agreement && resolved, "reestimate_agreement_votes: NULL");
+  const int64_t K = (M + 63) / 64;
+  const int64_t ab = (A + 255) / 256;
+  // enough blocks to fill the chip: slices of the vote words across blockIdx.y
+  int64_t ks = (4 * (int64_t)cu_count() * 8 + ab - 1) / ab;
+  if (ks > K) ks = K;
+  if (ks > 65535) ks = 65535;
+  if (ks < 1) ks = 1;
+  BCE_REQUIRE(ab < (1ll << 31), "reestimate_agreement_votes: grid too large");
+  hipLaunchKernelGGL(reestimate_agreement_votes_kernel, dim3((unsigned)ab, (unsigned)ks), dim3(256), 0,
+                     as_stream(stream), reinterpret_cast<const unsigned long long*>(vote_bits), A, K,
+                     reinterpret_cast<const unsigned long long*>(cvote_words),
+                     reinterpret_cast<const unsigned long long*>(ok_words), reinterpret_cast<long long*>(agreement),
+                     reinterpret_cast<long long*>(resolved));
+  return check_launch("reestimate_agreement_votes_kernel");
 }

@@ -257,6 +257,17 @@ int bce_reestimate_agreement(const double* P, int64_t A, int64_t M, int64_t ld,
                              int64_t* agreement, int64_t* resolved, void* stream);
 int bce_reestimate_weights(int64_t A, const int64_t* agreement, const int64_t* resolved,
                            double* w, void* stream);
+/* Single-read iteration (what batch.reestimate runs): the consensus pass above that also
+ * records the votes, then agreement from the votes alone, so P is read once per iteration.
+ * vote_bits [K][A] uint64 with K = ceil(M/64): bit j of vote_bits[k][a] = (P[a][64k+j] >= 0.5);
+ * cvote_words[k] bit j = market 64k+j is resolved and its consensus >= 0.5; ok_words[k] bit
+ * j = market 64k+j exists and is resolved.  Counts identical to bce_reestimate_agreement. */
+int bce_reestimate_consensus_votes(const double* P, int64_t A, int64_t M, int64_t ld, const double* w,
+                                   double* consensus, uint8_t* null_out, uint64_t* vote_bits,
+                                   uint64_t* cvote_words, uint64_t* ok_words, void* stream);
+int bce_reestimate_agreement_votes(const uint64_t* vote_bits, int64_t A, int64_t M, const uint64_t* cvote_words,
+                                   const uint64_t* ok_words, int64_t* agreement, int64_t* resolved,
+                                   void* stream);
 
 #ifdef __cplusplus
 }

@@ -363,6 +363,46 @@ def test_reestimate_vs_oracle_tiles(A, M, ld_pad):
     assert np.array_equal(w.cpu().numpy(), w_exp)
 
 
+@pytest.mark.parametrize("A,M", [(13, 1), (64, 63), (9, 129), (300, 4097), (13, 2), (64, 64), (9, 130), (300, 4096), (17, 190)])
+def test_reestimate_votes_match_two_pass(A, M):
+    """The single-read path (vote bits) gives the counts of the two-pass path that
+    re-reads P: ragged word edges, A not a multiple of 16, NaN cells, zero weights."""
+    import torch
+    from bayesian_engine import _native as N
+    rng = np.random.default_rng(A + M)
+    P = rng.beta(2, 2, size=(A, M))
+    P[rng.random((A, M)) < 0.01] = np.nan
+    P[:, rng.random(M) < 0.05] = 0.5
+    Pt = torch.from_numpy(P).cuda()
+    L = N.lib()
+    st = N.stream(Pt.device)
+    for w0 in (0.5, 0.0):
+        w = torch.full((A,), w0, dtype=torch.float64, device="cuda")
+        w[::3] = 0.25 if w0 else 0.0
+        c1, c2 = torch.empty(M, dtype=torch.float64, device="cuda"), torch.empty(M, dtype=torch.float64, device="cuda")
+        n1, n2 = torch.empty(M, dtype=torch.uint8, device="cuda"), torch.empty(M, dtype=torch.uint8, device="cuda")
+        g1, g2 = torch.zeros(A + 1, dtype=torch.int64, device="cuda"), torch.zeros(A + 1, dtype=torch.int64, device="cuda")
+        K = (M + 63) // 64
+        votes = torch.empty((K, A), dtype=torch.int64, device="cuda")
+        words = torch.empty((2, K), dtype=torch.int64, device="cuda")
+        N.check(L.bce_reestimate_consensus(N.ptr(Pt), A, M, M, N.ptr(w), N.ptr(c1), N.ptr(n1), st))
+        N.check(L.bce_reestimate_agreement(N.ptr(Pt), A, M, M, N.ptr(c1), N.ptr(n1), N.ptr(g1[:A]), N.ptr(g1[A:]), st))
+        N.check(L.bce_reestimate_consensus_votes(N.ptr(Pt), A, M, M, N.ptr(w), N.ptr(c2), N.ptr(n2), N.ptr(votes),
+                                                 N.ptr(words[0]), N.ptr(words[1]), st))
+        N.check(L.bce_reestimate_agreement_votes(N.ptr(votes), A, M, N.ptr(words[0]), N.ptr(words[1]),
+                                                 N.ptr(g2[:A]), N.ptr(g2[A:]), st))
+        torch.cuda.synchronize()
+        assert torch.equal(n1, n2)
+        assert np.array_equal(c1.cpu().numpy(), c2.cpu().numpy(), equal_nan=True)
+        assert torch.equal(g1, g2), (w0, g1[-1].item(), g2[-1].item())
+        # the vote bits themselves
+        vb = votes.cpu().numpy().view(np.uint64)
+        bits = ((vb[:, :, None] >> np.arange(64, dtype=np.uint64)) & np.uint64(1)).astype(bool)  # [K, A, 64]
+        exp = np.zeros((K * 64, A), bool)
+        exp[:M] = (P >= 0.5).T
+        assert np.array_equal(bits.transpose(0, 2, 1).reshape(K * 64, A), exp)
+
+
 def test_c4_replay_slice():
     """Config-4 replay through the fused replay_step kernel vs the reference trace."""
     import torch

@@ -40,7 +40,7 @@ def test_argument_errors_need_no_gpu():
                                None, None, None, None, None, None, None, None, None)
     assert rc == -1
     assert b"offsets" in lib.bce_last_error()
-    rc = lib.bce_tiebreak_csr(None, 3, None, 0, None, None, None, None, 8, 99, *([None] * 10))
+    rc = lib.bce_tiebreak_csr(None, 3, None, 0, None, None, None, None, 8, 99, *([None] * 11))
     assert rc == -1
 
 
