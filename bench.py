@@ -60,7 +60,10 @@ def parse(argv=None):
     p.add_argument("--markets", type=int, default=1_000_000)
     p.add_argument("--len", type=int, default=32)
     p.add_argument("--sources", type=int, default=10_000)
-    p.add_argument("--mode", default="exact", choices=["exact", "fast"])
+    p.add_argument("--mode", default=None, choices=["exact", "fast"],
+                   help="consensus summation mode (default: exact for c2, where it costs nothing; fast -- "
+                        "the north star's fixed-order trees within 1e-9 -- for c3, with the exact-mode "
+                        "time reported beside it)")
     p.add_argument("--agents", type=int, default=16384, help="config 5 agents")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=2.0, help="wall-clock budget of the CPU baseline")
@@ -312,7 +315,7 @@ def bench_c2(args, world, rank):
     stream = torch.cuda.current_stream(dev)
 
     def step():
-        batch.consensus(d_off, d_sid, d_prob, table, max_len=L, mode=args.mode, out=res)
+        batch.consensus(d_off, d_sid, d_prob, table, max_len=L, mode=args.mode or "exact", out=res)
 
     wall, avg_kernel_s, prewarm = timed_loop(step, args, world, stream)
     N.check_faults(dev, "c2 timed steps")  # a kernel that gave up would leave stale outputs
@@ -344,7 +347,7 @@ def bench_c2(args, world, rank):
         "dtype": "f64",
         "data": "synthetic (SURVEY.md d2 distributions, PCG64 seed 2+rank)",
         "config": {"workload": f"c2: {M} markets x {L} signals, {S} sources, batched consensus + "
-                               f"validation + sourceWeights outputs, mode={args.mode}",
+                               f"validation + sourceWeights outputs, mode={args.mode or 'exact'}",
                    "markets_per_gpu": M, "signals_per_market": L, "sources": S,
                    "parallelism": f"markets sharded, {world} independent rank(s), no collective"},
         "world_size": world,
