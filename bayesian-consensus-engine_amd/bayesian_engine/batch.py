@@ -184,12 +184,17 @@ def _alloc(M: int, Nsig: int, dev, unique: bool, validate: bool) -> ConsensusRes
 
 def consensus(offsets: torch.Tensor, sid: torch.Tensor, prob: torch.Tensor, table: SourceTable, *,
               plan: Optional[Plan] = None, max_len: Optional[int] = None, mode: str = "exact",
-              unique_outputs: bool = True, validate: bool = True,
+              unique_outputs: bool = True, validate: bool = True, check: bool = False,
               out: Optional[ConsensusResult] = None) -> ConsensusResult:
     """core.compute_consensus for every CSR market (+ the validation range check).
 
     Pass ``max_len`` (<= 64: one launch, no planning) or a prebuilt :class:`Plan` for
     ragged batches; with neither, a plan is built from a host copy of ``offsets``.
+
+    Raw CSR is trusted for speed: a ``sid`` outside ``[0, table.n)`` has its row read
+    clamped and a market longer than ``max_len`` is left unprocessed; either raises the
+    device fault word.  ``check=True`` synchronises and raises :class:`BCEError` for it
+    (otherwise call ``_native.check_faults()`` when convenient).
     """
     L = N.require_gpu()
     M = offsets.numel() - 1
@@ -204,6 +209,8 @@ def consensus(offsets: torch.Tensor, sid: torch.Tensor, prob: torch.Tensor, tabl
     if plan is None and max_len is not None and 0 < max_len <= 64:
         rc = L.bce_consensus_csr(*common, N.ptr(None), 0, int(max_len), md, *outs, N.stream(dev))
         N.check(rc, "bce_consensus_csr")
+        if check:
+            N.check_faults(dev, "consensus")
         return res
     if plan is None:
         plan = Plan.build(offsets.cpu().numpy(), dev)
@@ -211,6 +218,8 @@ def consensus(offsets: torch.Tensor, sid: torch.Tensor, prob: torch.Tensor, tabl
     rc = L.bce_consensus_planned(*common, N.ptr(plan.order), N.ptr(plan.bin_start), md, *outs,
                                  N.ptr(plan.scratch), sb, N.stream(dev))
     N.check(rc, "bce_consensus_planned")
+    if check:
+        N.check_faults(dev, "consensus")
     return res
 
 

@@ -274,6 +274,40 @@ def test_fault_word_reports_bad_sid_and_long_market():
         N.check_faults()
 
 
+@pytest.mark.parametrize("mode", ["exact", "fast"])
+def test_fault_word_wide_kernel(mode):
+    """The wide kernel (64 < n <= 4096) reports a bad sid and a market longer than the
+    launch's max_len; batch.consensus(check=True) raises it directly."""
+    from bayesian_engine import _native as N, batch
+    rng = np.random.default_rng(77)
+    lens = rng.integers(65, 900, 50)
+    off = np.zeros(len(lens) + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    S = 3000
+    sid = rng.integers(0, S, off[-1]).astype(np.int32)
+    prob = rng.random(off[-1])
+    table = batch.SourceTable.from_arrays(_dev(rng.random(S)), _dev(rng.random(S)), _dev(np.ones(S, np.uint8)))
+    N.check_faults()
+    bad = sid.copy()
+    bad[int(off[7]) + 3] = S + 5
+    with pytest.raises(N.BCEError, match="n_sources"):
+        batch.consensus(_dev(off), _dev(bad, np.int32), _dev(prob), table, max_len=1024, mode=mode, check=True)
+    N.check_faults()  # cleared
+    # markets of 900 > 512: launched as one wide launch sized for 512
+    L = N.lib()
+    d_off, d_sid, d_prob = _dev(off), _dev(sid, np.int32), _dev(prob)
+    res = batch._alloc(len(lens), int(off[-1]), d_off.device, True, True)
+    rc = L.bce_consensus_csr(N.ptr(d_off), len(lens), N.ptr(d_sid), N.ptr(d_prob), int(off[-1]),
+                             N.ptr(table.relconf), N.ptr(table.bits), table.n, N.ptr(None), 0, 512,
+                             N.MODE_FAST if mode == "fast" else N.MODE_EXACT, N.ptr(res.consensus),
+                             N.ptr(res.confidence), N.ptr(res.total_weight), N.ptr(res.n_unique),
+                             N.ptr(res.err_idx), N.ptr(res.usid), N.ptr(res.weight), N.ptr(res.nweight),
+                             N.stream(d_off.device))
+    assert rc == 0
+    with pytest.raises(N.BCEError, match="max_len"):
+        N.check_faults()
+
+
 def test_pipe_kernel_spin_cap_reports_fault():
     """A persistent wave that exhausts its bounded wait records a fault instead of silently
     leaving its tiles unwritten (forced with a tiny cap on the pipe kernel, S = 12000)."""
