@@ -7,7 +7,7 @@
 //      registers loaded one market ahead; the next market's sids are issued right away.
 //   2. register bitonic network (flip form): stages inside a thread are min/max pairs, lane
 //      exchanges use DPP / ds_swizzle / ds_bpermute, the few stages that cross waves go
-//      through LDS rows (region B).
+//      through LDS rows (region B, two alternating buffers: one barrier per stage).
 //   3. input-order probabilities (loaded during the previous market) land in region A, are
 //      range-checked (core.py:59-60), read back in sorted order into registers and written
 //      over region A in place; run leaders get their unique index from a workgroup prefix
@@ -21,7 +21,8 @@
 //              deterministic, within the north-star 1e-9 of the reference order.
 //        EXACT: rounds of NT products staged through two LDS buffers; wave 0 carries the
 //              three left-to-right chains (core.py:120,136,142) on lanes 0..2.
-//      w[j] is parked in the dead sorted-probability slot j for normalizedWeight.
+//      normalizedWeight reads w[j] back from the weight output (or, without one, from the
+//      dead sorted-probability slot j where it was parked).
 //   5. the next market's probabilities are issued, then per-market outputs and
 //      normalizedWeight = w / total (core.py:151).
 // LDS: region A = P doubles (+ read-ahead pad), region B = max(sort exchange rows,
@@ -67,7 +68,7 @@ struct WideCfg {
   static constexpr int NT = 64 * NW;
   static constexpr int P = NT * R;
   static constexpr int IB = ilog2c(P);
-  static constexpr int XROW = R + 4;  // padded exchange row (u32)
+  static constexpr int XROW = R;      // exchange row (u32), two buffers
   static constexpr int HR = (R < BCE_WIDE_HR) ? R : BCE_WIDE_HR;
   // register budget: workgroups of >= 4 waves get 4 waves per SIMD (<= 128 VGPRs), so two
   // LDS-sized workgroups share a CU
@@ -76,7 +77,7 @@ struct WideCfg {
   // region B (u32): sort exchange rows, then leaders [P] (+ exact: chain buffers
   // [2][3][NT] doubles + the chain's read-ahead)
   static constexpr int LEAD_U32 = FAST ? P : P + 2 * (6 * NT + 32);
-  static constexpr int B_U32 = (NT * XROW > LEAD_U32) ? NT * XROW : LEAD_U32;
+  static constexpr int B_U32 = (2 * NT * XROW > LEAD_U32) ? 2 * NT * XROW : LEAD_U32;
 };
 
 // v from lane ^ M (whole wave) for the masks the flip-form sort uses.
@@ -91,13 +92,24 @@ __device__ __forceinline__ unsigned lane_xor(unsigned v) {
   else return (unsigned)__shfl_xor((int)v, M);  // 32, 63: ds_bpermute
 }
 
+// Index of wave-crossing stage (K, J) among the network's wave-crossing stages (they
+// alternate between two exchange buffers, so each needs one barrier, not two).
+constexpr int xw_index(int K, int J, int R) {
+  int idx = 0;
+  for (int k = 2; k < K; k <<= 1)
+    for (int j = k / 2; j >= 1; j >>= 1)
+      if ((j == k / 2) ? (k > 64 * R) : (j >= 64 * R)) ++idx;
+  for (int j = K / 2; j > J; j >>= 1)
+    if ((j == K / 2) ? (K > 64 * R) : (j >= 64 * R)) ++idx;
+  return idx;
+}
+
 // One stage of the flip-form bitonic network over P = 64*NW*R keys, position q = t*R + r:
 // the first stage of merge K pairs q with q ^ (K-1), the others pair q with q ^ J, and the
 // lower position always keeps the minimum -- no direction bits anywhere.
 template <int NW, int R, int K, int J>
 __device__ __forceinline__ void wide_stage(unsigned (&key)[R], unsigned* sX, int t, int lane) {
   constexpr bool flip = (J == K / 2);
-  constexpr int XROW = R + 4;
   if constexpr (flip ? (K <= R) : (J < R)) {  // inside a thread: min/max pairs
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -116,18 +128,19 @@ __device__ __forceinline__ void wide_stage(unsigned (&key)[R], unsigned* sX, int
     for (int r = 0; r < R; ++r) y[r] = lane_xor<MK>(key[flip ? R - 1 - r : r]);
 #pragma unroll
     for (int r = 0; r < R; ++r) key[r] = ((key[r] < y[r]) == lower) ? key[r] : y[r];
-  } else {  // across waves, through LDS rows
+  } else {  // across waves, through LDS rows; buffers alternate, so the previous reads
+            // of this buffer finished before the last stage's barrier
     constexpr int MT = flip ? (K / R - 1) : (J / R);
+    unsigned* const buf = sX + (xw_index(K, J, R) & 1) * (64 * NW * R);
     const bool lower = (t & (flip ? (K / R / 2) : MT)) == 0;
-    __syncthreads();
 #pragma unroll
     for (int r = 0; r < R; r += 4)
-      *reinterpret_cast<uint4*>(sX + t * XROW + r) = make_uint4(key[r], key[r + 1], key[r + 2], key[r + 3]);
+      *reinterpret_cast<uint4*>(buf + t * R + r) = make_uint4(key[r], key[r + 1], key[r + 2], key[r + 3]);
     __syncthreads();
     unsigned y[R];
 #pragma unroll
     for (int r = 0; r < R; r += 4) {
-      const uint4 y4 = *reinterpret_cast<const uint4*>(sX + (t ^ MT) * XROW + r);
+      const uint4 y4 = *reinterpret_cast<const uint4*>(buf + (t ^ MT) * R + r);
       y[r] = y4.x;
       y[r + 1] = y4.y;
       y[r + 2] = y4.z;
@@ -148,11 +161,26 @@ __device__ __forceinline__ void wide_sort(unsigned (&key)[R], unsigned* sX, int 
   if constexpr (K < 64 * NW * R) wide_sort<NW, R, 2 * K>(key, sX, t, lane);
 }
 
-// Fixed xor butterfly: every lane ends with the same, run-independent sum.
+// One fixed-order sum over the wave, returned in every lane: DPP rotations inside each
+// 16-lane row and quad swaps (no LDS round trips), then the four row sums in row order.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)__double_as_longlong(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)((uint64_t)__double_as_longlong(v) >> 32), CTRL, 0xF, 0xF,
+                                          false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane((int)(uint32_t)__double_as_longlong(v), l);
+  const int hi = __builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)__double_as_longlong(v) >> 32), l);
+  return __hiloint2double(hi, lo);
+}
 __device__ __forceinline__ double wave_sum_fixed(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = v + __shfl_xor(v, o);
-  return v;
+  v = v + dpp_f64<0x128>(v);  // row_ror:8
+  v = v + dpp_f64<0x124>(v);  // row_ror:4
+  v = v + dpp_f64<0x4E>(v);   // quad_perm 2,3,0,1
+  v = v + dpp_f64<0xB1>(v);   // quad_perm 1,0,3,2
+  return (readlane_f64(v, 0) + readlane_f64(v, 16)) + (readlane_f64(v, 32) + readlane_f64(v, 48));
 }
 
 // builtin sum() from 0 over a run of len sorted probabilities in input order (core.py:116);
@@ -204,6 +232,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
   const int lane = lane_id();
   const int wv = t >> 6;
   const unsigned smax = (unsigned)(a.n_sources > 0 ? a.n_sources - 1 : 0);
+  // normalizedWeight reads w[j] back from the weight output (this thread's own stores)
+  // when there is one; else w[j] is parked in region A (dead sorted-prob slot j)
+  const bool wback = a.weight != nullptr;
 #if BCE_WIDE_PROF
   unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prof_t = __builtin_amdgcn_s_memtime();
 #endif
@@ -272,7 +303,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
     if (ballot(badsid)) raise_fault(a.fault, kFaultSid);
     int myerr = kNoErr;
     if constexpr (BCE_WIDE_EARLY) {  // input-order probs into region A before the next loads
-      if constexpr (NW > 1) __syncthreads();  // the previous market's readers of region A are done
+      // region A's last readers are the previous market's run sums (before its final
+      // barrier) unless normalizedWeight reads w[j] from it (no weight output)
+      if (NW > 1 && !wback) __syncthreads();
 #pragma unroll
       for (int c = 0; c < R; ++c) {
         const int i = c * NT + t;
@@ -421,11 +454,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
           pa += va[i];
           pc += vc[i];
         }
-        __syncthreads();  // every sorted-prob read of this group done
+        if (!wback) {
+          __syncthreads();  // every sorted-prob read of this group done
 #pragma unroll
-        for (int i = 0; i < HR; ++i) {
-          const int jj = (h + i) * NT + t;
-          if (jj < u) sA[jj] = vw[i];  // later groups read only slots > jj
+          for (int i = 0; i < HR; ++i) {
+            const int jj = (h + i) * NT + t;
+            if (jj < u) sA[jj] = vw[i];  // later groups read only slots > jj
+          }
         }
       } else {
 #pragma unroll
@@ -438,7 +473,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
             __syncthreads();  // round staged; every sorted-prob read of this group is done
             WMARK(4);
             const int jj = (h + i) * NT + t;
-            if (jj < u) sA[jj] = vw[i];  // slot jj is only read by uniques <= jj
+            if (jj < u && !wback) sA[jj] = vw[i];  // slot jj is only read by uniques <= jj
             if (wv == 0) {
               // Full 8-term steps run in asm: two 4-term batches in fixed registers, each
               // reloaded right after its adds, so one batch's LDS latency hides under the
@@ -544,7 +579,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
       if (a.err_idx) a.err_idx[m] = (sErr == kNoErr) ? -1 : sErr;
     }
     if (a.nweight)  // core.py:151
-      for (int jj = t; jj < u; jj += NT) a.nweight[off + jj] = (tw > 0.0) ? sA[jj] / tw : 0.0;
+      for (int jj = t; jj < u; jj += NT) {
+        const double wj = wback ? a.weight[off + jj] : sA[jj];
+        a.nweight[off + jj] = (tw > 0.0) ? wj / tw : 0.0;
+      }
     WMARK(6);
   }
 #if BCE_WIDE_PROF

@@ -91,6 +91,32 @@ def test_wide_key_limit_and_fallback():
         _check(g, "fast")
 
 
+@pytest.mark.parametrize("mode", MODES)
+def test_wide_nweight_without_weight_output(mode):
+    """normalizedWeight requested without the weight output (w[j] parked in LDS instead of
+    read back from the weight array)."""
+    from bayesian_engine import _native as N, batch
+    rng = np.random.default_rng(31)
+    lens = rng.integers(65, 4097, 60)
+    g = _zipf_case(lens, 50000, 31, bad=False)
+    exp = orc.consensus_csr(g["offsets"], g["sid"], g["prob"], g["rel"], g["conf"], g["present"])
+    table = batch.SourceTable.from_arrays(_dev(g["rel"]), _dev(g["conf"]), _dev(g["present"]))
+    M, n = len(lens), int(g["offsets"][-1])
+    off, sid, prob = _dev(g["offsets"]), _dev(g["sid"], np.int32), _dev(g["prob"])
+    res = batch._alloc(M, n, off.device, True, True)
+    L = N.lib()
+    rc = L.bce_consensus_csr(N.ptr(off), M, N.ptr(sid), N.ptr(prob), n, N.ptr(table.relconf), N.ptr(table.bits),
+                             table.n, N.ptr(None), 0, int(lens.max()), N.MODE_FAST if mode == "fast" else N.MODE_EXACT,
+                             N.ptr(res.consensus), N.ptr(res.confidence), N.ptr(res.total_weight), N.ptr(res.n_unique),
+                             N.ptr(res.err_idx), N.ptr(res.usid), N.ptr(None), N.ptr(res.nweight), N.stream(off.device))
+    assert rc == 0, L.bce_last_error()
+    torch.cuda.synchronize()
+    out = {k: getattr(res, k).cpu().numpy() for k in ("consensus", "confidence", "total_weight", "n_unique",
+                                                      "err_idx", "usid", "nweight")}
+    out["weight"] = exp["weight"]  # not written by this launch
+    _compare_vec(out, exp, g["offsets"], exact=(mode == "exact"))
+
+
 def test_wide_direct_csr_unplanned():
     """bce_consensus_csr with max_len in (64, 4096]: every market (short ones too) goes
     through one wide launch sized by max_len."""

@@ -25,14 +25,8 @@ SRCS = ["capi.hip", "consensus.hip", "consensus_tab.hip", "consensus_wide.hip", 
         "stats.hip", "aggregate.hip"]
 
 VARIANTS = {
-    "m0": ["-DBCE_WIDE_MAP=0"],
-    "m0_late": ["-DBCE_WIDE_MAP=0", "-DBCE_WIDE_EARLY=0"],
-    "m1hr4": ["-DBCE_WIDE_MAP=1", "-DBCE_WIDE_HR=4"],
-    "m1hr2": ["-DBCE_WIDE_MAP=1", "-DBCE_WIDE_HR=2"],
-    "m2hr2": ["-DBCE_WIDE_MAP=2", "-DBCE_WIDE_HR=2"],
-    "m2hr4": ["-DBCE_WIDE_MAP=2", "-DBCE_WIDE_HR=4"],
-    "m2hr2_prof": ["-DBCE_WIDE_MAP=2", "-DBCE_WIDE_HR=2", "-DBCE_WIDE_PROF=1"],
-    "m1hr2_prof": ["-DBCE_WIDE_MAP=1", "-DBCE_WIDE_HR=2", "-DBCE_WIDE_PROF=1"],
+    "base": [],
+    "prof": ["-DBCE_WIDE_PROF=1"],
 }
 PHASES = ["keys+next sids", "sort", "probs+leaders", "per-unique", "stage barrier", "chain", "tail"]
 
