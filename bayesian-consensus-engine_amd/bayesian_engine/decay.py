@@ -10,7 +10,8 @@ The early returns for ``elapsed <= 0`` hand back the caller's own object, as the
 reference does (decay.py:52-53, 90-91).
 
 Parity note: the reference's ``2.0 ** x`` is glibc ``pow``, which is itself not
-correctly rounded for ~0.09% of inputs (measured); the GPU's ``pow`` agrees to <= 1 ulp,
+correctly rounded for ~0.09% of inputs (measured); the GPU computes ``2.0 ** x`` as ocml
+``exp2(x)`` (<= 1 ulp), held to 2 ulp of the reference with the exact-match rate asserted,
 far inside the north-star tolerance (1e-9 absolute).  See DESIGN.md §3.
 """
 from __future__ import annotations

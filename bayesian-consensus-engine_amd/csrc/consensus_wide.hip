@@ -40,12 +40,6 @@
 #ifndef BCE_WIDE_WPE
 #define BCE_WIDE_WPE 2  // min waves per SIMD (register budget)
 #endif
-#ifndef BCE_WIDE_EARLY
-#define BCE_WIDE_EARLY 1  // next market's probabilities issued with its sids (1) or after the gathers (0)
-#endif
-#ifndef BCE_WIDE_MAP
-#define BCE_WIDE_MAP 1  // (NW, R) per key-bit width: 0 = R 16 from P 1024, 1 = R 8 from P 1024, 2 = R 4 from P 1024
-#endif
 #ifndef BCE_WIDE_PROF
 #define BCE_WIDE_PROF 0  // experiment builds only (tools/wide_variants.py): per-phase s_memtime
 #endif
@@ -233,8 +227,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
   const int wv = t >> 6;
   const unsigned smax = (unsigned)(a.n_sources > 0 ? a.n_sources - 1 : 0);
   // normalizedWeight reads w[j] back from the weight output (this thread's own stores)
-  // when there is one; else w[j] is parked in region A (dead sorted-prob slot j)
-  const bool wback = a.weight != nullptr;
+  // in workgroups of several waves (it saves their barriers); a single wave parks w[j] in
+  // region A (dead sorted-prob slot j), which is faster than the global round trip.
+  const bool wback = (NW > 1) && a.weight != nullptr;
 #if BCE_WIDE_PROF
   unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prof_t = __builtin_amdgcn_s_memtime();
 #endif
@@ -302,27 +297,25 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
     }
     if (ballot(badsid)) raise_fault(a.fault, kFaultSid);
     int myerr = kNoErr;
-    if constexpr (BCE_WIDE_EARLY) {  // input-order probs into region A before the next loads
-      // region A's last readers are the previous market's run sums (before its final
-      // barrier) unless normalizedWeight reads w[j] from it (no weight output)
-      if (NW > 1 && !wback) __syncthreads();
+    // input-order probs into region A before the next loads; region A's last readers are
+    // the previous market's run sums (before its final barrier) unless normalizedWeight
+    // reads w[j] from it
+    if (NW > 1 && !wback) __syncthreads();
 #pragma unroll
-      for (int c = 0; c < R; ++c) {
-        const int i = c * NT + t;
-        const double p = pp[c];
-        sA[i] = p;
-        if ((i < n) && (p < 0.0 || p > 1.0) && myerr == kNoErr) myerr = i;  // core.py:59-60
-      }
+    for (int c = 0; c < R; ++c) {
+      const int i = c * NT + t;
+      const double p = pp[c];
+      sA[i] = p;
+      if ((i < n) && (p < 0.0 || p > 1.0) && myerr == kNoErr) myerr = i;  // core.py:59-60
     }
     const bool has_next = li + G < a.n_list;
     if (has_next) {
       meta(li + G);
       load_sids();
-      if constexpr (BCE_WIDE_EARLY) load_probs();
+      load_probs();
     }
     if (n > P) {  // longer than this launch's max_len: left unprocessed, reported
       raise_fault(a.fault, kFaultTooLong);
-      if (!BCE_WIDE_EARLY && has_next) load_probs();
       continue;
     }
     if (t == 0) sErr = kNoErr;
@@ -333,15 +326,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
     WMARK(1);
 
     // ---- 3. input-order probs + range check, sorted probs in place, leaders ----------
-    if constexpr (!BCE_WIDE_EARLY) {
-#pragma unroll
-      for (int c = 0; c < R; ++c) {
-        const int i = c * NT + t;
-        const double p = pp[c];
-        sA[i] = p;
-        if ((i < n) && (p < 0.0 || p > 1.0) && myerr == kNoErr) myerr = i;  // core.py:59-60
-      }
-    }
     if (lane == 63) sLast[wv] = key[R - 1];
     __syncthreads();  // (a) input-order probs + sLast visible; exchange rows dead
     if (myerr != kNoErr) atomicMin(&sErr, myerr);
@@ -415,6 +399,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
           }
         }
       }
+#if BCE_WIDE_PROF
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // diagnostic: gather latency as its own phase
+      WMARK(7);
+#endif
       double vw[HR], va[HR], vc[HR];
 #pragma unroll
       for (int i = 0; i < HR; ++i) {
@@ -547,7 +535,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
     }
 
     // ---- 5. next market's probabilities; totals, per-market outputs, nweight ---------
-    if (!BCE_WIDE_EARLY && has_next) load_probs();
     if constexpr (FAST) {
       pw = wave_sum_fixed(pw);
       pa = wave_sum_fixed(pa);
@@ -587,7 +574,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
   }
 #if BCE_WIDE_PROF
   if (lane_id() == 0)
-    for (int k = 0; k < 7; ++k) atomicAdd(&g_wide_prof[k], prof[k]);
+    for (int k = 0; k < 8; ++k) atomicAdd(&g_wide_prof[k], prof[k]);
 #endif
 }
 
@@ -617,22 +604,10 @@ int launch_wide_mode(int ib, const ConsArgs& a, hipStream_t st) {
   switch (ib) {
     case 7: return launch_wide<1, 2, FAST>(a, st);
     case 8: return launch_wide<1, 4, FAST>(a, st);
-#if BCE_WIDE_MAP == 0
-    case 9: return launch_wide<1, 8, FAST>(a, st);
-    case 10: return launch_wide<1, 16, FAST>(a, st);
-    case 11: return launch_wide<2, 16, FAST>(a, st);
-    default: return launch_wide<4, 16, FAST>(a, st);
-#elif BCE_WIDE_MAP == 1
     case 9: return launch_wide<1, 8, FAST>(a, st);
     case 10: return launch_wide<2, 8, FAST>(a, st);
     case 11: return launch_wide<4, 8, FAST>(a, st);
     default: return launch_wide<8, 8, FAST>(a, st);
-#else
-    case 9: return launch_wide<2, 4, FAST>(a, st);
-    case 10: return launch_wide<4, 4, FAST>(a, st);
-    case 11: return launch_wide<8, 4, FAST>(a, st);
-    default: return launch_wide<16, 4, FAST>(a, st);
-#endif
   }
 }
 

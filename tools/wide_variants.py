@@ -28,7 +28,8 @@ VARIANTS = {
     "base": [],
     "prof": ["-DBCE_WIDE_PROF=1"],
 }
-PHASES = ["keys+next sids", "sort", "probs+leaders", "per-unique", "stage barrier", "chain", "tail"]
+PHASES = ["keys+next sids", "sort", "probs+leaders", "run sums+products+stores", "stage barrier", "chain", "tail",
+          "gather wait"]
 
 
 def build(names):
@@ -86,7 +87,7 @@ def one(name, mode, reps):
     out = {"variant": name, "mode": mode, "median_ms": ms[len(ms) // 2], "min_ms": ms[0]}
     if prof:
         lib.bce_wide_prof_read(buf)
-        v = list(buf)[:7]
+        v = list(buf)[:8]
         lens = np.diff(off)
         wide = int(((lens > 64) & (lens <= 4096)).sum())
         tot = sum(v)
