@@ -6,8 +6,9 @@
 //   1. keys (sid << IB | input index, 32 bits; needs n_sources <= 2^(32-IB)) from the sid
 //      registers loaded one market ahead; the next market's sids are issued right away.
 //   2. register bitonic network (flip form): stages inside a thread are min/max pairs, lane
-//      exchanges use DPP / ds_swizzle / ds_bpermute, the few stages that cross waves go
-//      through LDS rows (region B, two alternating buffers: one barrier per stage).
+//      exchanges are VALU only (DPP in rows, v_permlane16/32_swap across rows and halves),
+//      the few stages that cross waves go through LDS rows (region B, two alternating
+//      buffers: one barrier per stage).
 //   3. input-order probabilities (loaded during the previous market) land in region A, are
 //      range-checked (core.py:59-60), read back in sorted order into registers and written
 //      over region A in place; run leaders get their unique index from a workgroup prefix
@@ -74,16 +75,47 @@ struct WideCfg {
   static constexpr int B_U32 = (2 * NT * XROW > LEAD_U32) ? 2 * NT * XROW : LEAD_U32;
 };
 
-// v from lane ^ M (whole wave) for the masks the flip-form sort uses.
+// v from lane ^ M (whole wave) for the masks the flip-form sort uses -- all VALU, no LDS
+// round trip: DPP for the in-row patterns, the CDNA4 half-exchanges v_permlane16_swap /
+// v_permlane32_swap (plus a lane select) across rows and halves.
 template <int M>
 __device__ __forceinline__ unsigned lane_xor(unsigned v) {
+  const int lane = lane_id();
   if constexpr (M == 1) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
   else if constexpr (M == 2) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // 2,3,0,1
   else if constexpr (M == 3) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x1B, 0xF, 0xF, false);  // 3,2,1,0
-  else if constexpr (M == 7) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false); // row_half_mirror
-  else if constexpr (M == 15) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false);  // row_mirror
-  else if constexpr (M < 32) return (unsigned)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (M << 10));  // bitmask xor
-  else return (unsigned)__shfl_xor((int)v, M);  // 32, 63: ds_bpermute
+  else if constexpr (M == 4) {  // row_ror:N reads lane (l - N) mod 16: bit 2 set -> ror 4, clear -> ror 12
+    const unsigned a = (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xF, 0xF, false);
+    const unsigned b = (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x12C, 0xF, 0xF, false);
+    return (lane & 4) ? a : b;
+  } else if constexpr (M == 7) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  else if constexpr (M == 8) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false);    // row_ror:8
+  else if constexpr (M == 15) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false);   // row_mirror
+  else if constexpr (M == 16) {  // odd rows <-> even rows
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return (lane & 16) ? r[0] : r[1];
+  } else if constexpr (M == 32) {  // upper half <-> lower half
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return (lane & 32) ? r[0] : r[1];
+  } else if constexpr (M == 31) {  // l ^ 31 = (l ^ 16) ^ 15
+    return (unsigned)__builtin_amdgcn_mov_dpp((int)lane_xor<16>(v), 0x140, 0xF, 0xF, false);
+  } else if constexpr (M == 63) {  // l ^ 63 = (l ^ 32) ^ 31
+    return lane_xor<31>(lane_xor<32>(v));
+  } else {
+    static_assert(M == 1, "unsupported lane distance");
+    return v;
+  }
+}
+
+// Inclusive prefix sum over the wave with DPP (GFX9 row shifts + row broadcasts).
+__device__ __forceinline__ int wave_incl_scan(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+  return x;
 }
 
 // Index of wave-crossing stage (K, J) among the network's wave-crossing stages (they
@@ -335,7 +367,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
       const int q = t * R + r;
       x[r] = (q < n) ? sA[key[r] & QMASK] : 0.0;
     }
-    const unsigned prev_in_wave = (unsigned)__shfl_up((int)key[R - 1], 1);
+    const unsigned prev_in_wave = (unsigned)__builtin_amdgcn_update_dpp(0, (int)key[R - 1], 0x138, 0xF, 0xF, false);  // wave_shr:1
     const unsigned prev_key = (lane > 0) ? prev_in_wave : (wv > 0 ? sLast[wv - 1] : 0u);
     unsigned lead = 0;
 #pragma unroll
@@ -346,12 +378,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
       lead |= is ? (1u << r) : 0u;
     }
     const int cnt = __popc(lead);
-    int incl = cnt;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int y = __shfl_up(incl, d);
-      if (lane >= d) incl += y;
-    }
+    const int incl = wave_incl_scan(cnt);
     if (lane == 63) sCnt[wv] = incl;
     __syncthreads();  // (b) every read of the input-order probs done; counts visible
 #pragma unroll
@@ -391,7 +418,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
         if (jj < u) {
           const unsigned lv = sLead[jj];
           q0s[i] = (int)(lv & QMASK);
-          sids[i] = lv >> IB;  // <= smax by construction of the key
+          sids[i] = min(lv >> IB, smax);  // <= smax by construction of the key; clamped anyway
           q1s[i] = (jj + 1 < u) ? (int)(sLead[jj + 1] & QMASK) : n;
           if (a.n_sources > 0) {
             rc[i] = a.relconf[sids[i]];
@@ -621,6 +648,34 @@ extern "C" int bce_wide_prof_read(unsigned long long* host8) {
   return BCE_OK;
 }
 #endif
+
+namespace {
+__global__ void lane_xor_selftest_kernel(unsigned* out) {
+  const unsigned l = (unsigned)lane_id();
+  out[0 * 64 + l] = lane_xor<1>(l);
+  out[1 * 64 + l] = lane_xor<2>(l);
+  out[2 * 64 + l] = lane_xor<3>(l);
+  out[3 * 64 + l] = lane_xor<4>(l);
+  out[4 * 64 + l] = lane_xor<7>(l);
+  out[5 * 64 + l] = lane_xor<8>(l);
+  out[6 * 64 + l] = lane_xor<15>(l);
+  out[7 * 64 + l] = lane_xor<16>(l);
+  out[8 * 64 + l] = lane_xor<31>(l);
+  out[9 * 64 + l] = lane_xor<32>(l);
+  out[10 * 64 + l] = lane_xor<63>(l);
+  out[11 * 64 + l] = (unsigned)wave_incl_scan((int)l + 1);
+  out[12 * 64 + l] = (unsigned)__builtin_amdgcn_update_dpp(0, (int)l + 100, 0x138, 0xF, 0xF, false);  // wave_shr:1
+}
+}  // namespace
+
+// Self-test of the sort's lane exchanges and the wave scan (one wave, touches only `out`):
+// out[q*64 + l] must equal l ^ {1,2,3,4,7,8,15,16,31,32,63}[q], out[11*64 + l] = (l+1)(l+2)/2,
+// out[12*64 + l] = l + 99 (lane l-1's l+100; 0 in lane 0).  `out` holds 13*64 words.
+extern "C" int bce_debug_lane_selftest(unsigned* out, void* stream) {
+  BCE_REQUIRE(out, "lane_selftest: NULL");
+  hipLaunchKernelGGL(lane_xor_selftest_kernel, dim3(1), dim3(64), 0, as_stream(stream), out);
+  return check_launch("lane_xor_selftest_kernel");
+}
 
 int wide_key_bits(int64_t max_len) {
   return max_len <= 128 ? 7 : max_len <= 256 ? 8 : max_len <= 512 ? 9 : max_len <= 1024 ? 10 : max_len <= 2048 ? 11

@@ -83,6 +83,9 @@ int bce_fault_check(void* stream);
  * 2^22).  A tiny cap makes the pipe kernel's waves give up at once, which exercises the
  * fault path above; results of such a launch are garbage. */
 int bce_debug_set_spin_cap(int cap);
+/* Self-test of the wide kernel's VALU lane exchanges (DPP / permlane swaps) and wave scan:
+ * one wave writes 13*64 words to `out` (see consensus_wide.hip); tests run it first. */
+int bce_debug_lane_selftest(unsigned* out, void* stream);
 
 /* ---- consensus: core.compute_consensus (core.py:63-179) + validation -------------
  *

@@ -18,6 +18,21 @@ from test_gpu_consensus import _compare_vec, _dev, _run
 pytestmark = pytest.mark.gpu
 
 
+def test_lane_exchange_selftest():
+    """The wide kernel's VALU lane exchanges (DPP rotations/mirrors, v_permlane16/32_swap)
+    and its DPP wave scan, checked lane by lane before any sort runs on them."""
+    from bayesian_engine import _native as N
+    out = torch.zeros(13 * 64, dtype=torch.int32, device="cuda")
+    N.check(N.lib().bce_debug_lane_selftest(N.ptr(out), N.stream(out.device)))
+    torch.cuda.synchronize()
+    o = out.cpu().numpy().astype(np.int64).reshape(13, 64)
+    lane = np.arange(64)
+    for q, M in enumerate([1, 2, 3, 4, 7, 8, 15, 16, 31, 32, 63]):
+        assert np.array_equal(o[q], lane ^ M), (M, o[q].tolist())
+    assert np.array_equal(o[11], (lane + 1) * (lane + 2) // 2), o[11].tolist()
+    assert o[12][0] == 0 and np.array_equal(o[12][1:], lane[1:] + 99), o[12].tolist()
+
+
 def _zipf_case(lens, S, seed, a=1.1, base=0, bad=True):
     rng = np.random.default_rng(seed)
     off = np.zeros(len(lens) + 1, np.int64)
