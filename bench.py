@@ -104,6 +104,8 @@ def dist_setup(args):
         if world > 1:
             dist.init_process_group("gloo")
     elif world > 1:
+        # one rank per GPU; more ranks than GPUs only for a gloo rehearsal on a small box
+        local = local % max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local)
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
