@@ -56,7 +56,10 @@ __device__ unsigned long long g_wide_prof[8];
 #endif
 
 constexpr int ilog2c(int x) { return x <= 1 ? 0 : 1 + ilog2c(x >> 1); }
-constexpr int kWaveRun = 48;  // FAST: duplicate runs longer than this are summed wave-wide
+#ifndef BCE_WIDE_KWR
+#define BCE_WIDE_KWR 48
+#endif
+constexpr int kWaveRun = BCE_WIDE_KWR;  // FAST: duplicate runs longer than this are summed wave-wide
 
 template <int NW, int R, bool FAST>
 struct WideCfg {

@@ -27,6 +27,10 @@ SRCS = ["capi.hip", "consensus.hip", "consensus_tab.hip", "consensus_wide.hip", 
 VARIANTS = {
     "base": [],
     "prof": ["-DBCE_WIDE_PROF=1"],
+    "hr3": ["-DBCE_WIDE_HR=3"],
+    "hr4": ["-DBCE_WIDE_HR=4"],
+    "kwr32": ["-DBCE_WIDE_KWR=32"],
+    "kwr96": ["-DBCE_WIDE_KWR=96"],
 }
 PHASES = ["keys+next sids", "sort", "probs+leaders", "run sums+products+stores", "stage barrier", "chain", "tail",
           "gather wait"]
