@@ -1,0 +1,153 @@
+// tile_probe.hip -- the config-2 traffic of consensus_tab32_kernel with its occupancy and
+// access shapes but trivial compute (experiment tooling, not product code).
+//   hipcc --offload-arch=gfx950 -O3 tools/tile_probe.hip -o tools/bin/tile_probe
+//
+// One persistent workgroup of W waves per CU (the real kernel: W = 4, the LDS table takes
+// the CU), a wave owns a tile of 64 consecutive markets x 32 signals and moves exactly its
+// bytes: sid (4 B) + prob (8 B) in, usid (4 B) + weight + nweight (8 + 8 B) out per
+// signal, 3 fp64 + 2 int32 per market.  Shapes:
+//   piece64   the kernel's: four consecutive lanes cover one contiguous 64-B piece of a
+//             market's row, 16 markets per instruction
+//   row128    eight lanes cover a whole 128-B sid row / 256-B prob row piece
+//   linear    lane-linear: an instruction covers 1 KiB contiguous (ignores market rows)
+// and optionally the next tile's loads issued before this tile's stores (PREF).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1);} } while (0)
+
+struct Args {
+  const uint32_t* sid; const double* prob;
+  uint32_t* usid; double* w; double* nw;
+  double* cons; double* conf; double* tw; int* nu; int* err;
+  int64_t M;
+};
+
+// SHAPE: 0 piece64, 1 row128, 2 linear, 3 half-row 128-B pieces for probs too
+template <int SHAPE>
+__device__ __forceinline__ void tile_load(const Args& a, int64_t B, int lane, uint4 (&s)[8], uint4 (&p)[16]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    int64_t e;  // element (u32) offset of this lane's 16-B chunk
+    if (SHAPE == 0) e = 32 * (16 * (k & 3) + (lane >> 2)) + 16 * (k >> 2) + 4 * (lane & 3);
+    else if (SHAPE == 1 || SHAPE == 3) e = 32 * (8 * k + (lane >> 3)) + 4 * (lane & 7);
+    else e = 256 * k + 4 * lane;
+    s[k] = *reinterpret_cast<const uint4*>(a.sid + B + e);
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    int64_t e;  // element (u32 of the prob array viewed as u32) offset
+    if (SHAPE == 0) e = 64 * (16 * (k & 3) + (lane >> 2)) + 16 * (k >> 2) + 4 * (lane & 3);
+    else if (SHAPE == 1) e = 64 * (4 * k + (lane >> 4)) + 4 * (lane & 15);
+    else if (SHAPE == 3) e = 64 * (8 * (k & 7) + (lane >> 3)) + 32 * (k >> 3) + 4 * (lane & 7);
+    else e = 256 * k + 4 * lane;
+    p[k] = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint32_t*>(a.prob + B) + e);
+  }
+}
+
+template <int W, int SHAPE, bool PF = false>
+__global__ __launch_bounds__(64 * W) void tile_mix(Args a) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t n_tiles = a.M / 64;
+  const int64_t stride = (int64_t)gridDim.x * W;
+  uint4 sn[8], pn[16];
+  int64_t tile = (int64_t)blockIdx.x * W + wv;
+  if (PF && tile < n_tiles) tile_load<SHAPE>(a, tile * 64 * 32, lane, sn, pn);
+  for (; tile < n_tiles; tile += stride) {
+    const int64_t B = tile * 64 * 32;  // first signal of the tile
+    uint4 s[8];
+    uint4 p[16];
+    if (PF) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s[k] = sn[k];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) p[k] = pn[k];
+      if (tile + stride < n_tiles) tile_load<SHAPE>(a, (tile + stride) * 64 * 32, lane, sn, pn);
+    } else {
+      tile_load<SHAPE>(a, B, lane, s, p);
+    }
+    // trivial compute: fold so nothing is dead
+    uint32_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc ^= s[k].x ^ s[k].w;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc += p[k].y;
+    // per-market outputs (lane = market)
+    const int64_t mk = tile * 64 + lane;
+    a.cons[mk] = (double)acc;
+    a.conf[mk] = (double)lane;
+    a.tw[mk] = 1.0;
+    a.nu[mk] = 32;
+    a.err[mk] = -1;
+    // per-unique outputs: usid 8 KiB, weight 16 KiB, nweight 16 KiB per tile
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      int64_t e;
+      if (SHAPE == 0) e = 32 * (16 * (k & 3) + (lane >> 2)) + 16 * (k >> 2) + 4 * (lane & 3);
+      else if (SHAPE == 1 || SHAPE == 3) e = 32 * (8 * k + (lane >> 3)) + 4 * (lane & 7);
+      else e = 256 * k + 4 * lane;
+      *reinterpret_cast<uint4*>(a.usid + B + e) = s[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      int64_t e;
+      if (SHAPE == 0) e = 64 * (16 * (k & 3) + (lane >> 2)) + 16 * (k >> 2) + 4 * (lane & 3);
+      else if (SHAPE == 1) e = 64 * (4 * k + (lane >> 4)) + 4 * (lane & 15);
+      else if (SHAPE == 3) e = 64 * (8 * (k & 7) + (lane >> 3)) + 32 * (k >> 3) + 4 * (lane & 7);
+      else e = 256 * k + 4 * lane;
+      *reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(a.w + B) + e) = p[k];
+      *reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(a.nw + B) + e) = p[k];
+    }
+  }
+}
+
+int main() {
+  const int64_t M = 1000000, N = M * 32;
+  Args a;
+  a.M = M;
+  CK(hipMalloc((void**)&a.sid, N * 4)); CK(hipMalloc((void**)&a.prob, N * 8));
+  CK(hipMalloc((void**)&a.usid, N * 4)); CK(hipMalloc((void**)&a.w, N * 8)); CK(hipMalloc((void**)&a.nw, N * 8));
+  CK(hipMalloc((void**)&a.cons, M * 8)); CK(hipMalloc((void**)&a.conf, M * 8)); CK(hipMalloc((void**)&a.tw, M * 8));
+  CK(hipMalloc((void**)&a.nu, M * 4)); CK(hipMalloc((void**)&a.err, M * 4));
+  CK(hipMemset((void*)a.sid, 1, N * 4)); CK(hipMemset((void*)a.prob, 0, N * 8));
+  int cus = 0;
+  CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  const double bytes = 32.0 * N + 32.0 * M;
+  auto timeit = [&](const char* name, auto launch) {
+    for (int i = 0; i < 50; ++i) launch();
+    CK(hipGetLastError());
+    CK(hipDeviceSynchronize());
+    const int K = 100;
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < K; ++i) launch();
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    ms /= K;
+    printf("{\"probe\": \"%s\", \"ms\": %.5f, \"GBps\": %.1f}\n", name, ms, bytes / ms / 1e6);
+    fflush(stdout);
+  };
+  // one workgroup per CU (the LDS table's occupancy) and, for comparison, four
+  timeit("piece64 w4 1wg/cu", [&] { tile_mix<4, 0><<<cus, 256>>>(a); });
+  timeit("piece64 w8 1wg/cu", [&] { tile_mix<8, 0><<<cus, 512>>>(a); });
+  timeit("piece64 w16 1wg/cu", [&] { tile_mix<16, 0><<<cus, 1024>>>(a); });
+  timeit("row128 w4 1wg/cu", [&] { tile_mix<4, 1><<<cus, 256>>>(a); });
+  timeit("row128 w8 1wg/cu", [&] { tile_mix<8, 1><<<cus, 512>>>(a); });
+  timeit("linear w4 1wg/cu", [&] { tile_mix<4, 2><<<cus, 256>>>(a); });
+  timeit("linear w8 1wg/cu", [&] { tile_mix<8, 2><<<cus, 512>>>(a); });
+  timeit("linear w16 1wg/cu", [&] { tile_mix<16, 2><<<cus, 1024>>>(a); });
+  timeit("piece64 w4 4wg/cu", [&] { tile_mix<4, 0><<<4 * cus, 256>>>(a); });
+  timeit("linear w4 4wg/cu", [&] { tile_mix<4, 2><<<4 * cus, 256>>>(a); });
+  timeit("half128 w4 1wg/cu", [&] { tile_mix<4, 3><<<cus, 256>>>(a); });
+  timeit("piece64 w4 1wg/cu prefetch", [&] { tile_mix<4, 0, true><<<cus, 256>>>(a); });
+  timeit("half128 w4 1wg/cu prefetch", [&] { tile_mix<4, 3, true><<<cus, 256>>>(a); });
+  timeit("row128 w4 1wg/cu prefetch", [&] { tile_mix<4, 1, true><<<cus, 256>>>(a); });
+  timeit("linear w4 1wg/cu prefetch", [&] { tile_mix<4, 2, true><<<cus, 256>>>(a); });
+  timeit("half128 w8 1wg/cu prefetch", [&] { tile_mix<8, 3, true><<<cus, 512>>>(a); });
+  return 0;
+}
