@@ -60,6 +60,7 @@ static const char* fault_text(int code) {
     case kFaultSpinCompute: return "consensus_pipe_kernel: compute wave timed out waiting for its tile";
     case kFaultSid: return "consensus: a sid is >= n_sources (its row read was clamped)";
     case kFaultTooLong: return "consensus: a market is longer than the launch's max_len (left unprocessed)";
+    case kFaultSpinChain: return "consensus_wide_kernel: exact-mode chain hand-off timed out";
     default: return "unknown device fault";
   }
 }

@@ -39,6 +39,7 @@ constexpr int kFaultSpinLoader = 1;   // pipe kernel: loader never saw a slot re
 constexpr int kFaultSpinCompute = 2;  // pipe kernel: compute wave never saw its slot loaded
 constexpr int kFaultSid = 3;          // a sid >= n_sources (the row read was clamped)
 constexpr int kFaultTooLong = 4;      // a market longer than the launch's max_len (skipped)
+constexpr int kFaultSpinChain = 5;    // wide kernel, exact mode: chain / producer wait timed out
 
 constexpr int kBitsLds = 512;  // present bitmask words staged in LDS (S <= 16384)
 

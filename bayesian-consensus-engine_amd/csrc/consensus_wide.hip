@@ -20,8 +20,10 @@
 //        FAST  (BCE_MODE_FAST): per-thread partial sums in round order, then a fixed
 //              butterfly over the wave and a wave-ordered sum over the workgroup --
 //              deterministic, within the north-star 1e-9 of the reference order.
-//        EXACT: rounds of NT products staged through two LDS buffers; wave 0 carries the
-//              three left-to-right chains (core.py:120,136,142) on lanes 0..2.
+//        EXACT: rounds of products staged through a two-slot LDS ring; wave 0 carries the
+//              three left-to-right chains (core.py:120,136,142) on lanes 0..2 -- with
+//              several waves it does only that, fed by the others through LDS counters
+//              (no barriers), so the serial chains overlap the next rounds' gathers.
 //      normalizedWeight reads w[j] back from the weight output (or, without one, from the
 //      dead sorted-probability slot j where it was parked).
 //   5. the next market's probabilities are issued, then per-market outputs and
@@ -37,6 +39,9 @@
 
 #ifndef BCE_WIDE_HR
 #define BCE_WIDE_HR 2  // rounds of NT uniques whose gathers are in flight together
+#endif
+#ifndef BCE_WIDE_WPE_BIG
+#define BCE_WIDE_WPE_BIG 4  // the same for workgroups of >= 4 waves
 #endif
 #ifndef BCE_WIDE_WPE
 #define BCE_WIDE_WPE 2  // min waves per SIMD (register budget)
@@ -70,7 +75,7 @@ struct WideCfg {
   static constexpr int HR = (R < BCE_WIDE_HR) ? R : BCE_WIDE_HR;
   // register budget: workgroups of >= 4 waves get 4 waves per SIMD (<= 128 VGPRs), so two
   // LDS-sized workgroups share a CU
-  static constexpr int WPE = (NW >= 4 && BCE_WIDE_WPE < 4) ? 4 : BCE_WIDE_WPE;
+  static constexpr int WPE = (NW >= 4 && BCE_WIDE_WPE < BCE_WIDE_WPE_BIG) ? BCE_WIDE_WPE_BIG : BCE_WIDE_WPE;
   static constexpr int A_DBL = P + 64;  // + the run sums' read-ahead
   // region B (u32): sort exchange rows, then leaders [P] (+ exact: chain buffers
   // [2][3][NT] doubles + the chain's read-ahead)
@@ -241,6 +246,61 @@ __device__ __forceinline__ double run_sum(const double* rp, int len) {
   return (len > 1) ? sum / (double)len : sum;
 }
 
+// acc += src[0] + src[1] + ... + src[ce-1], left to right (the reference's chains,
+// core.py:120,136,142).  Full 8-term steps run in asm: two 4-term batches in fixed
+// registers, each reloaded right after its adds, so one batch's LDS latency hides under the
+// other's dependent adds (the compiler would copy loop-carried batch registers behind an
+// lgkmcnt(0)).  The < 8-term tail is added in C++ with masked terms adding +0.0 -- exact,
+// because these chains never hold -0.0.  src is 16-B aligned; reads may run 8 past ce.
+#ifndef BCE_WIDE_PIPE
+#define BCE_WIDE_PIPE 1
+#endif
+__device__ __forceinline__ void chain_add(double& acc, const double* src, int ce) {
+  const int nfull = ce & ~7;
+  if (nfull) {
+    unsigned addr = (unsigned)(uintptr_t)src;
+    int steps = nfull >> 3;
+    asm volatile(
+        "ds_read_b128 v[112:115], %[ad] offset:0\n"
+        "ds_read_b128 v[116:119], %[ad] offset:16\n"
+        "ds_read_b128 v[120:123], %[ad] offset:32\n"
+        "ds_read_b128 v[124:127], %[ad] offset:48\n"
+        "1:\n"
+        "s_waitcnt lgkmcnt(3)\n"
+        "v_add_f64 %[acc], %[acc], v[112:113]\n"
+        "v_add_f64 %[acc], %[acc], v[114:115]\n"
+        "s_waitcnt lgkmcnt(2)\n"
+        "v_add_f64 %[acc], %[acc], v[116:117]\n"
+        "v_add_f64 %[acc], %[acc], v[118:119]\n"
+        "ds_read_b128 v[112:115], %[ad] offset:64\n"
+        "ds_read_b128 v[116:119], %[ad] offset:80\n"
+        "s_waitcnt lgkmcnt(3)\n"
+        "v_add_f64 %[acc], %[acc], v[120:121]\n"
+        "v_add_f64 %[acc], %[acc], v[122:123]\n"
+        "s_waitcnt lgkmcnt(2)\n"
+        "v_add_f64 %[acc], %[acc], v[124:125]\n"
+        "v_add_f64 %[acc], %[acc], v[126:127]\n"
+        "ds_read_b128 v[120:123], %[ad] offset:96\n"
+        "ds_read_b128 v[124:127], %[ad] offset:112\n"
+        "v_add_u32 %[ad], 64, %[ad]\n"
+        "s_sub_u32 %[st], %[st], 1\n"
+        "s_cmp_lg_u32 %[st], 0\n"
+        "s_cbranch_scc1 1b\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        : [acc] "+v"(acc), [ad] "+v"(addr), [st] "+s"(steps)
+        :
+        : "memory", "scc", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121",
+          "v122", "v123", "v124", "v125", "v126", "v127");
+  }
+  if (nfull < ce) {
+    double xt[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) xt[e] = src[nfull + e];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc += (nfull + e < ce) ? xt[e] : 0.0;
+  }
+}
+
 template <int NW, int R, bool FAST>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg<NW, R, FAST>::WPE, 8))) void consensus_wide_kernel(ConsArgs a) {
   using Cfg = WideCfg<NW, R, FAST>;
@@ -253,6 +313,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
   __shared__ int sCnt[NW];
   __shared__ int sErr;
   __shared__ double sTot[3 * NW];
+  __shared__ int sRdy[2];  // exact, pipelined: producer-wave arrivals per ring slot
+  __shared__ int sDone;    // exact, pipelined: rounds the chain wave has consumed
   unsigned* const sX = sB;                                            // sort exchange rows
   unsigned* const sLead = sB;                                         // [u] sid<<IB | q0
   double* const sWAC = reinterpret_cast<double*>(sB + P);             // exact: [2][3][NT]
@@ -401,13 +463,116 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
         sLead[jj] = (key[r] & ~QMASK) | (unsigned)(t * R + r);
       }
     }
+    if (t == 0) {
+      sRdy[0] = sRdy[1] = 0;
+      sDone = 0;
+    }
     __syncthreads();  // (c) sorted probs + leaders visible
     WMARK(2);
 
     // ---- 4. per-unique products --------------------------------------------------------
-    const int nr = (u + NT - 1) / NT;
     double acc = 0.0;                     // exact: wave 0 lanes 0..2 carry the chains
     double pw = 0.0, pa = 0.0, pc = 0.0;  // fast: this thread's partial sums
+    // EXACT with several waves (and the weight output, so region A is not needed for w):
+    // wave 0 only carries the chains while waves 1.. produce rounds of NP = NT - 64
+    // uniques into a two-slot LDS ring, handed over with LDS counters instead of barriers,
+    // so the serial chains overlap the gathers and run sums of the next rounds.
+    const bool piped = BCE_WIDE_PIPE && !FAST && NW > 1 && wback;
+    if (piped) {
+      constexpr int NP = (NW > 1) ? NT - 64 : NT;
+      const int nrp = (u + NP - 1) / NP;
+      if (wv == 0) {
+        __builtin_amdgcn_s_setprio(2);  // the chain is the critical path
+        for (int r = 0; r < nrp; ++r) {
+          const int slot = r & 1;
+          const int need = (NW - 1) * ((r >> 1) + 1);
+          int spins = 0;
+          while (ldsflag(&sRdy[slot]) < need) {
+            if (++spins > a.spin_cap) {
+              raise_fault(a.fault, kFaultSpinChain);
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+          const int ce = (u - r * NP < NP) ? u - r * NP : NP;
+          chain_add(acc, sWAC + slot * 3 * NP + (lane % 3) * NP, ce);
+          if (lane == 0) __hip_atomic_store(&sDone, r + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        __builtin_amdgcn_s_setprio(0);
+      } else {
+        const int pt = t - 64;
+        for (int h = 0; h < nrp; h += HR) {
+          double2 rc[HR];
+          int q0s[HR], q1s[HR];
+          unsigned sids[HR], pwd[HR];
+#pragma unroll
+          for (int i = 0; i < HR; ++i) {  // every gather of the group in flight together
+            const int jj = (h + i) * NP + pt;
+            q0s[i] = q1s[i] = 0;
+            sids[i] = pwd[i] = 0;
+            rc[i] = make_double2(0.5, 0.25);  // DEFAULT_RELIABILITY / _CONFIDENCE (empty table)
+            if (jj < u) {
+              const unsigned lv = sLead[jj];
+              q0s[i] = (int)(lv & QMASK);
+              sids[i] = min(lv >> IB, smax);
+              q1s[i] = (jj + 1 < u) ? (int)(sLead[jj + 1] & QMASK) : n;
+              if (a.n_sources > 0) {
+                rc[i] = a.relconf[sids[i]];
+                pwd[i] = a.pbits[sids[i] >> 5];
+              }
+            }
+          }
+          double vw[HR], va[HR], vc[HR];
+#pragma unroll
+          for (int i = 0; i < HR; ++i) {
+            const int jj = (h + i) * NP + pt;
+            vw[i] = va[i] = vc[i] = 0.0;
+            if (jj < u) {
+              const double avg = run_sum(sA + q0s[i], q1s[i] - q0s[i]);  // core.py:116
+              const double w = rc[i].x;  // core.py:111,119
+              vw[i] = w;
+              va[i] = avg * w;        // core.py:136
+              vc[i] = rc[i].y * w;    // core.py:142
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < HR; ++i) {
+            const int r = h + i;
+            if (r < nrp) {
+              const int slot = r & 1;
+              if (r >= 2) {  // the slot's previous round is consumed
+                int spins = 0;
+                while (ldsflag(&sDone) < r - 1) {
+                  if (++spins > a.spin_cap) {
+                    raise_fault(a.fault, kFaultSpinChain);
+                    break;
+                  }
+                  __builtin_amdgcn_s_sleep(1);
+                }
+              }
+              double* const buf = sWAC + slot * 3 * NP;
+              buf[pt] = vw[i];
+              buf[NP + pt] = va[i];
+              buf[2 * NP + pt] = vc[i];
+              wave_sync_lds();  // this wave's part of the round is in LDS
+              if (lane == 0)
+                __hip_atomic_fetch_add(&sRdy[slot], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < HR; ++i) {
+            const int jj = (h + i) * NP + pt;
+            if (jj < u) {
+              const int64_t p = off + jj;
+              if (a.usid)
+                a.usid[p] = (int32_t)sids[i] | (((pwd[i] >> (sids[i] & 31)) & 1u) ? 0 : (int32_t)0x80000000);
+              a.weight[p] = vw[i];
+            }
+          }
+        }
+      }
+    }
+    const int nr = piped ? 0 : (u + NT - 1) / NT;
     for (int h = 0; h < nr; h += HR) {
       double2 rc[HR];
       int q0s[HR], q1s[HR];
@@ -493,57 +658,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
             const int jj = (h + i) * NT + t;
             if (jj < u && !wback) sA[jj] = vw[i];  // slot jj is only read by uniques <= jj
             if (wv == 0) {
-              // Full 8-term steps run in asm: two 4-term batches in fixed registers, each
-              // reloaded right after its adds, so one batch's LDS latency hides under the
-              // other's dependent adds (the compiler would copy loop-carried batch registers
-              // behind an lgkmcnt(0)).  The < 8-term tail is added in C++ with masked terms
-              // adding +0.0 -- exact, because these chains never hold -0.0.
               __builtin_amdgcn_s_setprio(2);  // the chain is the critical path
               const int ce = (u - (h + i) * NT < NT) ? u - (h + i) * NT : NT;
-              const double* src = buf + (lane % 3) * NT;
-              const int nfull = ce & ~7;
-              if (nfull) {
-                unsigned addr = (unsigned)(uintptr_t)src;
-                int steps = nfull >> 3;
-                asm volatile(
-                    "ds_read_b128 v[112:115], %[ad] offset:0\n"
-                    "ds_read_b128 v[116:119], %[ad] offset:16\n"
-                    "ds_read_b128 v[120:123], %[ad] offset:32\n"
-                    "ds_read_b128 v[124:127], %[ad] offset:48\n"
-                    "1:\n"
-                    "s_waitcnt lgkmcnt(3)\n"
-                    "v_add_f64 %[acc], %[acc], v[112:113]\n"
-                    "v_add_f64 %[acc], %[acc], v[114:115]\n"
-                    "s_waitcnt lgkmcnt(2)\n"
-                    "v_add_f64 %[acc], %[acc], v[116:117]\n"
-                    "v_add_f64 %[acc], %[acc], v[118:119]\n"
-                    "ds_read_b128 v[112:115], %[ad] offset:64\n"
-                    "ds_read_b128 v[116:119], %[ad] offset:80\n"
-                    "s_waitcnt lgkmcnt(3)\n"
-                    "v_add_f64 %[acc], %[acc], v[120:121]\n"
-                    "v_add_f64 %[acc], %[acc], v[122:123]\n"
-                    "s_waitcnt lgkmcnt(2)\n"
-                    "v_add_f64 %[acc], %[acc], v[124:125]\n"
-                    "v_add_f64 %[acc], %[acc], v[126:127]\n"
-                    "ds_read_b128 v[120:123], %[ad] offset:96\n"
-                    "ds_read_b128 v[124:127], %[ad] offset:112\n"
-                    "v_add_u32 %[ad], 64, %[ad]\n"
-                    "s_sub_u32 %[st], %[st], 1\n"
-                    "s_cmp_lg_u32 %[st], 0\n"
-                    "s_cbranch_scc1 1b\n"
-                    "s_waitcnt lgkmcnt(0)\n"
-                    : [acc] "+v"(acc), [ad] "+v"(addr), [st] "+s"(steps)
-                    :
-                    : "memory", "scc", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120",
-                      "v121", "v122", "v123", "v124", "v125", "v126", "v127");
-              }
-              if (nfull < ce) {
-                double xt[8];
-#pragma unroll
-                for (int e = 0; e < 8; ++e) xt[e] = src[nfull + e];
-#pragma unroll
-                for (int e = 0; e < 8; ++e) acc += (nfull + e < ce) ? xt[e] : 0.0;
-              }
+              chain_add(acc, buf + (lane % 3) * NT, ce);
               __builtin_amdgcn_s_setprio(0);
             }
             WMARK(5);

@@ -31,6 +31,8 @@ VARIANTS = {
     "hr4": ["-DBCE_WIDE_HR=4"],
     "kwr32": ["-DBCE_WIDE_KWR=32"],
     "kwr96": ["-DBCE_WIDE_KWR=96"],
+    "nopipe": ["-DBCE_WIDE_PIPE=0"],
+    "w2": ["-DBCE_WIDE_WPE_BIG=2"],
 }
 PHASES = ["keys+next sids", "sort", "probs+leaders", "run sums+products+stores", "stage barrier", "chain", "tail",
           "gather wait"]
