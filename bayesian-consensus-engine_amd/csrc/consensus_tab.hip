@@ -10,11 +10,12 @@
 // stays in VGPRs -- no LDS staging ring, no producer/consumer waves:
 //
 //  load       a wave owns a tile of 64 consecutive markets.  A REGULAR tile (every market
-//             has 32 signals, 16-B aligned) is read with coalesced 16-B loads: four
-//             consecutive lanes cover one contiguous 64-B piece of a market's row (chunk
-//             bits on lane bits 1..0, market bits on lane bits 5..2 and the load index).
-//             Two butterflies (DPP quad_perm + a wave-constant select) swap lane bits 1, 0
-//             with load-index bits, leaving lane = market, register index = position.
+//             has 32 signals, 16-B aligned) is read with coalesced 16-B loads: eight
+//             consecutive lanes cover one contiguous 128-B piece of a market's row (chunk
+//             bits on lane bits 2..0, market bits on lane bits 5..3 and the load index).
+//             Three butterflies (DPP quad_perm / row_ror + a wave-constant select) swap
+//             lane bits 2..0 with load-index bits, leaving lane = market, register index =
+//             position.  (BCE_TAB_PIECE=64: four lanes per 64-B piece, two butterflies.)
 //             Other tiles (ragged lengths, the last tile, misaligned shards) load per lane.
 //             The next tile's offsets are read at the top of each tile.
 //  sort       keys (sid << 5 | position) with the probability as payload, Batcher
@@ -39,7 +40,9 @@
 // Measured (tools/tab_variants.py, profiles/r02_tab_*): 4 waves per CU (one per SIMD,
 // ~260 registers) beat 8 (2 per SIMD, 256-register budget: spills); the per-unique stores
 // are the largest phase -- the CU's share of the chip's write bandwidth -- and moving
-// them between the next tile's phases or to fully contiguous addresses did not help.
+// them between the next tile's phases or to fully contiguous addresses did not help;
+// 128-B pieces beat 64-B ones by ~0.5%; loading the next tile's signals ahead (parked in
+// AGPRs, before or after this tile's stores) moved the wait elsewhere and ran 1-7% slower.
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -62,26 +65,41 @@ __device__ unsigned long long g_tab_prof[8];
 #else
 #define TAB_MARK(k) do {} while (0)
 #endif
+#ifndef BCE_TAB_PIECE
+#define BCE_TAB_PIECE 128  // bytes of a market row one load/store instruction's lane group covers
+#endif
 constexpr int kTabWaves = BCE_TAB_WAVES;  // waves per workgroup; one workgroup per CU (LDS-bound)
+constexpr int kPL = BCE_TAB_PIECE / 16;    // lanes per piece (16 B each): 4 or 8
+constexpr int kLB = (kPL == 8) ? 3 : 2;    // log2 kPL
+constexpr int kMG = 64 / kPL;              // markets per load instruction
+static_assert(kPL == 4 || kPL == 8, "BCE_TAB_PIECE: 64 or 128");
 constexpr int kTabRing = 8;    // LDS table reads issued ahead of the walk
 
 // ---- lane-bit <-> register-bit butterflies -------------------------------------------
-// For a register pair (a: index bit 0, b: index bit 1) swap lane bit L (0 or 1) with that
-// index bit: a' = bit_L ? b[lane ^ 2^L] : a,  b' = bit_L ? b : a[lane ^ 2^L].  The partner
-// lane comes from a DPP quad_perm; the select mask is a wave constant.
+// For a register pair (a: index bit 0, b: index bit 1) swap lane bit L (0, 1 or 2) with
+// that index bit: a' = bit_L ? b[lane ^ 2^L] : a,  b' = bit_L ? b : a[lane ^ 2^L].  The
+// partner lane comes from a DPP quad_perm (L < 2); the select mask is a wave constant.
+// Lane bit 2: the partner l ^ 4 is row_ror:4 (l - 4) for lanes with the bit set and
+// row_ror:12 (l + 4) for the others -- neither leaves its 8-lane group.
 template <int L>
 __device__ __forceinline__ void bfly(uint32_t& a, uint32_t& b, int lane) {
-  constexpr int qp = (L == 0) ? 0xB1 : 0x4E;  // quad_perm [1,0,3,2] / [2,3,0,1]
+  constexpr int hi_ctl = (L == 0) ? 0xB1 : (L == 1) ? 0x4E : 0x124;  // quad_perm / row_ror:4
+  constexpr int lo_ctl = (L == 0) ? 0xB1 : (L == 1) ? 0x4E : 0x12C;  // quad_perm / row_ror:12
   const bool hi = ((lane >> L) & 1) != 0;
-  const uint32_t bx = (uint32_t)__builtin_amdgcn_mov_dpp((int)b, qp, 0xF, 0xF, true);
-  const uint32_t ax = (uint32_t)__builtin_amdgcn_mov_dpp((int)a, qp, 0xF, 0xF, true);
+  const uint32_t bx = (uint32_t)__builtin_amdgcn_mov_dpp((int)b, hi_ctl, 0xF, 0xF, true);
+  const uint32_t ax = (uint32_t)__builtin_amdgcn_mov_dpp((int)a, lo_ctl, 0xF, 0xF, true);
   const uint32_t na = hi ? bx : a;
   b = hi ? b : ax;
   a = na;
 }
-// Swap lane bits 1, 0 with dword-index bits 3, 2 of r[N] (an involution).
+// Swap lane bits kLB-1..0 with dword-index bits kLB+1..2 of r[N] (an involution).
 template <int N>
 __device__ __forceinline__ void xpose(uint32_t (&r)[N], int lane) {
+  if constexpr (kLB == 3) {
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      if (!(i & 16)) bfly<2>(r[i], r[i | 16], lane);
+  }
 #pragma unroll
   for (int i = 0; i < N; ++i)
     if (!(i & 8)) bfly<1>(r[i], r[i | 8], lane);
@@ -90,15 +108,16 @@ __device__ __forceinline__ void xpose(uint32_t (&r)[N], int lane) {
     if (!(i & 4)) bfly<0>(r[i], r[i | 4], lane);
 }
 
-// Regular-tile address maps (tile = 64 markets x 32 signals from B; load index k,
-// q = lane >> 2, c = lane & 3): every four consecutive lanes read one contiguous 64-byte
-// piece of one market's row, so each wave-instruction is 16 fully coalesced pieces
-//   sid   k < 8:  market 16(k&3) + q, positions 16(k>>2) + 4c + d    dword index 4k + d
-//   prob  k < 16: market 16(k&3) + q, positions 8(k>>2) + 2c + h     double index 2k + h
-// Swapping lane bits (1, 0) with load-index bits (1, 0) leaves one market per lane --
-// lane L holds market tmkt(L) = 16 (L & 3) + (L >> 2) -- and the register index = the
-// position, for both arrays.
-__device__ __forceinline__ int tmkt(int lane) { return ((lane & 3) << 4) | (lane >> 2); }
+// Regular-tile address maps (tile = 64 markets x 32 signals from B; PL = kPL lanes per
+// piece, MG = 64 / PL, load index k, q = lane >> log2 PL, c = lane & (PL-1)): every PL
+// consecutive lanes read one contiguous 16·PL-byte piece of one market's row, so each
+// wave-instruction is MG fully coalesced pieces (PL = 4: 64-B pieces, 8: 128-B)
+//   sid   k < 8:  market MG(k&(PL-1)) + q, positions 4PL(k>>log2 PL) + 4c + d   dword 4k + d
+//   prob  k < 16: market MG(k&(PL-1)) + q, positions 2PL(k>>log2 PL) + 2c + h  double 2k + h
+// Swapping the log2 PL lane bits of c with the low load-index bits leaves one market per
+// lane -- lane L holds market tmkt(L) = MG (L & (PL-1)) + (L >> log2 PL) -- and the
+// register index = the position, for both arrays.
+__device__ __forceinline__ int tmkt(int lane) { return ((lane & (kPL - 1)) * kMG) | (lane >> kLB); }
 // Odd-even merge network over 31-bit keys with a 64-bit payload, branch- and SGPR-free:
 // the swap mask is the sign of y - x (keys < 2^31), the payload moves with v_bfi_b32.
 // (Compare-and-select would give every comparator of a stage its own SGPR-pair condition;
@@ -188,17 +207,19 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
   };
   // Regular-tile loads (the address maps above); raw, not yet transposed.
   auto load_regular = [&](int64_t B, int lane, uint32_t (&rs)[32], uint32_t (&rp)[64]) {
-    const int q = lane >> 2, c = lane & 3;
+    const int q = lane >> kLB, c = lane & (kPL - 1);
     const uint32_t* sb = reinterpret_cast<const uint32_t*>(a.sid + B);
     const double* pb = a.prob + B;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const uint4 v = *reinterpret_cast<const uint4*>(sb + 32 * (16 * (k & 3) + q) + 16 * (k >> 2) + 4 * c);
+      const uint4 v =
+          *reinterpret_cast<const uint4*>(sb + 32 * (kMG * (k & (kPL - 1)) + q) + 4 * kPL * (k >> kLB) + 4 * c);
       rs[4 * k] = v.x; rs[4 * k + 1] = v.y; rs[4 * k + 2] = v.z; rs[4 * k + 3] = v.w;
     }
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-      const uint4 v = *reinterpret_cast<const uint4*>(pb + 32 * (16 * (k & 3) + q) + 8 * (k >> 2) + 2 * c);
+      const uint4 v =
+          *reinterpret_cast<const uint4*>(pb + 32 * (kMG * (k & (kPL - 1)) + q) + 2 * kPL * (k >> kLB) + 2 * c);
       rp[4 * k] = v.x; rp[4 * k + 1] = v.y; rp[4 * k + 2] = v.z; rp[4 * k + 3] = v.w;
     }
   };
@@ -406,12 +427,12 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
       const int64_t B = (int64_t)(((uint64_t)bhi << 32) | blo);
       int lane = lane_id();
       asm volatile("" : "+v"(lane));
-      const int q = lane >> 2, c = lane & 3;
-      int uk[4];
-      double tk[4];
+      const int q = lane >> kLB, c = lane & (kPL - 1);
+      int uk[kPL];
+      double tk[kPL];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {  // market 16k + q of load index k sits in lane 4q + k
-        const int src = ((lane & ~3) | k) << 2;
+      for (int k = 0; k < kPL; ++k) {  // market MG·k + q of load index k sits in lane PL·q + k
+        const int src = ((lane & ~(kPL - 1)) | k) << 2;
         uk[k] = __builtin_amdgcn_ds_bpermute(src, u);
         tk[k] = dbl((uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)lo32(total)),
                     (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)hi32(total)));
@@ -424,9 +445,9 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
         xpose<32>(o, lane);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const int slot = 16 * (k >> 2) + 4 * c;
-          if (uk[k & 3] > slot)
-            *reinterpret_cast<uint4*>(a.usid + B + 32 * (16 * (k & 3) + q) + slot) =
+          const int slot = 4 * kPL * (k >> kLB) + 4 * c;
+          if (uk[k & (kPL - 1)] > slot)
+            *reinterpret_cast<uint4*>(a.usid + B + 32 * (kMG * (k & (kPL - 1)) + q) + slot) =
                 make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
         }
       }
@@ -440,11 +461,11 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
         xpose<64>(o, lane);
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
-          const int slot = 8 * (k >> 2) + 2 * c;
-          const int64_t pos = B + 32 * (16 * (k & 3) + q) + slot;
+          const int slot = 2 * kPL * (k >> kLB) + 2 * c;
+          const int64_t pos = B + 32 * (kMG * (k & (kPL - 1)) + q) + slot;
           const double w0 = dbl(o[4 * k], o[4 * k + 1]), w1 = dbl(o[4 * k + 2], o[4 * k + 3]);
-          const double tot = tk[k & 3];
-          if (uk[k & 3] > slot) {
+          const double tot = tk[k & (kPL - 1)];
+          if (uk[k & (kPL - 1)] > slot) {
             if (do_w) *reinterpret_cast<double2*>(a.weight + pos) = make_double2(w0, w1);
             if (do_nw)  // core.py:151
               *reinterpret_cast<double2*>(a.nweight + pos) =

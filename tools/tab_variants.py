@@ -20,14 +20,16 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "bayesian-consensus-engine_amd", "csrc")
 OUT = os.path.join(ROOT, "tools", "ablate_build")
-SRCS = ["capi.hip", "consensus.hip", "consensus_tab.hip", "elementwise.hip", "tiebreak.hip", "stats.hip",
-        "aggregate.hip"]
+SRCS = ["capi.hip", "consensus.hip", "consensus_tab.hip", "consensus_wide.hip", "elementwise.hip", "tiebreak.hip",
+        "stats.hip", "aggregate.hip"]
 
 VARIANTS = {
     "w4": ["-DBCE_TAB_WAVES=4"],
     "w8": ["-DBCE_TAB_WAVES=8"],
     "w4_prof": ["-DBCE_TAB_WAVES=4", "-DBCE_TAB_PROF=1"],
     "w8_prof": ["-DBCE_TAB_WAVES=8", "-DBCE_TAB_PROF=1"],
+    "p64": ["-DBCE_TAB_PIECE=64"],
+    "p64_prof": ["-DBCE_TAB_PIECE=64", "-DBCE_TAB_PROF=1"],
 }
 PHASES = ["load+xpose", "valid+sort", "walk", "per_market", "compaction", "per_unique_stores"]
 
