@@ -255,6 +255,12 @@ __device__ __forceinline__ double run_sum(const double* rp, int len) {
 #ifndef BCE_WIDE_PIPE
 #define BCE_WIDE_PIPE 1
 #endif
+#ifndef BCE_WIDE_NWB
+#define BCE_WIDE_NWB 1  // normalizedWeight: batched read-backs
+#endif
+#ifndef BCE_WIDE_NWBF
+#define BCE_WIDE_NWBF 4  // FAST: read-backs per batch (1: 1.645, 2: 1.634, 4: 1.587 ms C3)
+#endif
 __device__ __forceinline__ void chain_add(double& acc, const double* src, int ce) {
   const int nfull = ce & ~7;
   if (nfull) {
@@ -712,11 +718,39 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
       a.n_unique[m] = u;
       if (a.err_idx) a.err_idx[m] = (sErr == kNoErr) ? -1 : sErr;
     }
-    if (a.nweight)  // core.py:151
-      for (int jj = t; jj < u; jj += NT) {
-        const double wj = wback ? a.weight[off + jj] : sA[jj];
-        a.nweight[off + jj] = (tw > 0.0) ? wj / tw : 0.0;
+    if (a.nweight) {  // core.py:151
+      if constexpr (BCE_WIDE_NWB && !FAST) {
+        // every read-back issued before any nweight store: loads retire behind earlier
+        // stores (vmcnt is in order), so a load/store per iteration waits out each store
+        // (C3 exact -2.6%; FAST: batches of BCE_WIDE_NWBF, a full batch costs it spills)
+        double wj[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+          const int jj = t + NT * k;
+          wj[k] = (jj < u) ? (wback ? a.weight[off + jj] : sA[jj]) : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+          const int jj = t + NT * k;
+          if (jj < u) a.nweight[off + jj] = (tw > 0.0) ? wj[k] / tw : 0.0;
+        }
+      } else {
+        constexpr int NB = (BCE_WIDE_NWBF < R) ? BCE_WIDE_NWBF : R;  // read-backs per batch
+        for (int j0 = t; j0 < u; j0 += NB * NT) {
+          double wj[NB];
+#pragma unroll
+          for (int k = 0; k < NB; ++k) {
+            const int jj = j0 + NT * k;
+            wj[k] = (jj < u) ? (wback ? a.weight[off + jj] : sA[jj]) : 0.0;
+          }
+#pragma unroll
+          for (int k = 0; k < NB; ++k) {
+            const int jj = j0 + NT * k;
+            if (jj < u) a.nweight[off + jj] = (tw > 0.0) ? wj[k] / tw : 0.0;
+          }
+        }
       }
+    }
     WMARK(6);
   }
 #if BCE_WIDE_PROF

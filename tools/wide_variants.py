@@ -33,6 +33,9 @@ VARIANTS = {
     "kwr96": ["-DBCE_WIDE_KWR=96"],
     "nopipe": ["-DBCE_WIDE_PIPE=0"],
     "w2": ["-DBCE_WIDE_WPE_BIG=2"],
+    "nwb0": ["-DBCE_WIDE_NWB=0"],
+    "nwbf1": ["-DBCE_WIDE_NWBF=1"],
+    "nwbf2": ["-DBCE_WIDE_NWBF=2"],
 }
 PHASES = ["keys+next sids", "sort", "probs+leaders", "run sums+products+stores", "stage barrier", "chain", "tail",
           "gather wait"]
