@@ -54,7 +54,7 @@ namespace bce {
 namespace {
 
 #ifndef BCE_TAB_WAVES
-#define BCE_TAB_WAVES 4
+#define BCE_TAB_WAVES 8
 #endif
 #ifndef BCE_TAB_PROF
 #define BCE_TAB_PROF 0  // experiment builds only (tools/tab_variants.py): per-phase s_memtime
@@ -68,12 +68,44 @@ __device__ unsigned long long g_tab_prof[8];
 #ifndef BCE_TAB_PIECE
 #define BCE_TAB_PIECE 128  // bytes of a market row one load/store instruction's lane group covers
 #endif
+#ifndef BCE_TAB_NT
+#define BCE_TAB_NT 3  // bit 0: nontemporal signal loads, bit 1: per-unique stores, bit 2: per-market stores
+#endif
+typedef unsigned tab_u4v __attribute__((ext_vector_type(4)));
+typedef double tab_d2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint4 tab_ld16(const uint32_t* p) {
+  if constexpr ((BCE_TAB_NT & 1) != 0) {
+    const tab_u4v v = __builtin_nontemporal_load(reinterpret_cast<const tab_u4v*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  } else {
+    return *reinterpret_cast<const uint4*>(p);
+  }
+}
+__device__ __forceinline__ void tab_st16(int32_t* p, uint4 v) {
+  if constexpr ((BCE_TAB_NT & 2) != 0) {
+    const tab_u4v x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<tab_u4v*>(p));
+  } else {
+    *reinterpret_cast<uint4*>(p) = v;
+  }
+}
+__device__ __forceinline__ void tab_st16(double* p, double x0, double x1) {
+  if constexpr ((BCE_TAB_NT & 2) != 0) {
+    const tab_d2v x = {x0, x1};
+    __builtin_nontemporal_store(x, reinterpret_cast<tab_d2v*>(p));
+  } else {
+    *reinterpret_cast<double2*>(p) = make_double2(x0, x1);
+  }
+}
 constexpr int kTabWaves = BCE_TAB_WAVES;  // waves per workgroup; one workgroup per CU (LDS-bound)
 constexpr int kPL = BCE_TAB_PIECE / 16;    // lanes per piece (16 B each): 4 or 8
 constexpr int kLB = (kPL == 8) ? 3 : 2;    // log2 kPL
 constexpr int kMG = 64 / kPL;              // markets per load instruction
 static_assert(kPL == 4 || kPL == 8, "BCE_TAB_PIECE: 64 or 128");
-constexpr int kTabRing = 8;    // LDS table reads issued ahead of the walk
+#ifndef BCE_TAB_RING
+#define BCE_TAB_RING 8
+#endif
+constexpr int kTabRing = BCE_TAB_RING;  // LDS table reads issued ahead of the walk
 
 // ---- lane-bit <-> register-bit butterflies -------------------------------------------
 // For a register pair (a: index bit 0, b: index bit 1) swap lane bit L (0, 1 or 2) with
@@ -212,14 +244,13 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
     const double* pb = a.prob + B;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const uint4 v =
-          *reinterpret_cast<const uint4*>(sb + 32 * (kMG * (k & (kPL - 1)) + q) + 4 * kPL * (k >> kLB) + 4 * c);
+      const uint4 v = tab_ld16(sb + 32 * (kMG * (k & (kPL - 1)) + q) + 4 * kPL * (k >> kLB) + 4 * c);
       rs[4 * k] = v.x; rs[4 * k + 1] = v.y; rs[4 * k + 2] = v.z; rs[4 * k + 3] = v.w;
     }
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-      const uint4 v =
-          *reinterpret_cast<const uint4*>(pb + 32 * (kMG * (k & (kPL - 1)) + q) + 2 * kPL * (k >> kLB) + 2 * c);
+      const uint4 v = tab_ld16(reinterpret_cast<const uint32_t*>(pb + 32 * (kMG * (k & (kPL - 1)) + q) +
+                                                                 2 * kPL * (k >> kLB) + 2 * c));
       rp[4 * k] = v.x; rp[4 * k + 1] = v.y; rp[4 * k + 2] = v.z; rp[4 * k + 3] = v.w;
     }
   };
@@ -380,11 +411,19 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
     // ---- per-market results (lane = market, coalesced) -----------------------------------
     if (has) {
       const bool null_ = (total == 0.0);  // core.py:131-133
-      a.consensus[mk] = null_ ? 0.0 : ws / total;
-      a.confidence[mk] = null_ ? 0.0 : cs / total;
-      a.total_weight[mk] = total;
-      a.n_unique[mk] = u;
-      if (a.err_idx) a.err_idx[mk] = err;
+      if constexpr ((BCE_TAB_NT & 4) != 0) {
+        __builtin_nontemporal_store(null_ ? 0.0 : ws / total, a.consensus + mk);
+        __builtin_nontemporal_store(null_ ? 0.0 : cs / total, a.confidence + mk);
+        __builtin_nontemporal_store(total, a.total_weight + mk);
+        __builtin_nontemporal_store(u, a.n_unique + mk);
+        if (a.err_idx) __builtin_nontemporal_store(err, a.err_idx + mk);
+      } else {
+        a.consensus[mk] = null_ ? 0.0 : ws / total;
+        a.confidence[mk] = null_ ? 0.0 : cs / total;
+        a.total_weight[mk] = total;
+        a.n_unique[mk] = u;
+        if (a.err_idx) a.err_idx[mk] = err;
+      }
     }
     if (!do_any) {
       cur = nxt;
@@ -447,8 +486,8 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
         for (int k = 0; k < 8; ++k) {
           const int slot = 4 * kPL * (k >> kLB) + 4 * c;
           if (uk[k & (kPL - 1)] > slot)
-            *reinterpret_cast<uint4*>(a.usid + B + 32 * (kMG * (k & (kPL - 1)) + q) + slot) =
-                make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+            tab_st16(a.usid + B + 32 * (kMG * (k & (kPL - 1)) + q) + slot,
+                     make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]));
         }
       }
       if (do_w || do_nw) {
@@ -466,10 +505,8 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
           const double w0 = dbl(o[4 * k], o[4 * k + 1]), w1 = dbl(o[4 * k + 2], o[4 * k + 3]);
           const double tot = tk[k & (kPL - 1)];
           if (uk[k & (kPL - 1)] > slot) {
-            if (do_w) *reinterpret_cast<double2*>(a.weight + pos) = make_double2(w0, w1);
-            if (do_nw)  // core.py:151
-              *reinterpret_cast<double2*>(a.nweight + pos) =
-                  make_double2(tot > 0.0 ? w0 / tot : 0.0, tot > 0.0 ? w1 / tot : 0.0);
+            if (do_w) tab_st16(a.weight + pos, w0, w1);
+            if (do_nw) tab_st16(a.nweight + pos, tot > 0.0 ? w0 / tot : 0.0, tot > 0.0 ? w1 / tot : 0.0);  // core.py:151
           }
         }
       }

@@ -109,6 +109,36 @@ __global__ __launch_bounds__(256) void outcome_update_kernel(int64_t n, double* 
   }
 }
 
+#ifndef BCE_EW_NT
+#define BCE_EW_NT 2  // experiment switch: bit 0 nontemporal view stores, bit 1 rel/t loads, bit 2 conf load (with bit 1)
+#endif
+typedef double ew_d2v __attribute__((ext_vector_type(2)));
+typedef long long ew_l2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ double2 ew_ld(const double2* p) {
+  if constexpr ((BCE_EW_NT & 2) != 0) {
+    const ew_d2v v = __builtin_nontemporal_load(reinterpret_cast<const ew_d2v*>(p));
+    return make_double2(v.x, v.y);
+  } else {
+    return *p;
+  }
+}
+__device__ __forceinline__ longlong2 ew_ld(const longlong2* p) {
+  if constexpr ((BCE_EW_NT & 2) != 0) {
+    const ew_l2v v = __builtin_nontemporal_load(reinterpret_cast<const ew_l2v*>(p));
+    return make_longlong2(v.x, v.y);
+  } else {
+    return *p;
+  }
+}
+__device__ __forceinline__ void ew_st_view(double2* p, double x0, double x1) {
+  if constexpr ((BCE_EW_NT & 1) != 0) {
+    const ew_d2v v = {x0, x1};
+    __builtin_nontemporal_store(v, reinterpret_cast<ew_d2v*>(p));
+  } else {
+    *p = make_double2(x0, x1);
+  }
+}
+
 // Config-4 step.  Absent rows must carry the baked cold-start values
 // (rel = default_rel, conf = default_conf, t = BCE_NO_TIMESTAMP), so the view needs no
 // `present` read; `present` is only written (rows that now exist).
@@ -121,13 +151,14 @@ __global__ __launch_bounds__(256) void replay_step_kernel(int64_t n, double* __r
   const int64_t npair = n >> 1;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < npair;
        i += (int64_t)gridDim.x * blockDim.x) {
-    double2 r = reinterpret_cast<const double2*>(rel)[i];
-    longlong2 t = reinterpret_cast<const longlong2*>(t_us)[i];
+    double2 r = ew_ld(reinterpret_cast<const double2*>(rel) + i);
+    longlong2 t = ew_ld(reinterpret_cast<const longlong2*>(t_us) + i);
     const uint8_t fb = flags2[i >> 1];
     const unsigned f = (fb >> ((i & 1) * 4)) & 0xF;  // 2 bits per source, sources 2i, 2i+1
-    reinterpret_cast<double2*>(view)[i] = make_double2(decayed(r.x, t.x, k), decayed(r.y, t.y, k));
+    ew_st_view(reinterpret_cast<double2*>(view) + i, decayed(r.x, t.x, k), decayed(r.y, t.y, k));
     if (f & 0x5) {  // any participant in the pair
-      double2 c = reinterpret_cast<const double2*>(conf)[i];
+      double2 c = ((BCE_EW_NT & 4) != 0) ? ew_ld(reinterpret_cast<const double2*>(conf) + i)
+                                           : reinterpret_cast<const double2*>(conf)[i];
       if (f & 1) {
         update_one(r.x, c.x, (f & 2) != 0);
         t.x = k.now_us;

@@ -1,0 +1,143 @@
+// c5_probe.hip -- config-5 pass-1 access-shape probe (experiment tooling, not product code).
+// Times the single-read re-estimation pass (agent-major P [A][M] fp64, lane per market
+// column, agent-order sums + one vote bit per cell) in several shapes on a 16k x 1M P:
+//   CPL   market columns per lane (1: 8-B loads, 512 B per wave-instruction; 2: 16-B loads,
+//         1 KB, vote words split into even/odd columns of a 128-column group)
+//   ROWS  agent rows loaded per step (loads in flight per wave)
+//   NT    nontemporal loads of P
+// Every variant's consensus must be bit-identical (same agent order per column).
+//   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off tools/c5_probe.hip -o tools/bin/c5_probe
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#pragma clang fp contract(off)
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1);} } while (0)
+
+typedef double d2v __attribute__((ext_vector_type(2)));
+
+__global__ void fill(double* P, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t h = (uint64_t)i * 0x9E3779B97F4A7C15ull;
+    h ^= h >> 29; h *= 0xBF58476D1CE4E5B9ull; h ^= h >> 32;
+    P[i] = (double)(h >> 11) * (1.0 / 9007199254740992.0);
+  }
+}
+
+template <int CPL, int ROWS, bool NT>
+__global__ __launch_bounds__(256) void votes_k(const double* __restrict__ P, int64_t A, int64_t M, int64_t ld,
+                                               const double* __restrict__ w, double* __restrict__ cons,
+                                               unsigned long long* __restrict__ vbits) {
+  const int lane = threadIdx.x & 63;
+  const int64_t g = blockIdx.x * 4 + (threadIdx.x >> 6);  // wave group of 64*CPL columns
+  const int64_t c0 = g * 64 * CPL;
+  if (c0 >= M) return;
+  const int64_t m = c0 + lane * CPL;
+  const bool in = m + CPL - 1 < M;
+  const double* col = P + (in ? m : 0);
+  unsigned long long* vb = vbits + g * CPL * A;
+  double ws[CPL], total = 0.0;
+#pragma unroll
+  for (int e = 0; e < CPL; ++e) ws[e] = 0.0;
+  for (int64_t a = 0; a + ROWS <= A; a += ROWS) {
+    double v[ROWS][CPL];
+#pragma unroll
+    for (int q = 0; q < ROWS; ++q) {
+      const double* src = col + (a + q) * ld;
+      if constexpr (CPL == 2) {
+        d2v x = NT ? __builtin_nontemporal_load(reinterpret_cast<const d2v*>(src)) : *reinterpret_cast<const d2v*>(src);
+        v[q][0] = x.x; v[q][1] = x.y;
+      } else {
+        v[q][0] = NT ? __builtin_nontemporal_load(src) : *src;
+      }
+    }
+    unsigned long long mine[CPL];
+#pragma unroll
+    for (int e = 0; e < CPL; ++e) mine[e] = 0;
+#pragma unroll
+    for (int q = 0; q < ROWS; ++q) {
+      const double wq = w[a + q];
+      total += wq;
+#pragma unroll
+      for (int e = 0; e < CPL; ++e) {
+        ws[e] += (0.0 + v[q][e]) * wq;
+        const unsigned long long b = __ballot(in && v[q][e] >= 0.5);
+        mine[e] = (lane == q) ? b : mine[e];
+      }
+    }
+    if (lane < ROWS) {
+#pragma unroll
+      for (int e = 0; e < CPL; ++e) vb[e * A + a + lane] = mine[e];
+    }
+  }
+  if (in) {
+#pragma unroll
+    for (int e = 0; e < CPL; ++e) cons[m + e] = total == 0.0 ? 0.0 : ws[e] / total;
+  }
+}
+
+int main(int argc, char** argv) {
+  const int64_t A = 16384, M = 1000000, ld = M;
+  double *P, *w, *cons, *ref;
+  unsigned long long* vb;
+  CK(hipMalloc(&P, A * M * 8));
+  CK(hipMalloc(&w, A * 8));
+  CK(hipMalloc(&cons, M * 8));
+  CK(hipMalloc(&ref, M * 8));
+  CK(hipMalloc(&vb, ((M + 127) / 128) * 2 * A * 8));
+  fill<<<4096, 256>>>(P, A * M);
+  double* hw = (double*)malloc(A * 8);
+  for (int64_t i = 0; i < A; ++i) hw[i] = (i % 7 == 0) ? 0.25 : 0.5;
+  CK(hipMemcpy(w, hw, A * 8, hipMemcpyHostToDevice));
+  CK(hipDeviceSynchronize());
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  const double bytes = 8.0 * A * M;
+  bool have_ref = false;
+  double* h1 = (double*)malloc(M * 8);
+  double* h2 = (double*)malloc(M * 8);
+  auto run = [&](const char* name, int cpl, auto launch) {
+    const int reps = 4;
+    launch();
+    CK(hipDeviceSynchronize());
+    float best = 1e30f, sum = 0.f;
+    for (int r = 0; r < reps; ++r) {
+      CK(hipEventRecord(e0));
+      launch();
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+      best = ms < best ? ms : best; sum += ms;
+    }
+    bool same = true;
+    if (!have_ref) { CK(hipMemcpy(ref, cons, M * 8, hipMemcpyDeviceToDevice)); have_ref = true; }
+    else {
+      CK(hipMemcpy(h1, ref, M * 8, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(h2, cons, M * 8, hipMemcpyDeviceToHost));
+      same = memcmp(h1, h2, M * 8) == 0;
+    }
+    printf("{\"variant\": \"%s\", \"best_ms\": %.3f, \"mean_ms\": %.3f, \"TBps\": %.3f, \"frac\": %.3f, \"same_cons\": %s}\n",
+           name, best, sum / reps, bytes / best / 1e9, bytes / best / 1e9 / 8.0, same ? "true" : "false");
+    fflush(stdout);
+    (void)cpl;
+  };
+#define V(C, R, N)                                                                                      \
+  run("cpl" #C "_rows" #R "_nt" #N, C, [&] {                                                            \
+    const int64_t groups = (M + 64 * C - 1) / (64 * C);                                                 \
+    votes_k<C, R, N><<<(unsigned)((groups + 3) / 4), 256>>>(P, A, M, ld, w, cons, vb);                  \
+  })
+  for (int round = 0; round < 2; ++round) {
+    V(1, 16, 0);
+    V(1, 16, 1);
+    V(1, 32, 0);
+    V(1, 32, 1);
+    V(2, 8, 0);
+    V(2, 8, 1);
+    V(2, 16, 0);
+    V(2, 16, 1);
+  }
+  return 0;
+}

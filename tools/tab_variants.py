@@ -24,12 +24,28 @@ SRCS = ["capi.hip", "consensus.hip", "consensus_tab.hip", "consensus_wide.hip", 
         "stats.hip", "aggregate.hip"]
 
 VARIANTS = {
+    "base": [],  # the product defaults (8 waves, BCE_TAB_NT=3, BCE_EW_NT=2)
     "w4": ["-DBCE_TAB_WAVES=4"],
     "w8": ["-DBCE_TAB_WAVES=8"],
     "w4_prof": ["-DBCE_TAB_WAVES=4", "-DBCE_TAB_PROF=1"],
     "w8_prof": ["-DBCE_TAB_WAVES=8", "-DBCE_TAB_PROF=1"],
     "p64": ["-DBCE_TAB_PIECE=64"],
     "p64_prof": ["-DBCE_TAB_PIECE=64", "-DBCE_TAB_PROF=1"],
+    "nt1": ["-DBCE_TAB_NT=1"],  # nontemporal signal loads
+    "nt2": ["-DBCE_TAB_NT=2"],  # nontemporal per-unique stores
+    "nt3": ["-DBCE_TAB_NT=3"],
+    "nt7": ["-DBCE_TAB_NT=7"],
+    "nt3_w8": ["-DBCE_TAB_NT=3", "-DBCE_TAB_WAVES=8"],
+    "nt3_p64": ["-DBCE_TAB_NT=3", "-DBCE_TAB_PIECE=64"],
+    "nt3_prof": ["-DBCE_TAB_NT=3", "-DBCE_TAB_PROF=1"],
+    "ew1": ["-DBCE_EW_NT=1"],  # config-4 replay_step variants (bench.py --config c4)
+    "ew2": ["-DBCE_EW_NT=2"],
+    "ew3": ["-DBCE_EW_NT=3"],
+    "ew6": ["-DBCE_EW_NT=6"],
+    "nt7_w8": ["-DBCE_TAB_NT=7", "-DBCE_TAB_WAVES=8"],
+    "nt3_w8_r4": ["-DBCE_TAB_NT=3", "-DBCE_TAB_WAVES=8", "-DBCE_TAB_RING=4"],
+    "nt3_w8_r6": ["-DBCE_TAB_NT=3", "-DBCE_TAB_WAVES=8", "-DBCE_TAB_RING=6"],
+    "wide_nt": ["-DBCE_WIDE_AUX=2"],  # config-3 wide kernel: nontemporal sid/prob buffer loads
 }
 PHASES = ["load+xpose", "valid+sort", "walk", "per_market", "compaction", "per_unique_stores"]
 
