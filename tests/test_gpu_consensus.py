@@ -209,6 +209,31 @@ def test_c2_shape_every_table_size(S):
     _compare_vec(_run(g, max_len=32), exp, g["offsets"])
 
 
+@pytest.mark.parametrize("kind", ["extreme_in_range", "outside_range"])
+def test_c2_normalized_weight_division_paths(kind):
+    """LDS-table kernel with table weights spread over the whole exponent range (totals
+    that overflow the range of their terms' magnitudes), and tables holding tiny, huge,
+    negative, -0.0 and NaN weights: every output bit-exact against the oracle.  (Kept from
+    a measured-and-dropped reciprocal-based normalizedWeight division)"""
+    g = _c2_like(20000, 9000, 77 if kind == "extreme_in_range" else 78)
+    rng = np.random.default_rng(5)
+    S = len(g["rel"])
+    if kind == "extreme_in_range":
+        g["rel"] = np.ldexp(rng.random(S) + 0.5, rng.integers(-399, 399, S))
+        g["rel"][rng.random(S) < 0.3] = np.ldexp(1.0, 399)  # totals of several of these leave the range
+        g["rel"][rng.random(S) < 0.05] = 0.0
+    else:
+        pick = rng.random(S)
+        g["rel"][pick < 0.02] = 1e-200
+        g["rel"][(pick >= 0.02) & (pick < 0.04)] = -0.3
+        g["rel"][(pick >= 0.04) & (pick < 0.05)] = -0.0
+        g["rel"][(pick >= 0.05) & (pick < 0.06)] = 1e200
+        g["rel"][(pick >= 0.06) & (pick < 0.061)] = np.nan
+    g["present"][:] = 1
+    exp = orc.consensus_csr(g["offsets"], g["sid"], g["prob"], g["rel"], g["conf"], g["present"])
+    _compare_vec(_run(g, max_len=32), exp, g["offsets"])
+
+
 @pytest.mark.parametrize("S,L,base", [(10000, 32, 0), (10000, 32, 4), (10000, 32, 1), (12000, 32, 0),
                                       (30000, 32, 0), (5000, 16, 0), (40000, 8, 3)])
 def test_compact_mode(S, L, base):

@@ -26,7 +26,18 @@ struct Args {
 };
 
 // SHAPE: 0 piece64, 1 row128, 2 linear, 3 half-row 128-B pieces for probs too
-template <int SHAPE>
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ uint4 ld16(const uint32_t* p) {
+  if (NT) { const u4v v = __builtin_nontemporal_load(reinterpret_cast<const u4v*>(p)); return make_uint4(v.x, v.y, v.z, v.w); }
+  return *reinterpret_cast<const uint4*>(p);
+}
+template <bool NT>
+__device__ __forceinline__ void st16(uint32_t* p, uint4 v) {
+  if (NT) { const u4v x = {v.x, v.y, v.z, v.w}; __builtin_nontemporal_store(x, reinterpret_cast<u4v*>(p)); }
+  else *reinterpret_cast<uint4*>(p) = v;
+}
+template <int SHAPE, bool NT = false>
 __device__ __forceinline__ void tile_load(const Args& a, int64_t B, int lane, uint4 (&s)[8], uint4 (&p)[16]) {
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -34,7 +45,7 @@ __device__ __forceinline__ void tile_load(const Args& a, int64_t B, int lane, ui
     if (SHAPE == 0) e = 32 * (16 * (k & 3) + (lane >> 2)) + 16 * (k >> 2) + 4 * (lane & 3);
     else if (SHAPE == 1 || SHAPE == 3) e = 32 * (8 * k + (lane >> 3)) + 4 * (lane & 7);
     else e = 256 * k + 4 * lane;
-    s[k] = *reinterpret_cast<const uint4*>(a.sid + B + e);
+    s[k] = ld16<NT>(a.sid + B + e);
   }
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
@@ -43,18 +54,18 @@ __device__ __forceinline__ void tile_load(const Args& a, int64_t B, int lane, ui
     else if (SHAPE == 1) e = 64 * (4 * k + (lane >> 4)) + 4 * (lane & 15);
     else if (SHAPE == 3) e = 64 * (8 * (k & 7) + (lane >> 3)) + 32 * (k >> 3) + 4 * (lane & 7);
     else e = 256 * k + 4 * lane;
-    p[k] = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint32_t*>(a.prob + B) + e);
+    p[k] = ld16<NT>(reinterpret_cast<const uint32_t*>(a.prob + B) + e);
   }
 }
 
-template <int W, int SHAPE, bool PF = false>
+template <int W, int SHAPE, bool PF = false, bool NT = false>
 __global__ __launch_bounds__(64 * W) void tile_mix(Args a) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t n_tiles = a.M / 64;
   const int64_t stride = (int64_t)gridDim.x * W;
   uint4 sn[8], pn[16];
   int64_t tile = (int64_t)blockIdx.x * W + wv;
-  if (PF && tile < n_tiles) tile_load<SHAPE>(a, tile * 64 * 32, lane, sn, pn);
+  if (PF && tile < n_tiles) tile_load<SHAPE, NT>(a, tile * 64 * 32, lane, sn, pn);
   for (; tile < n_tiles; tile += stride) {
     const int64_t B = tile * 64 * 32;  // first signal of the tile
     uint4 s[8];
@@ -64,9 +75,9 @@ __global__ __launch_bounds__(64 * W) void tile_mix(Args a) {
       for (int k = 0; k < 8; ++k) s[k] = sn[k];
 #pragma unroll
       for (int k = 0; k < 16; ++k) p[k] = pn[k];
-      if (tile + stride < n_tiles) tile_load<SHAPE>(a, (tile + stride) * 64 * 32, lane, sn, pn);
+      if (tile + stride < n_tiles) tile_load<SHAPE, NT>(a, (tile + stride) * 64 * 32, lane, sn, pn);
     } else {
-      tile_load<SHAPE>(a, B, lane, s, p);
+      tile_load<SHAPE, NT>(a, B, lane, s, p);
     }
     // trivial compute: fold so nothing is dead
     uint32_t acc = 0;
@@ -88,7 +99,7 @@ __global__ __launch_bounds__(64 * W) void tile_mix(Args a) {
       if (SHAPE == 0) e = 32 * (16 * (k & 3) + (lane >> 2)) + 16 * (k >> 2) + 4 * (lane & 3);
       else if (SHAPE == 1 || SHAPE == 3) e = 32 * (8 * k + (lane >> 3)) + 4 * (lane & 7);
       else e = 256 * k + 4 * lane;
-      *reinterpret_cast<uint4*>(a.usid + B + e) = s[k];
+      st16<NT>(a.usid + B + e, s[k]);
     }
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
@@ -97,8 +108,8 @@ __global__ __launch_bounds__(64 * W) void tile_mix(Args a) {
       else if (SHAPE == 1) e = 64 * (4 * k + (lane >> 4)) + 4 * (lane & 15);
       else if (SHAPE == 3) e = 64 * (8 * (k & 7) + (lane >> 3)) + 32 * (k >> 3) + 4 * (lane & 7);
       else e = 256 * k + 4 * lane;
-      *reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(a.w + B) + e) = p[k];
-      *reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(a.nw + B) + e) = p[k];
+      st16<NT>(reinterpret_cast<uint32_t*>(a.w + B) + e, p[k]);
+      st16<NT>(reinterpret_cast<uint32_t*>(a.nw + B) + e, p[k]);
     }
   }
 }
@@ -132,22 +143,16 @@ int main() {
     printf("{\"probe\": \"%s\", \"ms\": %.5f, \"GBps\": %.1f}\n", name, ms, bytes / ms / 1e6);
     fflush(stdout);
   };
-  // one workgroup per CU (the LDS table's occupancy) and, for comparison, four
-  timeit("piece64 w4 1wg/cu", [&] { tile_mix<4, 0><<<cus, 256>>>(a); });
-  timeit("piece64 w8 1wg/cu", [&] { tile_mix<8, 0><<<cus, 512>>>(a); });
-  timeit("piece64 w16 1wg/cu", [&] { tile_mix<16, 0><<<cus, 1024>>>(a); });
-  timeit("row128 w4 1wg/cu", [&] { tile_mix<4, 1><<<cus, 256>>>(a); });
-  timeit("row128 w8 1wg/cu", [&] { tile_mix<8, 1><<<cus, 512>>>(a); });
-  timeit("linear w4 1wg/cu", [&] { tile_mix<4, 2><<<cus, 256>>>(a); });
-  timeit("linear w8 1wg/cu", [&] { tile_mix<8, 2><<<cus, 512>>>(a); });
-  timeit("linear w16 1wg/cu", [&] { tile_mix<16, 2><<<cus, 1024>>>(a); });
-  timeit("piece64 w4 4wg/cu", [&] { tile_mix<4, 0><<<4 * cus, 256>>>(a); });
-  timeit("linear w4 4wg/cu", [&] { tile_mix<4, 2><<<4 * cus, 256>>>(a); });
-  timeit("half128 w4 1wg/cu", [&] { tile_mix<4, 3><<<cus, 256>>>(a); });
-  timeit("piece64 w4 1wg/cu prefetch", [&] { tile_mix<4, 0, true><<<cus, 256>>>(a); });
-  timeit("half128 w4 1wg/cu prefetch", [&] { tile_mix<4, 3, true><<<cus, 256>>>(a); });
-  timeit("row128 w4 1wg/cu prefetch", [&] { tile_mix<4, 1, true><<<cus, 256>>>(a); });
-  timeit("linear w4 1wg/cu prefetch", [&] { tile_mix<4, 2, true><<<cus, 256>>>(a); });
-  timeit("half128 w8 1wg/cu prefetch", [&] { tile_mix<8, 3, true><<<cus, 512>>>(a); });
+  // round 2b: nontemporal loads + per-unique stores (the kernel's BCE_TAB_NT=3), half128 shape
+  for (int r = 0; r < 2; ++r) {
+    timeit("half128 w4 1wg/cu", [&] { tile_mix<4, 3><<<cus, 256>>>(a); });
+    timeit("half128 w8 1wg/cu", [&] { tile_mix<8, 3><<<cus, 512>>>(a); });
+    timeit("half128 w4 1wg/cu nt", [&] { tile_mix<4, 3, false, true><<<cus, 256>>>(a); });
+    timeit("half128 w8 1wg/cu nt", [&] { tile_mix<8, 3, false, true><<<cus, 512>>>(a); });
+    timeit("half128 w16 1wg/cu nt", [&] { tile_mix<16, 3, false, true><<<cus, 1024>>>(a); });
+    timeit("linear w8 1wg/cu nt", [&] { tile_mix<8, 2, false, true><<<cus, 512>>>(a); });
+    timeit("half128 w8 1wg/cu nt prefetch", [&] { tile_mix<8, 3, true, true><<<cus, 512>>>(a); });
+    timeit("half128 w4 4wg/cu nt", [&] { tile_mix<4, 3, false, true><<<4 * cus, 256>>>(a); });
+  }
   return 0;
 }
