@@ -65,6 +65,8 @@ def parse(argv=None):
                         "the north star's fixed-order trees within 1e-9 -- for c3, with the exact-mode "
                         "time reported beside it)")
     p.add_argument("--agents", type=int, default=16384, help="config 5 agents")
+    p.add_argument("--events", default="step", choices=["step", "region"],
+                   help="HIP events around every timed step, or one pair around the timed region")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=2.0, help="wall-clock budget of the CPU baseline")
     p.add_argument("--no-parity", action="store_true")
@@ -175,20 +177,29 @@ def timed_loop(step, args, world, stream=None):
     barrier(world)
     synchronize(args)
     ev = None
+    region = getattr(args, "events", "step") == "region"
     if stream is not None:
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(1 if region else args.steps)]
     t0 = time.perf_counter()
+    if ev and region:
+        ev[0][0].record(stream)
     for i in range(args.steps):
-        if ev:
+        if ev and not region:
             ev[i][0].record(stream)
         step()
-        if ev:
+        if ev and not region:
             ev[i][1].record(stream)
+    if ev and region:
+        ev[0][1].record(stream)
     synchronize(args)
     t1 = time.perf_counter()
     barrier(world)
     synchronize(args)
-    per = float(np.mean([a.elapsed_time(b) for a, b in ev])) / 1e3 if ev else (t1 - t0) / max(args.steps, 1)
+    if ev and region:  # launches + the boundaries between them, per step
+        per = ev[0][0].elapsed_time(ev[0][1]) / 1e3 / max(args.steps, 1)
+    else:
+        per = float(np.mean([a.elapsed_time(b) for a, b in ev])) / 1e3 if ev else (t1 - t0) / max(args.steps, 1)
     return max_over_ranks(t1 - t0, world, _dev(args)), per, prewarm
 
 
