@@ -66,8 +66,8 @@ def parse(argv=None):
                         "time reported beside it)")
     p.add_argument("--agents", type=int, default=16384, help="config 5 agents")
     p.add_argument("--events", default="region", choices=["step", "region"],
-                   help="one HIP event pair around the timed region (default: per-step average incl. the
-                        launch boundaries), or a pair around every step (adds ~6 us per step)")
+                   help="one HIP event pair around the timed region (default: per-step average "
+                        "incl. the launch boundaries), or a pair around every step (~6 us per step)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=2.0, help="wall-clock budget of the CPU baseline")
     p.add_argument("--no-parity", action="store_true")
