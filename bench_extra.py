@@ -71,23 +71,51 @@ def run_extra(args, world, rank):
 # CPU baselines: the oracle's C restatement (test infrastructure, oracle/) on host threads
 # ---------------------------------------------------------------------------------------
 def _cpu_c3(off, sid, prob, table_host, args):
+    """(cpu_baseline dict, the restatement's outputs of the first pass) or (None, None)."""
     if args.no_cpu_baseline:
-        return None
+        return None, None
     from bench import cpu_consensus_threaded
 
     rel, conf, present = table_host
     T = _threads()
-    t0, reps = time.perf_counter(), 0
+    t0, reps, out = time.perf_counter(), 0, None
     while True:
-        cpu_consensus_threaded(off, sid, prob, rel, conf, present, T)
+        o = cpu_consensus_threaded(off, sid, prob, rel, conf, present, T)
+        out = out or o
         reps += 1
         dt = time.perf_counter() - t0
         if dt >= args.cpu_seconds:
             break
     n = int(off[-1])
-    return {"value": n * reps / dt, "unit": "signals/s", "cores": T, "kind": "port", "label": "restatement",
-            "sample": f"this rank's whole shard ({len(off) - 1} markets, {n} signals), oracle/bce_oracle.c on "
-                      f"{T} threads, {reps} passes in {dt:.2f} s"}
+    return ({"value": n * reps / dt, "unit": "signals/s", "cores": T, "kind": "port", "label": "restatement",
+             "sample": f"this rank's whole shard ({len(off) - 1} markets, {n} signals), oracle/bce_oracle.c on "
+                       f"{T} threads, {reps} passes in {dt:.2f} s"}, out)
+
+
+def _parity_c3(res, cpu, off, exact, tol=1e-9):
+    """Every output at full size vs the restatement: integer outputs, usid and weight bit for
+    bit; consensus / confidence / total weight / normalizedWeight bit for bit in exact mode,
+    within the north star's 1e-9 absolute in fast mode (tree-ordered totals).  Returns
+    ({output: ok}, max abs deviation over the float outputs)."""
+    got = {k: getattr(res, k).cpu().numpy() for k in
+           ("consensus", "confidence", "total_weight", "n_unique", "err_idx", "usid", "weight", "nweight")}
+    u = cpu["n_unique"].astype(np.int64)
+    pos = np.repeat(off[:-1], u) + (np.arange(int(u.sum())) - np.repeat(np.cumsum(u) - u, u))
+    ok, dev = {}, 0.0
+    for k in ("n_unique", "err_idx"):
+        ok[k] = bool(np.array_equal(got[k], cpu[k]))
+    for k in ("usid", "weight"):
+        ok[k] = bool(np.array_equal(got[k][pos], cpu[k][pos], equal_nan=True))
+    for k in ("consensus", "confidence", "total_weight", "nweight"):
+        a, b = (got[k][pos], cpu[k][pos]) if k == "nweight" else (got[k], cpu[k])
+        if exact:
+            ok[k] = bool(np.array_equal(a, b, equal_nan=True))
+        else:
+            fin = np.isfinite(a) & np.isfinite(b)
+            d = float(np.max(np.abs(a[fin] - b[fin]))) if fin.any() else 0.0
+            dev = max(dev, d)
+            ok[k] = bool(d <= tol and np.array_equal(np.isnan(a), np.isnan(b)))
+    return ok, dev
 
 
 def _cpu_c4(args, S_sample=2_000_000):
@@ -238,6 +266,22 @@ def _c3(args, world, rank, barrier, max_over, sum_over):
     bytes_step = 12 * n + 8 * (Mloc + 1) + 32 * Mloc + 20 * sum_u + 17 * touched
     achieved = bytes_step / per / 1e9
     sig = sum_over(float(n * args.steps), world)
+    cpu_line, parity = None, None
+    if rank == 0 and world == 1:
+        cpu_line, cpu_out = _cpu_c3(off, sid, prob, table_host, args)
+        if cpu_out is not None and not args.no_parity:
+            # full-size parity of both modes: res holds the timed mode's last step; one more
+            # step in the other mode into a second result
+            res2 = batch._alloc(len(off) - 1, n, dev, True, True)
+            batch.consensus(d_off, d_sid, d_prob, table, plan=plan, mode=other, out=res2)
+            torch.cuda.synchronize()
+            parity = {}
+            for md, r in ((mode, res), (other, res2)):
+                ok, dv = _parity_c3(r, cpu_out, off, exact=(md == "exact"))
+                parity[md] = {"all_ok": all(ok.values()), "outputs": ok,
+                              "tolerance": "bit-exact" if md == "exact" else "1e-9 abs (float outputs)",
+                              "max_abs_dev": dv}
+            del res2
     return {
         "metric": "signals aggregated/sec (node), 100M-signal ragged CSR (config 3)",
         "value": sig / wall, "unit": "signals/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -252,7 +296,8 @@ def _c3(args, world, rank, barrier, max_over, sum_over):
                      "bytes_per_launch": bytes_step, "avg_launch_ms": per * 1e3,
                      f"{other}_mode": {"ms_per_step": wall2 / a2.steps * 1e3, "avg_launch_ms": per2 * 1e3,
                                        "frac": bytes_step / per2 / 1e9 / HBM_PEAK_GBS}},
-        "cpu_baseline": _cpu_c3(off, sid, prob, table_host, args) if rank == 0 and world == 1 else None,
+        "cpu_baseline": cpu_line,
+        "parity_vs_oracle": parity,
     }
 
 
