@@ -365,6 +365,8 @@ def _c4(args, world, rank, barrier, max_over, sum_over):
     from bayesian_engine import _native as N
 
     N.check_faults(dev, "c4 timed steps")
+    parity = _parity_c4(step, state, pool, (rel, conf, t_us, present, view), S, now0, day, args) \
+        if rank == 0 and world == 1 else None
     p = 0.1
     bps = 24 + 0.25 + 8 + p * (8 + 24 + 1)
     achieved = bps * S / per / 1e9
@@ -382,7 +384,40 @@ def _c4(args, world, rank, barrier, max_over, sum_over):
                      "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc("pmc_c4.json", sources_this_rank=S),
                      "kernel": "replay_step_kernel", "bytes_per_launch": bps * S, "avg_launch_ms": per * 1e3},
         "cpu_baseline": _cpu_c4(args) if rank == 0 and world == 1 else None,
+        "parity_vs_oracle": parity,
     }
+
+
+def _parity_c4(step, state, pool, arrays, S, now0, day, args):
+    """One more replay step on all S sources vs the restatement on a host snapshot of the
+    table: rel / conf / t / present bit for bit, the decayed view within 2 ulp (exp2 vs
+    glibc pow) with the bit-exact share reported."""
+    if args.no_parity or args.no_cpu_baseline:
+        return None
+    import sys
+
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as orc
+
+    rel, conf, t_us, present, view = arrays
+    snap = [x[:S].cpu().numpy() for x in (rel, conf, t_us, present)]
+    k = state["k"]
+    step()
+    torch.cuda.synchronize()
+    fl = pool[k % len(pool)].cpu().numpy()
+    flags = ((fl[:, None] >> (2 * np.arange(4, dtype=np.uint8))) & 3).reshape(-1)[:S].astype(np.uint8)
+    now = now0 + k * day
+    v_exp = orc.decay_view(snap[0], snap[2], snap[3], now)
+    r2, c2, t2, p2 = orc.outcome_update(snap[0], snap[1], snap[2], snap[3], flags, now)
+    v = view[:S].cpu().numpy()
+    ulps = np.abs(v - v_exp) / np.spacing(np.abs(v_exp))
+    ok = {"rel": bool(np.array_equal(rel[:S].cpu().numpy(), r2)),
+          "conf": bool(np.array_equal(conf[:S].cpu().numpy(), c2)),
+          "t_us": bool(np.array_equal(t_us[:S].cpu().numpy(), t2)),
+          "present": bool(np.array_equal(present[:S].cpu().numpy(), p2)),
+          "view_2ulp": bool(np.all(ulps <= 2.0))}
+    return {"all_ok": all(ok.values()), "outputs": ok, "sources": S, "participants": int((flags & 1).sum()),
+            "view_bit_exact_share": float(np.mean(v == v_exp)), "view_max_ulps": float(ulps.max())}
 
 
 # ---------------------------------------------------------------------------------------
@@ -435,6 +470,9 @@ def _c5(args, world, rank, barrier, max_over, sum_over):
 
     wall, per = _timed(step, args, world, torch.cuda.current_stream(dev), barrier, max_over)
     kern = float(np.mean([a.elapsed_time(b) for a, b in ev_k[-args.steps:]])) / 1e3
+    parity = None
+    if rank == 0 and world == 1 and not args.no_parity and not args.no_cpu_baseline:
+        parity = _parity_c5(P, L, N, st, args)
     # algorithmic: P once, w, agreement counts, consensus + null out (the vote bits, A*M/8
     # written and read back, are this implementation's intermediate -- in `traffic`)
     bytes_iter = 8 * A * Mloc + 16 * A + 9 * Mloc
@@ -459,7 +497,41 @@ def _c5(args, world, rank, barrier, max_over, sum_over):
                               "why": "w^T P is a GEMV at 0.25 flop/B: HBM-bound at ~2% of the fp64 matrix peak "
                                      "even if every flop ran on MFMA; exact agent-order sums on the VALU"}},
         "cpu_baseline": _cpu_c5(P, args) if rank == 0 and world == 1 else None,
+        "parity_vs_oracle": parity,
     }
+
+
+def _parity_c5(P, L, N, st, args, m=4096):
+    """The single-read iteration on the first m market columns of this rank's P (a strided
+    view: ld = the full row) from w = 0.5 vs the restatement's first iteration on the same
+    columns: consensus, null flags, per-agent agreement counts and resolved count, bit for bit."""
+    import sys
+
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as orc
+
+    A, Mloc = P.shape
+    m = min(m, Mloc)
+    dev = P.device
+    w = torch.full((A,), 0.5, dtype=torch.float64, device=dev)
+    cons = torch.empty(m, dtype=torch.float64, device=dev)
+    nul = torch.empty(m, dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(A + 1, dtype=torch.int64, device=dev)
+    K = (m + 63) // 64
+    votes = torch.empty((K, A), dtype=torch.int64, device=dev)
+    words = torch.empty((2, K), dtype=torch.int64, device=dev)
+    N.check(L.bce_reestimate_consensus_votes(N.ptr(P), A, m, P.stride(0), N.ptr(w), N.ptr(cons), N.ptr(nul),
+                                             N.ptr(votes), N.ptr(words[0]), N.ptr(words[1]), st), "c5 parity p1")
+    N.check(L.bce_reestimate_agreement_votes(N.ptr(votes), A, m, N.ptr(words[0]), N.ptr(words[1]),
+                                             N.ptr(cnt[:A]), N.ptr(cnt[A:]), st), "c5 parity p2")
+    torch.cuda.synchronize()
+    _, c_exp, n_exp, a_exp = orc.reestimate(P[:, :m].cpu().numpy(), 1)
+    resolved_exp = int(np.sum(n_exp[0] == 0))
+    ok = {"consensus": bool(np.array_equal(cons.cpu().numpy(), c_exp[0])),
+          "null": bool(np.array_equal(nul.cpu().numpy(), n_exp[0])),
+          "agreement": bool(np.array_equal(cnt[:A].cpu().numpy(), a_exp[0])),
+          "resolved": int(cnt[A].item()) == resolved_exp}
+    return {"all_ok": all(ok.values()), "outputs": ok, "sample": f"{A} agents x the first {m} market columns"}
 
 
 # ---------------------------------------------------------------------------------------
