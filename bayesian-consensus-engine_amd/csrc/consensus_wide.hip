@@ -44,7 +44,7 @@
 #define BCE_WIDE_WPE_BIG 4  // the same for workgroups of >= 4 waves
 #endif
 #ifndef BCE_WIDE_WPE
-#define BCE_WIDE_WPE 2  // min waves per SIMD (register budget)
+#define BCE_WIDE_WPE 4  // min waves per SIMD (register budget; 4 vs 2: exact -1.3%, fast unchanged)
 #endif
 #ifndef BCE_WIDE_PROF
 #define BCE_WIDE_PROF 0  // experiment builds only (tools/wide_variants.py): per-phase s_memtime

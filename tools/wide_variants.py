@@ -33,6 +33,8 @@ VARIANTS = {
     "kwr96": ["-DBCE_WIDE_KWR=96"],
     "nopipe": ["-DBCE_WIDE_PIPE=0"],
     "w2": ["-DBCE_WIDE_WPE_BIG=2"],
+    "wpe4": ["-DBCE_WIDE_WPE=4"],  # 4 waves/SIMD (<= 128 VGPRs) for the 1- and 2-wave kernels too
+    "wpe3": ["-DBCE_WIDE_WPE=3"],
     "nwb0": ["-DBCE_WIDE_NWB=0"],
     "nwbf1": ["-DBCE_WIDE_NWBF=1"],
     "nwbf2": ["-DBCE_WIDE_NWBF=2"],
