@@ -97,6 +97,9 @@ __device__ __forceinline__ void tab_st16(double* p, double x0, double x1) {
     *reinterpret_cast<double2*>(p) = make_double2(x0, x1);
   }
 }
+#ifndef BCE_TAB_MAP
+#define BCE_TAB_MAP 1  // 1: wave-major tile order (see the tile loop), 0: block-major
+#endif
 constexpr int kTabWaves = BCE_TAB_WAVES;  // waves per workgroup; one workgroup per CU (LDS-bound)
 constexpr int kPL = BCE_TAB_PIECE / 16;    // lanes per piece (16 B each): 4 or 8
 constexpr int kLB = (kPL == 8) ? 3 : 2;    // log2 kPL
@@ -258,7 +261,10 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
   // Software pipeline: the next tile's metadata is read at the top of a tile and its
   // signals are loaded right after this tile's sort, so they arrive during the walk,
   // the compaction and the stores.
-  int64_t tile = (int64_t)blockIdx.x * kTabWaves + w;
+  // wave-major tile order: tile = w * grid + block, so the tiles in flight at any moment
+  // are spread over every workgroup (and XCD) instead of 8 consecutive tiles per CU
+  // (tools/tile_probe.hip: 0.204 -> 0.195 ms for the same bytes and shapes)
+  int64_t tile = BCE_TAB_MAP ? (int64_t)w * gridDim.x + blockIdx.x : (int64_t)blockIdx.x * kTabWaves + w;
   Meta cur = meta(tile, lane_id());
   uint32_t s[32], pw[64];
 #if BCE_TAB_PROF

@@ -58,13 +58,20 @@ __device__ __forceinline__ void tile_load(const Args& a, int64_t B, int lane, ui
   }
 }
 
-template <int W, int SHAPE, bool PF = false, bool NT = false>
+template <int W, int SHAPE, bool PF = false, bool NT = false, int MAP = 0>
 __global__ __launch_bounds__(64 * W) void tile_mix(Args a) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t n_tiles = a.M / 64;
   const int64_t stride = (int64_t)gridDim.x * W;
   uint4 sn[8], pn[16];
-  int64_t tile = (int64_t)blockIdx.x * W + wv;
+  // MAP 0: a workgroup's waves take consecutive tiles (the kernel's); 1: wave-major, so
+  // consecutive tiles land on consecutive workgroups (and XCDs); 2: consecutive tiles on
+  // the same XCD's workgroups (blockIdx % 8 = XCD)
+  const int64_t G = gridDim.x;
+  int64_t tile;
+  if (MAP == 0) tile = (int64_t)blockIdx.x * W + wv;
+  else if (MAP == 1) tile = (int64_t)wv * G + blockIdx.x;
+  else tile = (int64_t)(((blockIdx.x & 7) * (G / 8) + (blockIdx.x >> 3)) * W + wv);
   if (PF && tile < n_tiles) tile_load<SHAPE, NT>(a, tile * 64 * 32, lane, sn, pn);
   for (; tile < n_tiles; tile += stride) {
     const int64_t B = tile * 64 * 32;  // first signal of the tile
@@ -143,16 +150,13 @@ int main() {
     printf("{\"probe\": \"%s\", \"ms\": %.5f, \"GBps\": %.1f}\n", name, ms, bytes / ms / 1e6);
     fflush(stdout);
   };
-  // round 2b: nontemporal loads + per-unique stores (the kernel's BCE_TAB_NT=3), half128 shape
-  for (int r = 0; r < 2; ++r) {
-    timeit("half128 w4 1wg/cu", [&] { tile_mix<4, 3><<<cus, 256>>>(a); });
-    timeit("half128 w8 1wg/cu", [&] { tile_mix<8, 3><<<cus, 512>>>(a); });
-    timeit("half128 w4 1wg/cu nt", [&] { tile_mix<4, 3, false, true><<<cus, 256>>>(a); });
-    timeit("half128 w8 1wg/cu nt", [&] { tile_mix<8, 3, false, true><<<cus, 512>>>(a); });
-    timeit("half128 w16 1wg/cu nt", [&] { tile_mix<16, 3, false, true><<<cus, 1024>>>(a); });
-    timeit("linear w8 1wg/cu nt", [&] { tile_mix<8, 2, false, true><<<cus, 512>>>(a); });
-    timeit("half128 w8 1wg/cu nt prefetch", [&] { tile_mix<8, 3, true, true><<<cus, 512>>>(a); });
-    timeit("half128 w4 4wg/cu nt", [&] { tile_mix<4, 3, false, true><<<4 * cus, 256>>>(a); });
+  // round 2b: tile -> wave mappings at the kernel's shape (half128, nt, 8 waves, 1 wg/cu)
+  for (int r = 0; r < 3; ++r) {
+    timeit("half128 w8 1wg/cu nt map0", [&] { tile_mix<8, 3, false, true, 0><<<cus, 512>>>(a); });
+    timeit("half128 w8 1wg/cu nt map1", [&] { tile_mix<8, 3, false, true, 1><<<cus, 512>>>(a); });
+    timeit("half128 w8 1wg/cu nt map2", [&] { tile_mix<8, 3, false, true, 2><<<cus, 512>>>(a); });
+    timeit("half128 w4 4wg/cu nt map0", [&] { tile_mix<4, 3, false, true, 0><<<4 * cus, 256>>>(a); });
+    timeit("half128 w4 4wg/cu nt map1", [&] { tile_mix<4, 3, false, true, 1><<<4 * cus, 256>>>(a); });
   }
   return 0;
 }
