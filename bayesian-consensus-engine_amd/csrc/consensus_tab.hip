@@ -258,10 +258,9 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
     }
   };
 
-  // Software pipeline: the next tile's metadata is read at the top of a tile and its
-  // signals are loaded right after this tile's sort, so they arrive during the walk,
-  // the compaction and the stores.
-  // wave-major tile order: tile = w * grid + block, so the tiles in flight at any moment
+  // The next tile's metadata is read at the top of each tile (loading the next tile's
+  // signals ahead, or the first tile's under the table staging, measured slower: spills).
+  // Wave-major tile order: tile = w * grid + block, so the tiles in flight at any moment
   // are spread over every workgroup (and XCD) instead of 8 consecutive tiles per CU
   // (tools/tile_probe.hip: 0.204 -> 0.195 ms for the same bytes and shapes)
   int64_t tile = BCE_TAB_MAP ? (int64_t)w * gridDim.x + blockIdx.x : (int64_t)blockIdx.x * kTabWaves + w;

@@ -71,7 +71,12 @@ __global__ __launch_bounds__(64 * W) void tile_mix(Args a) {
   int64_t tile;
   if (MAP == 0) tile = (int64_t)blockIdx.x * W + wv;
   else if (MAP == 1) tile = (int64_t)wv * G + blockIdx.x;
-  else tile = (int64_t)(((blockIdx.x & 7) * (G / 8) + (blockIdx.x >> 3)) * W + wv);
+  else if (MAP == 2) tile = (int64_t)(((blockIdx.x & 7) * (G / 8) + (blockIdx.x >> 3)) * W + wv);
+  else {  // wave-major with chunks of C = MAP - 1 consecutive tiles on one XCD
+    constexpr int C = MAP - 1;
+    const int64_t x = blockIdx.x & 7, sl = blockIdx.x >> 3;
+    tile = (int64_t)wv * G + ((sl / C) * 8 + x) * C + (sl % C);
+  }
   if (PF && tile < n_tiles) tile_load<SHAPE, NT>(a, tile * 64 * 32, lane, sn, pn);
   for (; tile < n_tiles; tile += stride) {
     const int64_t B = tile * 64 * 32;  // first signal of the tile
@@ -154,9 +159,12 @@ int main() {
   for (int r = 0; r < 3; ++r) {
     timeit("half128 w8 1wg/cu nt map0", [&] { tile_mix<8, 3, false, true, 0><<<cus, 512>>>(a); });
     timeit("half128 w8 1wg/cu nt map1", [&] { tile_mix<8, 3, false, true, 1><<<cus, 512>>>(a); });
-    timeit("half128 w8 1wg/cu nt map2", [&] { tile_mix<8, 3, false, true, 2><<<cus, 512>>>(a); });
-    timeit("half128 w4 4wg/cu nt map0", [&] { tile_mix<4, 3, false, true, 0><<<4 * cus, 256>>>(a); });
-    timeit("half128 w4 4wg/cu nt map1", [&] { tile_mix<4, 3, false, true, 1><<<4 * cus, 256>>>(a); });
+    timeit("half128 w8 1wg/cu nt map1 chunk2", [&] { tile_mix<8, 3, false, true, 3><<<cus, 512>>>(a); });
+    timeit("half128 w8 1wg/cu nt map1 chunk4", [&] { tile_mix<8, 3, false, true, 5><<<cus, 512>>>(a); });
+    timeit("half128 w8 1wg/cu nt map1 chunk8", [&] { tile_mix<8, 3, false, true, 9><<<cus, 512>>>(a); });
+    timeit("half128 w4 1wg/cu nt map1", [&] { tile_mix<4, 3, false, true, 1><<<cus, 256>>>(a); });
+    timeit("half128 w16 1wg/cu nt map1", [&] { tile_mix<16, 3, false, true, 1><<<cus, 1024>>>(a); });
+    timeit("linear w8 1wg/cu nt map1", [&] { tile_mix<8, 2, false, true, 1><<<cus, 512>>>(a); });
   }
   return 0;
 }
