@@ -27,14 +27,19 @@ __global__ void fill(double* P, int64_t n) {
   }
 }
 
-template <int CPL, int ROWS, bool NT>
+template <int CPL, int ROWS, bool NT, bool SYNC = false, int MAP = 0>
 __global__ __launch_bounds__(256) void votes_k(const double* __restrict__ P, int64_t A, int64_t M, int64_t ld,
                                                const double* __restrict__ w, double* __restrict__ cons,
                                                unsigned long long* __restrict__ vbits) {
   const int lane = threadIdx.x & 63;
-  const int64_t g = blockIdx.x * 4 + (threadIdx.x >> 6);  // wave group of 64*CPL columns
+  // wave group of 64*CPL columns; MAP 1: wave-major (group = wave * grid + block), MAP 2:
+  // consecutive groups on one XCD (blockIdx % 8), MAP 0: block-major
+  const int64_t G = gridDim.x;
+  const int64_t g = MAP == 1 ? (int64_t)(threadIdx.x >> 6) * G + blockIdx.x
+                  : MAP == 2 ? (int64_t)(((blockIdx.x & 7) * (G / 8) + (blockIdx.x >> 3)) * 4 + (threadIdx.x >> 6))
+                             : (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t c0 = g * 64 * CPL;
-  if (c0 >= M) return;
+  if (!SYNC && c0 >= M) return;
   const int64_t m = c0 + lane * CPL;
   const bool in = m + CPL - 1 < M;
   const double* col = P + (in ? m : 0);
@@ -47,9 +52,12 @@ __global__ __launch_bounds__(256) void votes_k(const double* __restrict__ P, int
 #pragma unroll
     for (int q = 0; q < ROWS; ++q) {
       const double* src = col + (a + q) * ld;
-      if constexpr (CPL == 2) {
-        d2v x = NT ? __builtin_nontemporal_load(reinterpret_cast<const d2v*>(src)) : *reinterpret_cast<const d2v*>(src);
-        v[q][0] = x.x; v[q][1] = x.y;
+      if constexpr (CPL == 2 || CPL == 4) {
+#pragma unroll
+        for (int h = 0; h < CPL / 2; ++h) {
+          d2v x = NT ? __builtin_nontemporal_load(reinterpret_cast<const d2v*>(src) + h) : reinterpret_cast<const d2v*>(src)[h];
+          v[q][2 * h] = x.x; v[q][2 * h + 1] = x.y;
+        }
       } else {
         v[q][0] = NT ? __builtin_nontemporal_load(src) : *src;
       }
@@ -68,10 +76,11 @@ __global__ __launch_bounds__(256) void votes_k(const double* __restrict__ P, int
         mine[e] = (lane == q) ? b : mine[e];
       }
     }
-    if (lane < ROWS) {
+    if (lane < ROWS && c0 < M) {
 #pragma unroll
       for (int e = 0; e < CPL; ++e) vb[e * A + a + lane] = mine[e];
     }
+    if (SYNC) __syncthreads();
   }
   if (in) {
 #pragma unroll
@@ -124,20 +133,16 @@ int main(int argc, char** argv) {
     fflush(stdout);
     (void)cpl;
   };
-#define V(C, R, N)                                                                                      \
-  run("cpl" #C "_rows" #R "_nt" #N, C, [&] {                                                            \
+#define V(C, R, N, S, MP)                                                                               \
+  run("cpl" #C "_rows" #R "_nt" #N "_sync" #S "_map" #MP, C, [&] {                                      \
     const int64_t groups = (M + 64 * C - 1) / (64 * C);                                                 \
-    votes_k<C, R, N><<<(unsigned)((groups + 3) / 4), 256>>>(P, A, M, ld, w, cons, vb);                  \
+    votes_k<C, R, N, S, MP><<<(unsigned)(((groups + 3) / 4 + 7) & ~7), 256>>>(P, A, M, ld, w, cons, vb); \
   })
   for (int round = 0; round < 2; ++round) {
-    V(1, 16, 0);
-    V(1, 16, 1);
-    V(1, 32, 0);
-    V(1, 32, 1);
-    V(2, 8, 0);
-    V(2, 8, 1);
-    V(2, 16, 0);
-    V(2, 16, 1);
+    V(1, 16, 0, 0, 0);
+    V(1, 16, 0, 0, 1);
+    V(1, 16, 0, 0, 2);
+    V(2, 16, 0, 0, 1);
   }
   return 0;
 }
