@@ -97,6 +97,9 @@ __device__ __forceinline__ void tab_st16(double* p, double x0, double x1) {
     *reinterpret_cast<double2*>(p) = make_double2(x0, x1);
   }
 }
+#ifndef BCE_TAB_PRIO
+#define BCE_TAB_PRIO 1  // raised wave priority from the walk through the stores (0: off)
+#endif
 #ifndef BCE_TAB_MAP
 #define BCE_TAB_MAP 1  // 1: wave-major tile order (see the tile loop), 0: block-major
 #endif
@@ -378,6 +381,10 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
     __builtin_amdgcn_sched_barrier(0);
 
     // ---- walk (core.py:107-144 in sorted-source order) ----------------------------------
+    // raised wave priority from the walk through the stores: of the two waves on a SIMD,
+    // the one further into its tile issues first, so its stores leave (and its registers
+    // free up) while the other wave's loads are in flight (-3%, tools/tab_variants.py)
+    if (BCE_TAB_PRIO) __builtin_amdgcn_s_setprio(2);
     double2 ring[kTabRing];
     uint32_t rbits[kTabRing];
 #pragma unroll
@@ -431,6 +438,7 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
       }
     }
     if (!do_any) {
+      if (BCE_TAB_PRIO) __builtin_amdgcn_s_setprio(0);
       cur = nxt;
       continue;
     }
@@ -532,6 +540,7 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
         }
       }
     }
+    if (BCE_TAB_PRIO) __builtin_amdgcn_s_setprio(0);
     TAB_MARK(5);  // per-unique stores
     cur = nxt;
   }

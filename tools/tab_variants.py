@@ -40,6 +40,7 @@ VARIANTS = {
     "nt3_prof": ["-DBCE_TAB_NT=3", "-DBCE_TAB_PROF=1"],
     "base_prof": ["-DBCE_TAB_PROF=1"],
     "map0": ["-DBCE_TAB_MAP=0"],
+    "prio0": ["-DBCE_TAB_PRIO=0"],
     "ew1": ["-DBCE_EW_NT=1"],  # config-4 replay_step variants (bench.py --config c4)
     "ew2": ["-DBCE_EW_NT=2"],
     "ew3": ["-DBCE_EW_NT=3"],
