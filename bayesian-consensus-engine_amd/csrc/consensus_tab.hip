@@ -98,7 +98,7 @@ __device__ __forceinline__ void tab_st16(double* p, double x0, double x1) {
   }
 }
 #ifndef BCE_TAB_PRIO
-#define BCE_TAB_PRIO 1  // raised wave priority from the walk through the stores (0: off)
+#define BCE_TAB_PRIO 1  // wave priority ramp from the walk through the stores (0: off)
 #endif
 #ifndef BCE_TAB_MAP
 #define BCE_TAB_MAP 1  // 1: wave-major tile order (see the tile loop), 0: block-major
@@ -381,10 +381,11 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
     __builtin_amdgcn_sched_barrier(0);
 
     // ---- walk (core.py:107-144 in sorted-source order) ----------------------------------
-    // raised wave priority from the walk through the stores: of the two waves on a SIMD,
-    // the one further into its tile issues first, so its stores leave (and its registers
-    // free up) while the other wave's loads are in flight (-3%, tools/tab_variants.py)
-    if (BCE_TAB_PRIO) __builtin_amdgcn_s_setprio(2);
+    // wave priority ramps up through the tile (1 walk, 2 per-market outputs + compaction, 3
+    // per-unique stores, back to 0 for the next tile's loads): of the two waves sharing a
+    // SIMD, the one further into its tile issues first, so its stores leave while the other
+    // wave's loads are in flight (-4.2% against none, tools/tab_variants.py)
+    if (BCE_TAB_PRIO) __builtin_amdgcn_s_setprio(1);
     double2 ring[kTabRing];
     uint32_t rbits[kTabRing];
 #pragma unroll
@@ -421,6 +422,7 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
 
     TAB_MARK(2);  // walk
     // ---- per-market results (lane = market, coalesced) -----------------------------------
+    if (BCE_TAB_PRIO) __builtin_amdgcn_s_setprio(2);
     if (has) {
       const bool null_ = (total == 0.0);  // core.py:131-133
       if constexpr ((BCE_TAB_NT & 4) != 0) {
@@ -470,6 +472,7 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
 
     TAB_MARK(4);  // compaction
     // ---- per-unique outputs --------------------------------------------------------------
+    if (BCE_TAB_PRIO) __builtin_amdgcn_s_setprio(3);
     __builtin_amdgcn_sched_barrier(0);
     if (reg) {
       // re-derive the tile base and the lane offsets here: without the opaque copies the
