@@ -27,7 +27,7 @@ __global__ void fill(double* P, int64_t n) {
   }
 }
 
-template <int CPL, int ROWS, bool NT, bool SYNC = false, int MAP = 0>
+template <int CPL, int ROWS, bool NT, bool SYNC = false, int MAP = 0, bool BLK = false>
 __global__ __launch_bounds__(256) void votes_k(const double* __restrict__ P, int64_t A, int64_t M, int64_t ld,
                                                const double* __restrict__ w, double* __restrict__ cons,
                                                unsigned long long* __restrict__ vbits) {
@@ -42,7 +42,10 @@ __global__ __launch_bounds__(256) void votes_k(const double* __restrict__ P, int
   if (!SYNC && c0 >= M) return;
   const int64_t m = c0 + lane * CPL;
   const bool in = m + CPL - 1 < M;
-  const double* col = P + (in ? m : 0);
+  // BLK: column-blocked layout, block g of 64*CPL columns is one contiguous [A][64*CPL]
+  // slab, so a wave's rows are adjacent (8 KB per 16 rows) instead of ld*8 bytes apart
+  const double* col = BLK ? P + (in ? g * A * 64 * CPL + lane * CPL : 0) : P + (in ? m : 0);
+  const int64_t rs = BLK ? 64 * CPL : ld;
   unsigned long long* vb = vbits + g * CPL * A;
   double ws[CPL], total = 0.0;
 #pragma unroll
@@ -51,7 +54,7 @@ __global__ __launch_bounds__(256) void votes_k(const double* __restrict__ P, int
     double v[ROWS][CPL];
 #pragma unroll
     for (int q = 0; q < ROWS; ++q) {
-      const double* src = col + (a + q) * ld;
+      const double* src = col + (a + q) * rs;
       if constexpr (CPL == 2 || CPL == 4) {
 #pragma unroll
         for (int h = 0; h < CPL / 2; ++h) {
@@ -92,12 +95,12 @@ int main(int argc, char** argv) {
   const int64_t A = 16384, M = 1000000, ld = M;
   double *P, *w, *cons, *ref;
   unsigned long long* vb;
-  CK(hipMalloc(&P, A * M * 8));
+  CK(hipMalloc(&P, (A * M + A * 128) * 8));  // + one 128-column slab: the blocked layout's last partial block
   CK(hipMalloc(&w, A * 8));
   CK(hipMalloc(&cons, M * 8));
   CK(hipMalloc(&ref, M * 8));
   CK(hipMalloc(&vb, ((M + 127) / 128) * 2 * A * 8));
-  fill<<<4096, 256>>>(P, A * M);
+  fill<<<4096, 256>>>(P, A * M + A * 128);
   double* hw = (double*)malloc(A * 8);
   for (int64_t i = 0; i < A; ++i) hw[i] = (i % 7 == 0) ? 0.25 : 0.5;
   CK(hipMemcpy(w, hw, A * 8, hipMemcpyHostToDevice));
@@ -133,16 +136,17 @@ int main(int argc, char** argv) {
     fflush(stdout);
     (void)cpl;
   };
-#define V(C, R, N, S, MP)                                                                               \
-  run("cpl" #C "_rows" #R "_nt" #N "_sync" #S "_map" #MP, C, [&] {                                      \
+#define V(C, R, N, S, MP, B)                                                                            \
+  run("cpl" #C "_rows" #R "_nt" #N "_map" #MP "_blk" #B, C, [&] {                                      \
     const int64_t groups = (M + 64 * C - 1) / (64 * C);                                                 \
-    votes_k<C, R, N, S, MP><<<(unsigned)(((groups + 3) / 4 + 7) & ~7), 256>>>(P, A, M, ld, w, cons, vb); \
+    votes_k<C, R, N, S, MP, B><<<(unsigned)(((groups + 3) / 4 + 7) & ~7), 256>>>(P, A, M, ld, w, cons, vb); \
   })
   for (int round = 0; round < 2; ++round) {
-    V(1, 16, 0, 0, 0);
-    V(1, 16, 0, 0, 1);
-    V(1, 16, 0, 0, 2);
-    V(2, 16, 0, 0, 1);
+    V(1, 16, 0, 0, 0, false);
+    V(1, 16, 0, 0, 0, true);
+    V(1, 16, 1, 0, 0, true);
+    V(1, 32, 0, 0, 0, true);
+    V(2, 16, 0, 0, 0, true);
   }
   return 0;
 }
