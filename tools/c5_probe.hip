@@ -91,6 +91,37 @@ __global__ __launch_bounds__(256) void votes_k(const double* __restrict__ P, int
   }
 }
 
+// Row-band sweep: one launch per band of B agent rows, every wave of the chip in the same
+// band, each column's running sum carried in HBM between bands (ws[M] read + written per
+// band) -- the chip-wide access front stays B rows deep instead of drifting apart.
+template <int ROWS>
+__global__ __launch_bounds__(256) void band_k(const double* __restrict__ P, int64_t A, int64_t M, int64_t ld,
+                                              const double* __restrict__ w, double* __restrict__ wsb,
+                                              unsigned long long* __restrict__ vbits, int64_t a0, int64_t B) {
+  const int lane = threadIdx.x & 63;
+  const int64_t m = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t g = m >> 6;
+  if ((g << 6) >= M) return;
+  const bool in = m < M;
+  const double* col = P + (in ? m : 0);
+  unsigned long long* vb = vbits + g * A;
+  double ws = (a0 == 0 || !in) ? 0.0 : wsb[m];
+  for (int64_t a = a0; a < a0 + B; a += ROWS) {
+    double v[ROWS];
+#pragma unroll
+    for (int q = 0; q < ROWS; ++q) v[q] = in ? col[(a + q) * ld] : 0.0;
+    unsigned long long mine = 0;
+#pragma unroll
+    for (int q = 0; q < ROWS; ++q) {
+      ws += (0.0 + v[q]) * w[a + q];
+      const unsigned long long b = __ballot(in && v[q] >= 0.5);
+      mine = (lane == q) ? b : mine;
+    }
+    if (lane < ROWS) vb[a + lane] = mine;
+  }
+  if (in) wsb[m] = ws;
+}
+
 int main(int argc, char** argv) {
   const int64_t A = 16384, M = 1000000, ld = M;
   double *P, *w, *cons, *ref;
@@ -141,12 +172,29 @@ int main(int argc, char** argv) {
     const int64_t groups = (M + 64 * C - 1) / (64 * C);                                                 \
     votes_k<C, R, N, S, MP, B><<<(unsigned)(((groups + 3) / 4 + 7) & ~7), 256>>>(P, A, M, ld, w, cons, vb); \
   })
+  double* wsb;
+  CK(hipMalloc(&wsb, M * 8));
+  for (int64_t B : {64, 256, 1024}) {
+    for (int round = 0; round < 2; ++round) {
+      const int reps = 3;
+      float best = 1e30f;
+      for (int r = 0; r < reps; ++r) {
+        CK(hipEventRecord(e0));
+        for (int64_t a0 = 0; a0 < A; a0 += B)
+          band_k<16><<<(unsigned)((M + 255) / 256), 256>>>(P, A, M, ld, w, wsb, vb, a0, B);
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+        best = ms < best ? ms : best;
+      }
+      printf("{\"variant\": \"band%lld_rows16\", \"best_ms\": %.3f, \"TBps\": %.3f, \"frac\": %.3f}\n", (long long)B, best,
+             bytes / best / 1e9, bytes / best / 1e9 / 8.0);
+      fflush(stdout);
+    }
+  }
   for (int round = 0; round < 2; ++round) {
     V(1, 16, 0, 0, 0, false);
     V(1, 16, 0, 0, 0, true);
-    V(1, 16, 1, 0, 0, true);
-    V(1, 32, 0, 0, 0, true);
-    V(2, 16, 0, 0, 0, true);
   }
   return 0;
 }
