@@ -281,8 +281,11 @@ def test_aggregate_store_golden():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("G,maxlen", [(1, 0), (7, 1), (300, 40), (50, 3000), (3, 200_000)])
+@pytest.mark.parametrize("G,maxlen", [(1, 0), (7, 1), (300, 40), (50, 3000), (3, 200_000), (5000, 40), (3000, 2500),
+                                      (9000, 3)])
 def test_aggregate_kernel_vs_oracle(G, maxlen):
+    """Many more groups than workgroups (each workgroup pipelines its groups as one chunk
+    stream, across group boundaries), empty groups, multi-chunk groups."""
     import torch
 
     from bayesian_engine import batch
