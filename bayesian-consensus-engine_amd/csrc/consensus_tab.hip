@@ -37,12 +37,13 @@
 // Validation (core.py:59-60: first p < 0 or p > 1, NaN passes) reads the probabilities in
 // input order before the sort.  Exact mode only: every sum is the reference's own order.
 //
-// Measured (tools/tab_variants.py, profiles/r02_tab_*): 4 waves per CU (one per SIMD,
-// ~260 registers) beat 8 (2 per SIMD, 256-register budget: spills); the per-unique stores
-// are the largest phase -- the CU's share of the chip's write bandwidth -- and moving
-// them between the next tile's phases or to fully contiguous addresses did not help;
-// 128-B pieces beat 64-B ones by ~0.5%; loading the next tile's signals ahead (parked in
-// AGPRs, before or after this tile's stores) moved the wait elsewhere and ran 1-7% slower.
+// Measured (tools/tab_variants.py, measurements/tab_*_r02.txt): with nontemporal signal
+// loads and per-unique stores, 8 waves per CU (two per SIMD, 256 VGPRs, 6 spilled) beat 4;
+// wave-major tile order (consecutive tiles on consecutive workgroups / XCDs) -3.3%; a wave
+// priority ramp through the tile (1 walk, 2 per-market outputs, 3 per-unique stores) -4%.
+// The per-unique stores are the largest phase; 128-B pieces beat 64-B ones; loading the
+// next tile's signals ahead, unconditional chunk stores, a reciprocal-based normalizedWeight
+// and nontemporal per-market stores did not help.
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -54,7 +55,7 @@ namespace bce {
 namespace {
 
 #ifndef BCE_TAB_WAVES
-#define BCE_TAB_WAVES 8
+#define BCE_TAB_WAVES 8  // waves per workgroup (build knob; 8 = two per SIMD)
 #endif
 #ifndef BCE_TAB_PROF
 #define BCE_TAB_PROF 0  // experiment builds only (tools/tab_variants.py): per-phase s_memtime
@@ -109,7 +110,7 @@ constexpr int kLB = (kPL == 8) ? 3 : 2;    // log2 kPL
 constexpr int kMG = 64 / kPL;              // markets per load instruction
 static_assert(kPL == 4 || kPL == 8, "BCE_TAB_PIECE: 64 or 128");
 #ifndef BCE_TAB_RING
-#define BCE_TAB_RING 8
+#define BCE_TAB_RING 8  // LDS table reads in flight during the walk (4/6/8 measured equal)
 #endif
 constexpr int kTabRing = BCE_TAB_RING;  // LDS table reads issued ahead of the walk
 

@@ -110,7 +110,7 @@ __global__ __launch_bounds__(256) void outcome_update_kernel(int64_t n, double* 
 }
 
 #ifndef BCE_EW_NT
-#define BCE_EW_NT 2  // experiment switch: bit 0 nontemporal view stores, bit 1 rel/t loads, bit 2 conf load (with bit 1)
+#define BCE_EW_NT 2  // nontemporal hints (build knob): bit 0 view stores, bit 1 rel/t loads (on), bit 2 conf load (with bit 1)
 #endif
 typedef double ew_d2v __attribute__((ext_vector_type(2)));
 typedef long long ew_l2v __attribute__((ext_vector_type(2)));
