@@ -101,6 +101,9 @@ __device__ __forceinline__ void tab_st16(double* p, double x0, double x1) {
 #ifndef BCE_TAB_PRIO
 #define BCE_TAB_PRIO 1  // wave priority ramp from the walk through the stores (0: off)
 #endif
+#ifndef BCE_TAB_PLX
+#define BCE_TAB_PLX 0  // permlane-swap transposes (chunks on lane bits 5..3), needs BCE_TAB_PIECE 128
+#endif
 #ifndef BCE_TAB_MAP
 #define BCE_TAB_MAP 1  // 1: wave-major tile order (see the tile loop), 0: block-major
 #endif
@@ -109,6 +112,7 @@ constexpr int kPL = BCE_TAB_PIECE / 16;    // lanes per piece (16 B each): 4 or 
 constexpr int kLB = (kPL == 8) ? 3 : 2;    // log2 kPL
 constexpr int kMG = 64 / kPL;              // markets per load instruction
 static_assert(kPL == 4 || kPL == 8, "BCE_TAB_PIECE: 64 or 128");
+static_assert(!BCE_TAB_PLX || kPL == 8, "BCE_TAB_PLX needs 128-B pieces");
 #ifndef BCE_TAB_RING
 #define BCE_TAB_RING 8  // LDS table reads in flight during the walk (4/6/8 measured equal)
 #endif
@@ -131,9 +135,44 @@ __device__ __forceinline__ void bfly(uint32_t& a, uint32_t& b, int lane) {
   b = hi ? b : ax;
   a = na;
 }
-// Swap lane bits kLB-1..0 with dword-index bits kLB+1..2 of r[N] (an involution).
+// BCE_TAB_PLX: the piece's eight 16-B chunks sit on lane bits 5..3 instead of 2..0 (same
+// addresses per instruction, lanes permuted -- no memory cost, tools/tile_probe.hip), so
+// two of the three butterflies are single v_permlane32_swap / v_permlane16_swap
+// instructions per register pair and the third a row_ror:8 DPP pair; lane = market.
+__device__ __forceinline__ void bfly_pl32(uint32_t& a, uint32_t& b) {  // lane bit 5
+  const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+  a = r[0];
+  b = r[1];
+}
+__device__ __forceinline__ void bfly_pl16(uint32_t& a, uint32_t& b) {  // lane bit 4
+  const auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
+  a = r[0];
+  b = r[1];
+}
+__device__ __forceinline__ void bfly_r8(uint32_t& a, uint32_t& b, int lane) {  // lane bit 3: l ^ 8 = row_ror:8
+  const bool hi = (lane & 8) != 0;
+  const uint32_t bx = (uint32_t)__builtin_amdgcn_mov_dpp((int)b, 0x128, 0xF, 0xF, true);
+  const uint32_t ax = (uint32_t)__builtin_amdgcn_mov_dpp((int)a, 0x128, 0xF, 0xF, true);
+  const uint32_t na = hi ? bx : a;
+  b = hi ? b : ax;
+  a = na;
+}
+// Swap lane bits kLB-1..0 (BCE_TAB_PLX: 5..3) with dword-index bits kLB+1..2 of r[N] (an
+// involution).
 template <int N>
 __device__ __forceinline__ void xpose(uint32_t (&r)[N], int lane) {
+  if constexpr (BCE_TAB_PLX) {
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      if (!(i & 16)) bfly_pl32(r[i], r[i | 16]);
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      if (!(i & 8)) bfly_pl16(r[i], r[i | 8]);
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      if (!(i & 4)) bfly_r8(r[i], r[i | 4], lane);
+    return;
+  }
   if constexpr (kLB == 3) {
 #pragma unroll
     for (int i = 0; i < N; ++i)
@@ -156,7 +195,12 @@ __device__ __forceinline__ void xpose(uint32_t (&r)[N], int lane) {
 // Swapping the log2 PL lane bits of c with the low load-index bits leaves one market per
 // lane -- lane L holds market tmkt(L) = MG (L & (PL-1)) + (L >> log2 PL) -- and the
 // register index = the position, for both arrays.
-__device__ __forceinline__ int tmkt(int lane) { return ((lane & (kPL - 1)) * kMG) | (lane >> kLB); }
+__device__ __forceinline__ int tmkt(int lane) {
+  return BCE_TAB_PLX ? lane : ((lane & (kPL - 1)) * kMG) | (lane >> kLB);
+}
+// this lane's market-within-group q and chunk c in the regular-tile address maps
+__device__ __forceinline__ int lq(int lane) { return BCE_TAB_PLX ? (lane & 7) : (lane >> kLB); }
+__device__ __forceinline__ int lc(int lane) { return BCE_TAB_PLX ? (lane >> 3) : (lane & (kPL - 1)); }
 // Odd-even merge network over 31-bit keys with a 64-bit payload, branch- and SGPR-free:
 // the swap mask is the sign of y - x (keys < 2^31), the payload moves with v_bfi_b32.
 // (Compare-and-select would give every comparator of a stage its own SGPR-pair condition;
@@ -246,7 +290,7 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
   };
   // Regular-tile loads (the address maps above); raw, not yet transposed.
   auto load_regular = [&](int64_t B, int lane, uint32_t (&rs)[32], uint32_t (&rp)[64]) {
-    const int q = lane >> kLB, c = lane & (kPL - 1);
+    const int q = lq(lane), c = lc(lane);
     const uint32_t* sb = reinterpret_cast<const uint32_t*>(a.sid + B);
     const double* pb = a.prob + B;
 #pragma unroll
@@ -483,12 +527,12 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
       const int64_t B = (int64_t)(((uint64_t)bhi << 32) | blo);
       int lane = lane_id();
       asm volatile("" : "+v"(lane));
-      const int q = lane >> kLB, c = lane & (kPL - 1);
+      const int q = lq(lane), c = lc(lane);
       int uk[kPL];
       double tk[kPL];
 #pragma unroll
       for (int k = 0; k < kPL; ++k) {  // market MG·k + q of load index k sits in lane PL·q + k
-        const int src = ((lane & ~(kPL - 1)) | k) << 2;
+        const int src = (BCE_TAB_PLX ? ((k << 3) | (lane & 7)) : ((lane & ~(kPL - 1)) | k)) << 2;
         uk[k] = __builtin_amdgcn_ds_bpermute(src, u);
         tk[k] = dbl((uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)lo32(total)),
                     (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)hi32(total)));

@@ -38,21 +38,25 @@ __device__ __forceinline__ void st16(uint32_t* p, uint4 v) {
   else *reinterpret_cast<uint4*>(p) = v;
 }
 template <int SHAPE, bool NT = false>
-__device__ __forceinline__ void tile_load(const Args& a, int64_t B, int lane, uint4 (&s)[8], uint4 (&p)[16]) {
+__device__ __forceinline__ void tile_load(const Args& a, int64_t B, int lane_in, uint4 (&s)[8], uint4 (&p)[16]) {
+  // SHAPE 4 = SHAPE 3's addresses, lanes permuted (bits 0-2 <-> 3-5): a 128-B piece is
+  // read by lanes m, m+8, ..., m+56 instead of 8 consecutive lanes
+  const int lane = (SHAPE == 4) ? (((lane_in & 7) << 3) | (lane_in >> 3)) : lane_in;
+  constexpr int SH = (SHAPE == 4) ? 3 : SHAPE;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     int64_t e;  // element (u32) offset of this lane's 16-B chunk
-    if (SHAPE == 0) e = 32 * (16 * (k & 3) + (lane >> 2)) + 16 * (k >> 2) + 4 * (lane & 3);
-    else if (SHAPE == 1 || SHAPE == 3) e = 32 * (8 * k + (lane >> 3)) + 4 * (lane & 7);
+    if (SH == 0) e = 32 * (16 * (k & 3) + (lane >> 2)) + 16 * (k >> 2) + 4 * (lane & 3);
+    else if (SH == 1 || SH == 3) e = 32 * (8 * k + (lane >> 3)) + 4 * (lane & 7);
     else e = 256 * k + 4 * lane;
     s[k] = ld16<NT>(a.sid + B + e);
   }
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     int64_t e;  // element (u32 of the prob array viewed as u32) offset
-    if (SHAPE == 0) e = 64 * (16 * (k & 3) + (lane >> 2)) + 16 * (k >> 2) + 4 * (lane & 3);
-    else if (SHAPE == 1) e = 64 * (4 * k + (lane >> 4)) + 4 * (lane & 15);
-    else if (SHAPE == 3) e = 64 * (8 * (k & 7) + (lane >> 3)) + 32 * (k >> 3) + 4 * (lane & 7);
+    if (SH == 0) e = 64 * (16 * (k & 3) + (lane >> 2)) + 16 * (k >> 2) + 4 * (lane & 3);
+    else if (SH == 1) e = 64 * (4 * k + (lane >> 4)) + 4 * (lane & 15);
+    else if (SH == 3) e = 64 * (8 * (k & 7) + (lane >> 3)) + 32 * (k >> 3) + 4 * (lane & 7);
     else e = 256 * k + 4 * lane;
     p[k] = ld16<NT>(reinterpret_cast<const uint32_t*>(a.prob + B) + e);
   }
@@ -105,21 +109,24 @@ __global__ __launch_bounds__(64 * W) void tile_mix(Args a) {
     a.nu[mk] = 32;
     a.err[mk] = -1;
     // per-unique outputs: usid 8 KiB, weight 16 KiB, nweight 16 KiB per tile
+    const int lane_o = lane;
+    const int lane_s = (SHAPE == 4) ? (((lane_o & 7) << 3) | (lane_o >> 3)) : lane_o;
+    constexpr int SS = (SHAPE == 4) ? 3 : SHAPE;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       int64_t e;
-      if (SHAPE == 0) e = 32 * (16 * (k & 3) + (lane >> 2)) + 16 * (k >> 2) + 4 * (lane & 3);
-      else if (SHAPE == 1 || SHAPE == 3) e = 32 * (8 * k + (lane >> 3)) + 4 * (lane & 7);
-      else e = 256 * k + 4 * lane;
+      if (SS == 0) e = 32 * (16 * (k & 3) + (lane_s >> 2)) + 16 * (k >> 2) + 4 * (lane_s & 3);
+      else if (SS == 1 || SS == 3) e = 32 * (8 * k + (lane_s >> 3)) + 4 * (lane_s & 7);
+      else e = 256 * k + 4 * lane_s;
       st16<NT>(a.usid + B + e, s[k]);
     }
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       int64_t e;
-      if (SHAPE == 0) e = 64 * (16 * (k & 3) + (lane >> 2)) + 16 * (k >> 2) + 4 * (lane & 3);
-      else if (SHAPE == 1) e = 64 * (4 * k + (lane >> 4)) + 4 * (lane & 15);
-      else if (SHAPE == 3) e = 64 * (8 * (k & 7) + (lane >> 3)) + 32 * (k >> 3) + 4 * (lane & 7);
-      else e = 256 * k + 4 * lane;
+      if (SS == 0) e = 64 * (16 * (k & 3) + (lane_s >> 2)) + 16 * (k >> 2) + 4 * (lane_s & 3);
+      else if (SS == 1) e = 64 * (4 * k + (lane_s >> 4)) + 4 * (lane_s & 15);
+      else if (SS == 3) e = 64 * (8 * (k & 7) + (lane_s >> 3)) + 32 * (k >> 3) + 4 * (lane_s & 7);
+      else e = 256 * k + 4 * lane_s;
       st16<NT>(reinterpret_cast<uint32_t*>(a.w + B) + e, p[k]);
       st16<NT>(reinterpret_cast<uint32_t*>(a.nw + B) + e, p[k]);
     }
@@ -155,16 +162,10 @@ int main() {
     printf("{\"probe\": \"%s\", \"ms\": %.5f, \"GBps\": %.1f}\n", name, ms, bytes / ms / 1e6);
     fflush(stdout);
   };
-  // round 2b: tile -> wave mappings at the kernel's shape (half128, nt, 8 waves, 1 wg/cu)
+  // lane-permuted pieces (for VALU-only permlane transposes) vs the kernel's shape
   for (int r = 0; r < 3; ++r) {
-    timeit("half128 w8 1wg/cu nt map0", [&] { tile_mix<8, 3, false, true, 0><<<cus, 512>>>(a); });
     timeit("half128 w8 1wg/cu nt map1", [&] { tile_mix<8, 3, false, true, 1><<<cus, 512>>>(a); });
-    timeit("half128 w8 1wg/cu nt map1 chunk2", [&] { tile_mix<8, 3, false, true, 3><<<cus, 512>>>(a); });
-    timeit("half128 w8 1wg/cu nt map1 chunk4", [&] { tile_mix<8, 3, false, true, 5><<<cus, 512>>>(a); });
-    timeit("half128 w8 1wg/cu nt map1 chunk8", [&] { tile_mix<8, 3, false, true, 9><<<cus, 512>>>(a); });
-    timeit("half128 w4 1wg/cu nt map1", [&] { tile_mix<4, 3, false, true, 1><<<cus, 256>>>(a); });
-    timeit("half128 w16 1wg/cu nt map1", [&] { tile_mix<16, 3, false, true, 1><<<cus, 1024>>>(a); });
-    timeit("linear w8 1wg/cu nt map1", [&] { tile_mix<8, 2, false, true, 1><<<cus, 512>>>(a); });
+    timeit("half128-lanes-permuted w8 1wg/cu nt map1", [&] { tile_mix<8, 4, false, true, 1><<<cus, 512>>>(a); });
   }
   return 0;
 }
