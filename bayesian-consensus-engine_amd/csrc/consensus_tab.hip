@@ -102,7 +102,7 @@ __device__ __forceinline__ void tab_st16(double* p, double x0, double x1) {
 #define BCE_TAB_PRIO 1  // wave priority ramp from the walk through the stores (0: off)
 #endif
 #ifndef BCE_TAB_PLX
-#define BCE_TAB_PLX 0  // permlane-swap transposes (chunks on lane bits 5..3), needs BCE_TAB_PIECE 128
+#define BCE_TAB_PLX 1  // permlane-swap transposes (chunks on lane bits 5..3; -2..3%), needs BCE_TAB_PIECE 128
 #endif
 #ifndef BCE_TAB_MAP
 #define BCE_TAB_MAP 1  // 1: wave-major tile order (see the tile loop), 0: block-major
