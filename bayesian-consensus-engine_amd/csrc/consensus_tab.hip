@@ -162,6 +162,9 @@ __device__ __forceinline__ void bfly_r8(uint32_t& a, uint32_t& b, int lane) {  /
 template <int N>
 __device__ __forceinline__ void xpose(uint32_t (&r)[N], int lane) {
   if constexpr (BCE_TAB_PLX) {
+    // (the three butterflies commute; this order keeps the kernel at 6 spilled VGPRs,
+    // permlane32 first spilled 21)
+#ifdef BCE_TAB_XORD_OLD
 #pragma unroll
     for (int i = 0; i < N; ++i)
       if (!(i & 16)) bfly_pl32(r[i], r[i | 16]);
@@ -171,6 +174,17 @@ __device__ __forceinline__ void xpose(uint32_t (&r)[N], int lane) {
 #pragma unroll
     for (int i = 0; i < N; ++i)
       if (!(i & 4)) bfly_r8(r[i], r[i | 4], lane);
+#else
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      if (!(i & 4)) bfly_r8(r[i], r[i | 4], lane);
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      if (!(i & 8)) bfly_pl16(r[i], r[i | 8]);
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      if (!(i & 16)) bfly_pl32(r[i], r[i | 16]);
+#endif
     return;
   }
   if constexpr (kLB == 3) {

@@ -42,6 +42,7 @@ VARIANTS = {
     "map0": ["-DBCE_TAB_MAP=0"],
     "prio0": ["-DBCE_TAB_PRIO=0"],
     "plx": ["-DBCE_TAB_PLX=1"],
+    "xord_old": ["-DBCE_TAB_XORD_OLD=1"],
     "ewg16": ["-DBCE_EW_GRID_CAP=16"],
     "agg8": ["-DBCE_AGG_CAP=8"],  # f4: 8 workgroups per CU looping over groups (bench --config agg)  # elementwise kernels: 16 workgroups per CU (bench --config c4 / ns)
     "ew1": ["-DBCE_EW_NT=1"],  # config-4 replay_step variants (bench.py --config c4)
