@@ -163,7 +163,8 @@ def compute_consensus(
     T = lambda a: torch.from_numpy(a).to(dev, non_blocking=False)  # noqa: E731
     table = batch.SourceTable.from_arrays(T(rel), T(conf), T(present[:S]), source_ids)
     off = torch.tensor([0, n], dtype=torch.int64, device=dev)
-    res = batch.consensus(off, T(sid), T(prob), table, max_len=n if n <= 64 else None, validate=False)
+    res = batch.consensus(off, T(sid), T(prob), table, max_len=n if n <= 64 else None, validate=False,
+                          check=True)
     cons = float(res.consensus[0].item())
     total = float(res.total_weight[0].item())
     confidence = float(res.confidence[0].item())

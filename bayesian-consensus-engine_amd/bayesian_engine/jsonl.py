@@ -131,7 +131,8 @@ def consensus_many(signal_lists: Sequence[list], source_reliability: Optional[di
     max_len = int(lens.max())
     plan = None if max_len <= 64 else batch.Plan.build(off, dev)
     res = batch.consensus(T(off), T(sid), T(prob), table, plan=plan,
-                          max_len=max_len if plan is None else None, mode=mode, validate=False)
+                          max_len=max_len if plan is None else None, mode=mode, validate=False,
+                          check=True)
     # one device->host copy per array, then plain lists (numpy scalar/slice access per
     # market cost more than the whole launch)
     cons = res.consensus.cpu().tolist()

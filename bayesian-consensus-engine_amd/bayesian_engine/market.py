@@ -220,7 +220,7 @@ def _batched_consensus(markets: List[Market], store: Optional[SQLiteReliabilityS
     off = np.array(offsets, np.int64)
     T = lambda a: torch.from_numpy(a).to(dev)  # noqa: E731
     res = batch.consensus(T(off), T(np.array(sid_list, np.int32)), T(np.array(prob_list, np.float64)), table,
-                          validate=False)
+                          validate=False, check=True)
     cons = res.consensus.cpu().numpy()
     confd = res.confidence.cpu().numpy()
     tot = res.total_weight.cpu().numpy()

@@ -68,6 +68,27 @@ def combine_flags(local_flags: torch.Tensor) -> torch.Tensor:
     return (part | (corr.to(torch.int32) << 1)).to(torch.uint8)
 
 
+def pack_owner_flags(part: torch.Tensor, corr: torch.Tensor, mine: torch.Tensor, pos: torch.Tensor,
+                     world: int, blk: int) -> torch.Tensor:
+    """This market shard's 2-bit outcome flags over ALL sources, laid out by owner block
+    (``pos[s]`` = owner(s) * blk + index inside the owner's block) and packed 4 sources per
+    byte (source j of a byte in bits 2j, 2j+1): the send buffer of the per-step
+    reduce-scatter that hands each owner its block (e2).
+
+    ``mine`` masks the sources whose outcome this shard resolved; the correct bit is set only
+    with the participate bit.  Both bits are masked,
+    so a rank contributes an all-zero 2-bit field for every source it did not resolve; with
+    each (source, step) outcome resolved by exactly one shard the uint8 SUM of the ranks'
+    buffers then never carries between fields and equals their OR.
+    """
+    p = (part & mine).to(torch.uint8)
+    c = (part & corr & mine).to(torch.uint8)
+    f = torch.zeros(world * blk, dtype=torch.uint8, device=part.device)
+    f[pos] = p | (c << 1)
+    f = f.view(-1, 4)
+    return (f[:, 0] | (f[:, 1] << 2) | (f[:, 2] << 4) | (f[:, 3] << 6)).contiguous()
+
+
 def allreduce_counts(correct: torch.Tensor, total: torch.Tensor) -> None:
     """Sum per-source agreement counts over market shards (summarize_sources, market.py:293-304)."""
     if dist.is_initialized() and dist.get_world_size() > 1:

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+
 #include "../../include/bce.h"
 
 namespace bce {
@@ -14,8 +16,22 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 // Check the launch that was just enqueued.
 int check_launch(const char* what);
 
-// Device properties cached per process (CU count for grid sizing).
+// Device properties cached per device (CU count for grid sizing).  Thread-safe.
 int cu_count();
+
+// Resident workgroups per CU of `fn` at `threads` threads and `lds` dynamic LDS bytes,
+// cached per (device, kernel, shape); `fallback` when the query fails.  Thread-safe.
+int blocks_per_cu(const void* fn, int threads, size_t lds, int fallback, const char* name = nullptr);
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (device, kernel).  Thread-safe.
+int ensure_dynamic_lds(const void* fn, int bytes);
+
+// The planned launch's side stream (one per device): side_fork records a fork event on
+// `st`, makes the side stream wait on it and takes the device's fork lock, which the
+// caller holds until side_join has made `st` wait on the side stream's work -- so two host
+// threads planning on different streams never wait on each other's fork/join events.
+int side_fork(hipStream_t st, hipStream_t* side, std::unique_lock<std::mutex>* lock);
+int side_join(hipStream_t st);
 
 }  // namespace bce
 

@@ -1,6 +1,12 @@
 // capi.hip -- library-level C ABI: version, errors, device queries.
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
+
+#include <map>
+#include <mutex>
+#include <set>
+#include <tuple>
 
 #include "bce_internal.hpp"
 #include "consensus_common.hpp"
@@ -25,30 +31,110 @@ int check_launch(const char* what) {
   return BCE_OK;
 }
 
-int cu_count() {
-  static int cached = 0;
-  if (!cached) {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
-      cached = n;
-    else
-      cached = 256;
+// ---- per-device context -------------------------------------------------------------
+// Everything the launchers cache is keyed by the calling thread's current device and
+// initialised under a once-flag / mutex: one process may drive several GPUs from several
+// host threads (ctypes releases the GIL), and lazily created device objects must not race.
+namespace {
+constexpr int kMaxDev = 64;
+
+struct DevCtx {
+  std::once_flag once;
+  int cus = 256;
+  int* fault = nullptr;
+  hipError_t init_err = hipSuccess;
+  std::mutex side_mu;  // held from the plan's fork to its join (bce_consensus_planned)
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+};
+DevCtx g_dev[kMaxDev];
+
+DevCtx* dev_ctx() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return nullptr;
+  DevCtx* c = &g_dev[dev];
+  std::call_once(c->once, [c, dev] {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0) c->cus = n;
+    int* p = nullptr;
+    hipError_t e = hipMalloc((void**)&p, sizeof(int));
+    if (e == hipSuccess) e = hipMemset(p, 0, sizeof(int));  // synchronous: done before first use
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
+    c->init_err = e;
+    if (e == hipSuccess) c->fault = p;
+  });
+  return c;
+}
+
+struct OccKey {
+  int dev;
+  const void* fn;
+  int threads;
+  size_t lds;
+  bool operator<(const OccKey& o) const {
+    return std::tie(dev, fn, threads, lds) < std::tie(o.dev, o.fn, o.threads, o.lds);
   }
-  return cached;
+};
+std::mutex g_occ_mu;
+std::map<OccKey, int> g_occ;
+std::set<std::pair<int, const void*>> g_attr;
+}  // namespace
+
+int cu_count() {
+  DevCtx* c = dev_ctx();
+  return c ? c->cus : 256;
 }
 
 int* fault_word() {
-  static int* words[64] = {nullptr};
+  DevCtx* c = dev_ctx();
+  return c ? c->fault : nullptr;
+}
+
+int blocks_per_cu(const void* fn, int threads, size_t lds, int fallback, const char* name) {
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  if (!words[dev]) {
-    int* p = nullptr;
-    if (hipMalloc((void**)&p, sizeof(int)) != hipSuccess) return nullptr;
-    if (hipMemset(p, 0, sizeof(int)) != hipSuccess) return nullptr;
-    words[dev] = p;
+  if (hipGetDevice(&dev) != hipSuccess) return fallback;
+  std::lock_guard<std::mutex> lk(g_occ_mu);
+  const OccKey k{dev, fn, threads, lds};
+  auto it = g_occ.find(k);
+  if (it != g_occ.end()) return it->second;
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, threads, lds) != hipSuccess || nb <= 0) nb = fallback;
+  g_occ[k] = nb;
+  if (name && getenv("BCE_DEBUG_LAUNCH"))
+    fprintf(stderr, "[bce] %s: %d blocks/CU x %d CUs (dev %d, %zu B dynamic LDS)\n", name, nb, cu_count(), dev, lds);
+  return nb;
+}
+
+int ensure_dynamic_lds(const void* fn, int bytes) {
+  int dev = 0;
+  BCE_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(g_occ_mu);
+  if (g_attr.count({dev, fn})) return BCE_OK;
+  BCE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  g_attr.insert({dev, fn});
+  return BCE_OK;
+}
+
+int side_fork(hipStream_t st, hipStream_t* side, std::unique_lock<std::mutex>* lock) {
+  DevCtx* c = dev_ctx();
+  if (!c || !c->side) {
+    set_error("side stream unavailable: %s", c ? hipGetErrorString(c->init_err) : "no device");
+    return BCE_EHIP;
   }
-  return words[dev];
+  *lock = std::unique_lock<std::mutex>(c->side_mu);
+  BCE_HIP(hipEventRecord(c->ev_fork, st));
+  BCE_HIP(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+  *side = c->side;
+  return BCE_OK;
+}
+
+int side_join(hipStream_t st) {
+  DevCtx* c = dev_ctx();
+  BCE_HIP(hipEventRecord(c->ev_join, c->side));
+  BCE_HIP(hipStreamWaitEvent(st, c->ev_join, 0));
+  return BCE_OK;
 }
 
 static int g_spin_cap = 1 << 22;

@@ -1483,14 +1483,7 @@ int launch_seg(const ConsArgs& a, hipStream_t st) {
   const int64_t tiles = (a.n_list + TM - 1) / TM;
   if (tiles == 0) return BCE_OK;
   // persistent grid: every workgroup resident at once, tiles dealt round-robin
-  static int per_cu = 0;
-  if (!per_cu) {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, consensus_seg_kernel<G, TM>, 64, 0) !=
-                 hipSuccess || nb <= 0)
-      nb = 8;
-    per_cu = nb;
-  }
+  const int per_cu = blocks_per_cu(reinterpret_cast<const void*>(&consensus_seg_kernel<G, TM>), 64, 0, 8);
   const int64_t cap = (int64_t)cu_count() * per_cu;
   const int grid = (int)(tiles < cap ? tiles : cap);
   hipLaunchKernelGGL((consensus_seg_kernel<G, TM>), dim3(grid), dim3(64), 0, st, a);
@@ -1501,14 +1494,7 @@ template <int G>
 int launch_lpm(const ConsArgs& a, hipStream_t st) {
   const int64_t tiles = (a.n_list + kWave - 1) / kWave;
   if (tiles == 0) return BCE_OK;
-  static int per_cu = 0;
-  if (!per_cu) {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, consensus_lpm_kernel<G>, 64, 0) !=
-                 hipSuccess || nb <= 0)
-      nb = 4;
-    per_cu = nb;
-  }
+  const int per_cu = blocks_per_cu(reinterpret_cast<const void*>(&consensus_lpm_kernel<G>), 64, 0, 4);
   const int64_t cap = (int64_t)cu_count() * per_cu;
   const int grid = (int)(tiles < cap ? tiles : cap);
   hipLaunchKernelGGL((consensus_lpm_kernel<G>), dim3(grid), dim3(64), 0, st, a);
@@ -1520,17 +1506,8 @@ int launch_pipe(const ConsArgs& a, hipStream_t st) {
   constexpr int TM = 64;
   const int64_t tiles = (a.n_list + TM - 1) / TM;
   if (tiles == 0) return BCE_OK;
-  static int per_cu = 0;
-  if (!per_cu) {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, consensus_pipe_kernel<G>,
-                                                     64 * (PipeCfg<G>::C + PipeCfg<G>::L), 0) !=
-            hipSuccess || nb <= 0)
-      nb = 1;
-    per_cu = nb;
-    if (getenv("BCE_DEBUG_LAUNCH"))
-      fprintf(stderr, "[bce] consensus_pipe_kernel<%d>: %d blocks/CU x %d CUs\n", G, nb, cu_count());
-  }
+  const int per_cu = blocks_per_cu(reinterpret_cast<const void*>(&consensus_pipe_kernel<G>),
+                                   64 * (PipeCfg<G>::C + PipeCfg<G>::L), 0, 1, "consensus_pipe_kernel");
   const int64_t cap = (int64_t)cu_count() * per_cu;
   const int grid = (int)(tiles < cap ? tiles : cap);
   hipLaunchKernelGGL((consensus_pipe_kernel<G>), dim3(grid), dim3(64 * (PipeCfg<G>::C + PipeCfg<G>::L)), 0, st,
@@ -1543,16 +1520,8 @@ int launch_flat(const ConsArgs& a, hipStream_t st) {
   constexpr int TM = BCE_FLAT_TM, WPB = BCE_FLAT_WPB;
   const int64_t tiles = (a.n_list + TM - 1) / TM;
   if (tiles == 0) return BCE_OK;
-  static int per_cu = 0;
-  if (!per_cu) {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, consensus_flat_kernel<G, TM, WPB>, 64 * WPB, 0) !=
-                 hipSuccess || nb <= 0)
-      nb = 2;
-    per_cu = nb;
-    if (getenv("BCE_DEBUG_LAUNCH"))
-      fprintf(stderr, "[bce] consensus_flat_kernel<%d,%d,%d>: %d blocks/CU x %d CUs\n", G, TM, WPB, nb, cu_count());
-  }
+  const int per_cu = blocks_per_cu(reinterpret_cast<const void*>(&consensus_flat_kernel<G, TM, WPB>), 64 * WPB, 0, 2,
+                                   "consensus_flat_kernel");
   const int64_t blocks = (tiles + WPB - 1) / WPB;
   const int64_t cap = (int64_t)cu_count() * per_cu;
   const int grid = (int)(blocks < cap ? blocks : cap);
@@ -1784,20 +1753,12 @@ extern "C" int bce_consensus_planned(const int64_t* offsets, int64_t n_markets, 
   // over 2-8 streams, was slower (profiles/r02_c3_plan_streams.jsonl).  BCE_PLAN_SIDE = the
   // last bin index on the side stream (default 3; -1 = everything on st).
   hipStream_t side = st;
-  static hipStream_t side_s[64] = {nullptr};
-  static hipEvent_t ev_fork[64], ev_join[64];
-  int dev = 0;
+  std::unique_lock<std::mutex> fork_lock;
   const int side_last = getenv("BCE_PLAN_SIDE") ? atoi(getenv("BCE_PLAN_SIDE")) : 3;  // last side bin
-  const bool fork = side_last >= 0 && hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64;
+  const bool fork = side_last >= 0;
   if (fork) {
-    if (!side_s[dev]) {
-      BCE_HIP(hipStreamCreateWithFlags(&side_s[dev], hipStreamNonBlocking));
-      BCE_HIP(hipEventCreateWithFlags(&ev_fork[dev], hipEventDisableTiming));
-      BCE_HIP(hipEventCreateWithFlags(&ev_join[dev], hipEventDisableTiming));
-    }
-    side = side_s[dev];
-    BCE_HIP(hipEventRecord(ev_fork[dev], st));
-    BCE_HIP(hipStreamWaitEvent(side, ev_fork[dev], 0));
+    rc = side_fork(st, &side, &fork_lock);
+    if (rc) return rc;
   }
   for (int b = BCE_NBINS - 1; b >= 0; --b) {
     ConsArgs a = base;
@@ -1814,7 +1775,11 @@ extern "C" int bce_consensus_planned(const int64_t* offsets, int64_t n_markets, 
       // scratch stride from the caller's sizing (bce_consensus_scratch_bytes)
       const int grid = (int)(a.n_list < kHugeGrid ? a.n_list : kHugeGrid);
       const int64_t P = scratch_bytes / ((int64_t)grid * 4 * 8);
-      BCE_REQUIRE(P > kLongMaxLds, "planned: scratch too small for the >4096 bin");
+      if (P <= kLongMaxLds) {  // not BCE_REQUIRE: the side stream must still be joined
+        set_error("planned: scratch too small for the >4096 bin");
+        rc = BCE_EINVAL;
+        break;
+      }
       a.scratch = scratch;
       a.scratch_stride = P;
       hipLaunchKernelGGL((consensus_long_kernel<false>), dim3(grid), dim3(kLongThreads), 0, st, a);
@@ -1823,8 +1788,8 @@ extern "C" int bce_consensus_planned(const int64_t* offsets, int64_t n_markets, 
     if (rc) break;
   }
   if (fork) {
-    BCE_HIP(hipEventRecord(ev_join[dev], side));
-    BCE_HIP(hipStreamWaitEvent(st, ev_join[dev], 0));
+    const int rj = side_join(st);  // join even after a failed launch: st must not run ahead
+    if (!rc) rc = rj;
   }
   return rc;
 }

@@ -628,24 +628,11 @@ int launch_tab32(const ConsArgs& a, hipStream_t st) {
   if (tiles == 0) return BCE_OK;
   const int S = a.n_sources > 0 ? a.n_sources : 1;
   const size_t lds = 16 * (size_t)S + 4 * (size_t)((S + 31) / 32);
-  static bool attr_set = false;
-  if (!attr_set) {
-    const size_t cap = 16 * (size_t)kTabMaxSources + 4 * (size_t)(kTabMaxSources / 32);
-    BCE_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&consensus_tab32_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)cap));
-    attr_set = true;
-  }
-  static int cached_S = -1, per_cu = 1;
-  if (cached_S != S) {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, consensus_tab32_kernel, 64 * kTabWaves, lds) !=
-            hipSuccess || nb <= 0)
-      nb = 1;
-    per_cu = nb;
-    cached_S = S;
-    if (getenv("BCE_DEBUG_LAUNCH"))
-      fprintf(stderr, "[bce] consensus_tab32_kernel: %d blocks/CU x %d CUs, %zu B LDS\n", nb, cu_count(), lds);
-  }
+  const size_t cap_lds = 16 * (size_t)kTabMaxSources + 4 * (size_t)(kTabMaxSources / 32);
+  const int rc = ensure_dynamic_lds(reinterpret_cast<const void*>(&consensus_tab32_kernel), (int)cap_lds);
+  if (rc) return rc;
+  const int per_cu = blocks_per_cu(reinterpret_cast<const void*>(&consensus_tab32_kernel), 64 * kTabWaves, lds, 1,
+                                   "consensus_tab32_kernel");
   const int64_t blocks = (tiles + kTabWaves - 1) / kTabWaves;
   const int64_t cap = (int64_t)cu_count() * per_cu;
   const int grid = (int)(blocks < cap ? blocks : cap);

@@ -762,18 +762,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
 template <int NW, int R, bool FAST>
 int launch_wide(const ConsArgs& a, hipStream_t st) {
   if (a.n_list == 0) return BCE_OK;
-  static int per_cu = 0;
-  if (!per_cu) {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, consensus_wide_kernel<NW, R, FAST>, 64 * NW, 0) !=
-            hipSuccess ||
-        nb <= 0)
-      nb = 1;
-    per_cu = nb;
-    if (getenv("BCE_DEBUG_LAUNCH"))
-      fprintf(stderr, "[bce] consensus_wide_kernel<%d,%d,%s>: %d blocks/CU x %d CUs\n", NW, R,
-              FAST ? "fast" : "exact", nb, cu_count());
-  }
+  const int per_cu = blocks_per_cu(reinterpret_cast<const void*>(&consensus_wide_kernel<NW, R, FAST>), 64 * NW, 0,
+                                   1, "consensus_wide_kernel");
   const int64_t cap = (int64_t)cu_count() * per_cu;
   const int grid = (int)(a.n_list < cap ? a.n_list : cap);
   hipLaunchKernelGGL((consensus_wide_kernel<NW, R, FAST>), dim3(grid), dim3(64 * NW), 0, st, a);

@@ -442,8 +442,13 @@ extern "C" int bce_tiebreak_csr_long(const int64_t* offsets, int64_t n_markets, 
   // any longer market: sort in a global scratch slice per workgroup (16 B per entry)
   int64_t P = 1;
   while (P < max_len) P <<= 1;
+  // each workgroup walks the list with a stride of the grid, so its slice must hold the
+  // longest market; the grid shrinks instead of the scratch growing past 1 GiB (one
+  // 10M-agent market beside other long ones would otherwise ask for CUs x 256 MB)
   int64_t blocks = n_list;
-  const int64_t cap = (int64_t)cu_count();
+  int64_t cap = (int64_t)cu_count();
+  const int64_t by_budget = ((int64_t)1 << 30) / (16 * P);
+  if (cap > by_budget) cap = by_budget > 0 ? by_budget : 1;
   if (blocks > cap) blocks = cap;
   void* scratch = nullptr;
   BCE_HIP(hipMallocAsync(&scratch, (size_t)(blocks * 16 * P), st));

@@ -304,7 +304,7 @@ def _c3(args, world, rank, barrier, max_over, sum_over):
 # ---------------------------------------------------------------------------------------
 def _c4(args, world, rank, barrier, max_over, sum_over):
     from bayesian_engine import batch
-    from bayesian_engine.sharding import owner_of
+    from bayesian_engine.sharding import owner_of, pack_owner_flags
 
     S_total = 10_000_000
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -338,11 +338,9 @@ def _c4(args, world, rank, barrier, max_over, sum_over):
         gg.manual_seed(k_seed)
         part = torch.rand(S_total, generator=gg, device=dev) < 0.1
         corr = torch.rand(S_total, generator=gg, device=dev) < 0.6
-        part &= contrib == rank  # this rank's market shard resolved these (disjoint across ranks)
-        f = torch.zeros(world * blk, dtype=torch.uint8, device=dev)
-        f[pos] = part.to(torch.uint8) | (corr.to(torch.uint8) << 1)
-        f = f.view(-1, 4)
-        return (f[:, 0] | (f[:, 1] << 2) | (f[:, 2] << 4) | (f[:, 3] << 6)).contiguous()
+        # this rank's market shard resolved the sources with contrib == rank (disjoint
+        # across ranks); both flag bits are masked so the SUM reduce-scatter equals an OR
+        return pack_owner_flags(part, corr, contrib == rank, pos, world, blk)
 
     pool = [flags_for(1000 + k) for k in range(POOL)]
     recv = torch.empty(nbytes, dtype=torch.uint8, device=dev)

@@ -71,13 +71,40 @@ def _worker(rank, world, port, q):
         collided = False
     except FlagCollision as exc:
         collided = "[7]" in str(exc)
+    # config-4 exchange (bench_extra._c4): each shard packs its resolved sources' 2-bit flags
+    # by owner block; the uint8 SUM over ranks must equal the OR of the ranks' buffers and
+    # decode to the global (participated, correct) flags
+    from bayesian_engine.sharding import owner_of, pack_owner_flags
+    S4 = 1003
+    gid = np.arange(S4, dtype=np.int64)
+    own = owner_of(gid, world)
+    cnts = np.bincount(own, minlength=world)
+    blk = int((cnts.max() + 3) // 4 * 4)
+    loc = np.empty(S4, np.int64)
+    for r in range(world):
+        sel = np.nonzero(own == r)[0]
+        loc[sel] = np.arange(len(sel))
+    pos = torch.from_numpy(own.astype(np.int64) * blk + loc)
+    contrib = torch.from_numpy(((gid * 0x2545F491) >> 7) % world)
+    g4 = np.random.default_rng(44)  # the same draw on every rank, as the bench's seeded generator
+    part4 = torch.from_numpy(g4.random(S4) < 0.4)
+    corr4 = torch.from_numpy(g4.random(S4) < 0.6)
+    bufs = [pack_owner_flags(part4, corr4, contrib == r, pos, world, blk) for r in range(world)]
+    red = bufs[rank].clone()
+    dist.all_reduce(red, op=dist.ReduceOp.SUM)
+    orv = bufs[0].clone()
+    for b in bufs[1:]:
+        orv |= b
+    dec = ((red.numpy()[:, None] >> (2 * np.arange(4, dtype=np.uint8))) & 3).reshape(-1)[pos.numpy()]
+    exp4 = part4.numpy().astype(np.uint8) | ((part4 & corr4).numpy().astype(np.uint8) << 1)
+    c4_ok = bool(torch.equal(red, orv)) and bool(np.array_equal(dec, exp4))
     if rank == 0:
         full = orc.consensus_csr(off, sid, prob, rel, conf, present)
         call, tall = orc.agreement_stats(off, sid, prob, outcome, S)
         q.put(dict(parts=parts, full_cons=full["consensus"].tolist(), full_nu=full["n_unique"].tolist(),
                    counts_ok=bool(np.array_equal(ct.numpy(), call) and np.array_equal(tt.numpy(), tall)),
                    flags_ok=bool(torch.all(comb == 1).item()) and bool(torch.equal(comb2, exp2)),
-                   collided=collided))
+                   collided=collided, c4_ok=c4_ok))
     dist.destroy_process_group()
 
 
@@ -101,3 +128,4 @@ def test_two_rank_gloo_sharding():
     assert cons == res["full_cons"] and nu == res["full_nu"]
     assert res["counts_ok"] and res["flags_ok"]
     assert res["collided"], "a source flagged by two shards in one step must raise FlagCollision"
+    assert res["c4_ok"], "config-4 flag reduce must equal the OR of the shards' packed flags"
