@@ -317,7 +317,8 @@ class TieBreakResult:
 
 
 def tiebreak(offsets: torch.Tensor, pred: torch.Tensor, conf: torch.Tensor, weight: torch.Tensor,
-             rel: torch.Tensor, *, precision: int = 6, offsets_host: Optional[np.ndarray] = None) -> TieBreakResult:
+             rel: torch.Tensor, *, precision: int = 6, offsets_host: Optional[np.ndarray] = None,
+             out: Optional[TieBreakResult] = None) -> TieBreakResult:
     """DeterministicTieBreaker(precision).resolve for every CSR market (tiebreak.py:73-152).
 
     Any market length (> 4096 agents sort in a global scratch slice).  ``precision`` as
@@ -328,11 +329,11 @@ def tiebreak(offsets: torch.Tensor, pred: torch.Tensor, conf: torch.Tensor, weig
     dev = offsets.device
     f64 = dict(dtype=torch.float64, device=dev)
     i32 = dict(dtype=torch.int32, device=dev)
-    r = TieBreakResult(torch.empty(M, **f64), torch.empty(M, **i32), torch.empty(M, **i32),
-                       torch.empty(M, **f64), torch.empty(max(Nsig, 1), **f64),
-                       torch.empty(max(Nsig, 1), **i32), torch.empty(max(Nsig, 1), **f64),
-                       torch.empty(max(Nsig, 1), **f64), torch.empty(max(Nsig, 1), **f64),
-                       torch.empty(max(Nsig, 1), **i32))
+    r = out or TieBreakResult(torch.empty(M, **f64), torch.empty(M, **i32), torch.empty(M, **i32),
+                              torch.empty(M, **f64), torch.empty(max(Nsig, 1), **f64),
+                              torch.empty(max(Nsig, 1), **i32), torch.empty(max(Nsig, 1), **f64),
+                              torch.empty(max(Nsig, 1), **f64), torch.empty(max(Nsig, 1), **f64),
+                              torch.empty(max(Nsig, 1), **i32))
     offh = offsets_host if offsets_host is not None else offsets.cpu().numpy()
     lens = np.diff(offh)
     long_ = np.nonzero(lens > 64)[0]

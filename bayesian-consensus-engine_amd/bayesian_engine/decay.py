@@ -9,10 +9,10 @@ Scalars in -> Python floats out; numpy arrays / torch tensors in -> arrays out (
 The early returns for ``elapsed <= 0`` hand back the caller's own object, as the
 reference does (decay.py:52-53, 90-91).
 
-Parity note: the reference's ``2.0 ** x`` is glibc ``pow``, which is itself not
-correctly rounded for ~0.09% of inputs (measured); the GPU computes ``2.0 ** x`` as ocml
-``exp2(x)`` (<= 1 ulp), held to 2 ulp of the reference with the exact-match rate asserted,
-far inside the north-star tolerance (1e-9 absolute).  See DESIGN.md §3.
+Parity note: the reference's ``2.0 ** x`` is glibc ``pow``, which is not correctly
+rounded (it differs from a correctly rounded 2^x for ~0.1% of inputs); the GPU restates
+glibc's pow(2.0, y) itself (csrc/glibc_pow.hpp), so decayed values are bit-identical to
+the reference's.  See DESIGN.md §3.
 """
 from __future__ import annotations
 

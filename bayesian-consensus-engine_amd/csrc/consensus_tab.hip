@@ -11,13 +11,11 @@
 //
 //  load       a wave owns a tile of 64 consecutive markets.  A REGULAR tile (every market
 //             has 32 signals, 16-B aligned) is read with coalesced 16-B loads: eight
-//             consecutive lanes cover one contiguous 128-B piece of a market's row (chunk
-//             bits on lane bits 2..0, market bits on lane bits 5..3 and the load index).
-//             Three butterflies (DPP quad_perm / row_ror + a wave-constant select) swap
-//             lane bits 2..0 with load-index bits, leaving lane = market, register index =
-//             position.  (BCE_TAB_PIECE=64: four lanes per 64-B piece, two butterflies.)
-//             Other tiles (ragged lengths, the last tile, misaligned shards) load per lane.
-//             The next tile's offsets are read at the top of each tile.
+//             lanes (m, m+8, ..., m+56) cover one contiguous 128-B piece of a market's
+//             row.  Three butterflies (v_permlane32_swap, v_permlane16_swap, row_ror:8 DPP)
+//             swap those lane bits with load-index bits, leaving lane = market, register
+//             index = position.  Other tiles (ragged lengths, the last tile, misaligned
+//             shards) load per lane.  The next tile's offsets are read at the top of each tile.
 //  sort       keys (sid << 5 | position) with the probability as payload, Batcher
 //             odd-even merge network in VGPRs (branch-free, VGPR swap masks):
 //             duplicates of a source stay in input order.
@@ -37,13 +35,14 @@
 // Validation (core.py:59-60: first p < 0 or p > 1, NaN passes) reads the probabilities in
 // input order before the sort.  Exact mode only: every sum is the reference's own order.
 //
-// Measured (tools/tab_variants.py, measurements/tab_*_r02.txt): with nontemporal signal
-// loads and per-unique stores, 8 waves per CU (two per SIMD, 256 VGPRs, 6 spilled) beat 4;
-// wave-major tile order (consecutive tiles on consecutive workgroups / XCDs) -3.3%; a wave
-// priority ramp through the tile (1 walk, 2 per-market outputs, 3 per-unique stores) -4%.
-// The per-unique stores are the largest phase; 128-B pieces beat 64-B ones; loading the
-// next tile's signals ahead, unconditional chunk stores, a reciprocal-based normalizedWeight
-// and nontemporal per-market stores did not help.
+// Measured (tools/tab_variants.py, measurements/tab_*_r0[23].txt): with nontemporal signal
+// loads and per-unique stores, 8 waves per CU (two per SIMD, 256 VGPRs) beat 4; wave-major
+// tile order (consecutive tiles on consecutive workgroups / XCDs) -3.3%; a wave priority
+// ramp through the tile (1 walk, 2 per-market outputs, 3 per-unique stores) -4%; the
+// permlane transposes -2..3% against DPP-only ones.  The per-unique stores are the largest
+// phase; loading the next tile's signals ahead, unconditional chunk stores, a
+// reciprocal-based normalizedWeight and nontemporal per-market stores did not help.  The
+// alternatives live in tools/tab_variants.py (source patches), not here.
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -54,91 +53,37 @@
 namespace bce {
 namespace {
 
-#ifndef BCE_TAB_WAVES
-#define BCE_TAB_WAVES 8  // waves per workgroup (build knob; 8 = two per SIMD)
-#endif
-#ifndef BCE_TAB_PROF
-#define BCE_TAB_PROF 0  // experiment builds only (tools/tab_variants.py): per-phase s_memtime
-#endif
-#if BCE_TAB_PROF
-__device__ unsigned long long g_tab_prof[8];
-#define TAB_MARK(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); prof[k] += t_ - prof_t; prof_t = t_; } while (0)
-#else
-#define TAB_MARK(k) do {} while (0)
-#endif
-#ifndef BCE_TAB_PIECE
-#define BCE_TAB_PIECE 128  // bytes of a market row one load/store instruction's lane group covers
-#endif
-#ifndef BCE_TAB_NT
-#define BCE_TAB_NT 3  // bit 0: nontemporal signal loads, bit 1: per-unique stores, bit 2: per-market stores
-#endif
+constexpr int kTabWaves = 8;  // waves per workgroup (two per SIMD); one workgroup per CU (LDS-bound)
+constexpr int kPL = 8;         // lanes per 128-B piece of a market row (16 B each)
+constexpr int kLB = 3;         // log2 kPL
+constexpr int kMG = 64 / kPL;  // markets per load instruction
+constexpr int kTabRing = 8;    // LDS table reads issued ahead of the walk (4/6/8 measured equal)
+
+// Nontemporal signal loads and per-unique stores (the per-market stores stay default:
+// nt there measured slower, measurements/tab_nt_variants_r02.txt).
 typedef unsigned tab_u4v __attribute__((ext_vector_type(4)));
 typedef double tab_d2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint4 tab_ld16(const uint32_t* p) {
-  if constexpr ((BCE_TAB_NT & 1) != 0) {
-    const tab_u4v v = __builtin_nontemporal_load(reinterpret_cast<const tab_u4v*>(p));
-    return make_uint4(v.x, v.y, v.z, v.w);
-  } else {
-    return *reinterpret_cast<const uint4*>(p);
-  }
+  const tab_u4v v = __builtin_nontemporal_load(reinterpret_cast<const tab_u4v*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ void tab_st16(int32_t* p, uint4 v) {
-  if constexpr ((BCE_TAB_NT & 2) != 0) {
-    const tab_u4v x = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(x, reinterpret_cast<tab_u4v*>(p));
-  } else {
-    *reinterpret_cast<uint4*>(p) = v;
-  }
+  const tab_u4v x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, reinterpret_cast<tab_u4v*>(p));
 }
 __device__ __forceinline__ void tab_st16(double* p, double x0, double x1) {
-  if constexpr ((BCE_TAB_NT & 2) != 0) {
-    const tab_d2v x = {x0, x1};
-    __builtin_nontemporal_store(x, reinterpret_cast<tab_d2v*>(p));
-  } else {
-    *reinterpret_cast<double2*>(p) = make_double2(x0, x1);
-  }
+  const tab_d2v x = {x0, x1};
+  __builtin_nontemporal_store(x, reinterpret_cast<tab_d2v*>(p));
 }
-#ifndef BCE_TAB_PRIO
-#define BCE_TAB_PRIO 1  // wave priority ramp from the walk through the stores (0: off)
-#endif
-#ifndef BCE_TAB_PLX
-#define BCE_TAB_PLX 1  // permlane-swap transposes (chunks on lane bits 5..3; -2..3%), needs BCE_TAB_PIECE 128
-#endif
-#ifndef BCE_TAB_MAP
-#define BCE_TAB_MAP 1  // 1: wave-major tile order (see the tile loop), 0: block-major
-#endif
-constexpr int kTabWaves = BCE_TAB_WAVES;  // waves per workgroup; one workgroup per CU (LDS-bound)
-constexpr int kPL = BCE_TAB_PIECE / 16;    // lanes per piece (16 B each): 4 or 8
-constexpr int kLB = (kPL == 8) ? 3 : 2;    // log2 kPL
-constexpr int kMG = 64 / kPL;              // markets per load instruction
-static_assert(kPL == 4 || kPL == 8, "BCE_TAB_PIECE: 64 or 128");
-static_assert(!BCE_TAB_PLX || kPL == 8, "BCE_TAB_PLX needs 128-B pieces");
-#ifndef BCE_TAB_RING
-#define BCE_TAB_RING 8  // LDS table reads in flight during the walk (4/6/8 measured equal)
-#endif
-constexpr int kTabRing = BCE_TAB_RING;  // LDS table reads issued ahead of the walk
 
 // ---- lane-bit <-> register-bit butterflies -------------------------------------------
-// For a register pair (a: index bit 0, b: index bit 1) swap lane bit L (0, 1 or 2) with
-// that index bit: a' = bit_L ? b[lane ^ 2^L] : a,  b' = bit_L ? b : a[lane ^ 2^L].  The
-// partner lane comes from a DPP quad_perm (L < 2); the select mask is a wave constant.
-// Lane bit 2: the partner l ^ 4 is row_ror:4 (l - 4) for lanes with the bit set and
-// row_ror:12 (l + 4) for the others -- neither leaves its 8-lane group.
-template <int L>
-__device__ __forceinline__ void bfly(uint32_t& a, uint32_t& b, int lane) {
-  constexpr int hi_ctl = (L == 0) ? 0xB1 : (L == 1) ? 0x4E : 0x124;  // quad_perm / row_ror:4
-  constexpr int lo_ctl = (L == 0) ? 0xB1 : (L == 1) ? 0x4E : 0x12C;  // quad_perm / row_ror:12
-  const bool hi = ((lane >> L) & 1) != 0;
-  const uint32_t bx = (uint32_t)__builtin_amdgcn_mov_dpp((int)b, hi_ctl, 0xF, 0xF, true);
-  const uint32_t ax = (uint32_t)__builtin_amdgcn_mov_dpp((int)a, lo_ctl, 0xF, 0xF, true);
-  const uint32_t na = hi ? bx : a;
-  b = hi ? b : ax;
-  a = na;
-}
-// BCE_TAB_PLX: the piece's eight 16-B chunks sit on lane bits 5..3 instead of 2..0 (same
-// addresses per instruction, lanes permuted -- no memory cost, tools/tile_probe.hip), so
-// two of the three butterflies are single v_permlane32_swap / v_permlane16_swap
-// instructions per register pair and the third a row_ror:8 DPP pair; lane = market.
+// A 128-B piece of a market row is read by eight lanes m, m+8, ..., m+56: the piece's
+// eight 16-B chunks sit on lane bits 5..3 (the same addresses per instruction as eight
+// consecutive lanes -- no memory cost, tools/tile_probe.hip).  For a register pair (a:
+// index bit j, b: the partner with that bit set) each butterfly swaps one of those lane
+// bits with the index bit: a' = bit ? b[lane ^ 2^L] : a, b' = bit ? b : a[lane ^ 2^L].
+// Lane bit 5 is one v_permlane32_swap per pair, bit 4 one v_permlane16_swap, bit 3 a
+// row_ror:8 DPP pair with a wave-constant select.
 __device__ __forceinline__ void bfly_pl32(uint32_t& a, uint32_t& b) {  // lane bit 5
   const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
   a = r[0];
@@ -157,47 +102,21 @@ __device__ __forceinline__ void bfly_r8(uint32_t& a, uint32_t& b, int lane) {  /
   b = hi ? b : ax;
   a = na;
 }
-// Swap lane bits kLB-1..0 (BCE_TAB_PLX: 5..3) with dword-index bits kLB+1..2 of r[N] (an
-// involution).
+// Swap lane bits 5..3 with dword-index bits 4..2 of r[N] (an involution).  The three
+// butterflies commute; permlane32 / permlane16 / row_ror:8 measured 4% faster than the
+// reverse order on the same box (0.2090 vs 0.2184 ms median, measurements/tab_xord_r03.txt)
+// although the reverse order spills fewer VGPRs.
 template <int N>
 __device__ __forceinline__ void xpose(uint32_t (&r)[N], int lane) {
-  if constexpr (BCE_TAB_PLX) {
-    // (the three butterflies commute; this order keeps the kernel at 6 spilled VGPRs,
-    // permlane32 first spilled 21)
-#ifdef BCE_TAB_XORD_OLD
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-      if (!(i & 16)) bfly_pl32(r[i], r[i | 16]);
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-      if (!(i & 8)) bfly_pl16(r[i], r[i | 8]);
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-      if (!(i & 4)) bfly_r8(r[i], r[i | 4], lane);
-#else
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-      if (!(i & 4)) bfly_r8(r[i], r[i | 4], lane);
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-      if (!(i & 8)) bfly_pl16(r[i], r[i | 8]);
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-      if (!(i & 16)) bfly_pl32(r[i], r[i | 16]);
-#endif
-    return;
-  }
-  if constexpr (kLB == 3) {
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-      if (!(i & 16)) bfly<2>(r[i], r[i | 16], lane);
-  }
 #pragma unroll
   for (int i = 0; i < N; ++i)
-    if (!(i & 8)) bfly<1>(r[i], r[i | 8], lane);
+    if (!(i & 16)) bfly_pl32(r[i], r[i | 16]);
 #pragma unroll
   for (int i = 0; i < N; ++i)
-    if (!(i & 4)) bfly<0>(r[i], r[i | 4], lane);
+    if (!(i & 8)) bfly_pl16(r[i], r[i | 8]);
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+    if (!(i & 4)) bfly_r8(r[i], r[i | 4], lane);
 }
 
 // Regular-tile address maps (tile = 64 markets x 32 signals from B; PL = kPL lanes per
@@ -209,12 +128,12 @@ __device__ __forceinline__ void xpose(uint32_t (&r)[N], int lane) {
 // Swapping the log2 PL lane bits of c with the low load-index bits leaves one market per
 // lane -- lane L holds market tmkt(L) = MG (L & (PL-1)) + (L >> log2 PL) -- and the
 // register index = the position, for both arrays.
-__device__ __forceinline__ int tmkt(int lane) {
-  return BCE_TAB_PLX ? lane : ((lane & (kPL - 1)) * kMG) | (lane >> kLB);
-}
+// (With the chunks on lane bits 5..3, lane L reads market group q = L & 7, chunk c = L >> 3,
+// and after the transpose holds market L.)
+__device__ __forceinline__ int tmkt(int lane) { return lane; }
 // this lane's market-within-group q and chunk c in the regular-tile address maps
-__device__ __forceinline__ int lq(int lane) { return BCE_TAB_PLX ? (lane & 7) : (lane >> kLB); }
-__device__ __forceinline__ int lc(int lane) { return BCE_TAB_PLX ? (lane >> 3) : (lane & (kPL - 1)); }
+__device__ __forceinline__ int lq(int lane) { return lane & 7; }
+__device__ __forceinline__ int lc(int lane) { return lane >> 3; }
 // Odd-even merge network over 31-bit keys with a 64-bit payload, branch- and SGPR-free:
 // the swap mask is the sign of y - x (keys < 2^31), the payload moves with v_bfi_b32.
 // (Compare-and-select would give every comparator of a stage its own SGPR-pair condition;
@@ -325,12 +244,9 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
   // Wave-major tile order: tile = w * grid + block, so the tiles in flight at any moment
   // are spread over every workgroup (and XCD) instead of 8 consecutive tiles per CU
   // (tools/tile_probe.hip: 0.204 -> 0.195 ms for the same bytes and shapes)
-  int64_t tile = BCE_TAB_MAP ? (int64_t)w * gridDim.x + blockIdx.x : (int64_t)blockIdx.x * kTabWaves + w;
+  int64_t tile = (int64_t)w * gridDim.x + blockIdx.x;
   Meta cur = meta(tile, lane_id());
   uint32_t s[32], pw[64];
-#if BCE_TAB_PROF
-  unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prof_t = __builtin_amdgcn_s_memtime();
-#endif
   for (; tile < n_tiles; tile += stride) {
     // lane-derived offsets are recomputed per tile: hoisted out of the loop, the 24 load
     // and 40 store address offsets would stay live across the whole tile
@@ -367,7 +283,6 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
 #pragma unroll
       for (int t = 0; t < 32; ++t) s[t] = 0u;
     }
-    TAB_MARK(0);  // metadata + loads + transposes
     __builtin_amdgcn_sched_barrier(0);
     double p[32];
 #pragma unroll
@@ -395,7 +310,6 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
       key[t] = (m & ((min(s[t], smax) << 5) | (unsigned)t)) | (~m & 0x7FFFFFFFu);
     }
     oem_sort_kv31(key, p);
-    TAB_MARK(1);  // validation + keys + sort
     __builtin_amdgcn_sched_barrier(0);
     unsigned nq = 0;
 #pragma unroll
@@ -444,7 +358,7 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
     // per-unique stores, back to 0 for the next tile's loads): of the two waves sharing a
     // SIMD, the one further into its tile issues first, so its stores leave while the other
     // wave's loads are in flight (-4.2% against none, tools/tab_variants.py)
-    if (BCE_TAB_PRIO) __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_s_setprio(1);
     double2 ring[kTabRing];
     uint32_t rbits[kTabRing];
 #pragma unroll
@@ -479,32 +393,22 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
     }
     const int u = __builtin_popcount(lb);
 
-    TAB_MARK(2);  // walk
     // ---- per-market results (lane = market, coalesced) -----------------------------------
-    if (BCE_TAB_PRIO) __builtin_amdgcn_s_setprio(2);
+    __builtin_amdgcn_s_setprio(2);
     if (has) {
       const bool null_ = (total == 0.0);  // core.py:131-133
-      if constexpr ((BCE_TAB_NT & 4) != 0) {
-        __builtin_nontemporal_store(null_ ? 0.0 : ws / total, a.consensus + mk);
-        __builtin_nontemporal_store(null_ ? 0.0 : cs / total, a.confidence + mk);
-        __builtin_nontemporal_store(total, a.total_weight + mk);
-        __builtin_nontemporal_store(u, a.n_unique + mk);
-        if (a.err_idx) __builtin_nontemporal_store(err, a.err_idx + mk);
-      } else {
-        a.consensus[mk] = null_ ? 0.0 : ws / total;
-        a.confidence[mk] = null_ ? 0.0 : cs / total;
-        a.total_weight[mk] = total;
-        a.n_unique[mk] = u;
-        if (a.err_idx) a.err_idx[mk] = err;
-      }
+      a.consensus[mk] = null_ ? 0.0 : ws / total;
+      a.confidence[mk] = null_ ? 0.0 : cs / total;
+      a.total_weight[mk] = total;
+      a.n_unique[mk] = u;
+      if (a.err_idx) a.err_idx[mk] = err;
     }
     if (!do_any) {
-      if (BCE_TAB_PRIO) __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_setprio(0);
       cur = nxt;
       continue;
     }
 
-    TAB_MARK(3);  // per-market stores
     // ---- compaction: unique j = the j-th emitted position ---------------------------------
     const unsigned full = (u >= 32) ? 0xFFFFFFFFu : ((1u << u) - 1u);
     if (ballot(lb != full)) {
@@ -529,9 +433,8 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
       }
     }
 
-    TAB_MARK(4);  // compaction
     // ---- per-unique outputs --------------------------------------------------------------
-    if (BCE_TAB_PRIO) __builtin_amdgcn_s_setprio(3);
+    __builtin_amdgcn_s_setprio(3);
     __builtin_amdgcn_sched_barrier(0);
     if (reg) {
       // re-derive the tile base and the lane offsets here: without the opaque copies the
@@ -546,7 +449,7 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
       double tk[kPL];
 #pragma unroll
       for (int k = 0; k < kPL; ++k) {  // market MG·k + q of load index k sits in lane PL·q + k
-        const int src = (BCE_TAB_PLX ? ((k << 3) | (lane & 7)) : ((lane & ~(kPL - 1)) | k)) << 2;
+        const int src = ((k << 3) | (lane & 7)) << 2;
         uk[k] = __builtin_amdgcn_ds_bpermute(src, u);
         tk[k] = dbl((uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)lo32(total)),
                     (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)hi32(total)));
@@ -602,26 +505,13 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
         }
       }
     }
-    if (BCE_TAB_PRIO) __builtin_amdgcn_s_setprio(0);
-    TAB_MARK(5);  // per-unique stores
+    __builtin_amdgcn_s_setprio(0);
     cur = nxt;
   }
-#if BCE_TAB_PROF
-  if (lane_id() == 0)
-    for (int k = 0; k < 6; ++k) atomicAdd(&g_tab_prof[k], prof[k]);
-#endif
 }
 
 }  // namespace
 
-#if BCE_TAB_PROF
-extern "C" int bce_tab_prof_read(unsigned long long* host8) {
-  BCE_HIP(hipMemcpyFromSymbol(host8, HIP_SYMBOL(g_tab_prof), 8 * sizeof(unsigned long long)));
-  unsigned long long z[8] = {0};
-  BCE_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_tab_prof), z, sizeof z));
-  return BCE_OK;
-}
-#endif
 
 int launch_tab32(const ConsArgs& a, hipStream_t st) {
   const int64_t tiles = (a.n_list + 63) / 64;

@@ -9,6 +9,7 @@
 // and written with 16-byte accesses.  FP contraction off (CPython rounding).
 #include "bce_device.hpp"
 #include "bce_internal.hpp"
+#include "glibc_pow.hpp"
 
 #pragma clang fp contract(off)
 
@@ -28,7 +29,7 @@ __device__ __forceinline__ double decayed(double r, int64_t t_us, const DecayCon
   const double secs = (double)(k.now_us - t_us) / 1e6;  // timedelta.total_seconds()
   const double days = py_max(0.0, secs / 86400.0);
   if (!(days > 0.0)) return r;
-  const double f = exp2(-days / k.half_life);  // == 2.0 ** x (ocml exp2, <= 1 ulp)
+  const double f = bce_pow::pow_base2(-days / k.half_life);  // 2.0 ** x as libm pow (glibc_pow.hpp)
   const double d = k.min_rel + (r - k.min_rel) * f;
   return py_max(k.min_rel, py_min(1.0, d));
 }
@@ -76,7 +77,7 @@ __global__ __launch_bounds__(256) void decay_apply_kernel(int64_t n, const doubl
   for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < n;
        s += (int64_t)gridDim.x * blockDim.x) {
     const double e = days[s];
-    const double f = (e <= 0) ? 1.0 : exp2(-e / h);  // == 2.0 ** x (ocml exp2, <= 1 ulp)
+    const double f = (e <= 0) ? 1.0 : bce_pow::pow_base2(-e / h);  // 2.0 ** x as libm pow
     if (factor) factor[s] = f;
     if (out) {
       const double r = rel[s];

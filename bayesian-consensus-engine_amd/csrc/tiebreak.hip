@@ -10,6 +10,7 @@
 // reduction order selects the same winner.
 #include "bce_device.hpp"
 #include "bce_internal.hpp"
+#include "glibc_pow.hpp"
 
 #pragma clang fp contract(off)
 
@@ -128,13 +129,13 @@ __global__ __launch_bounds__(256) void tiebreak_wave_kernel(TbArgs a, const int3
     }
     const double dens = is_leader ? tot / (double)cnt : 0.0;
     const double avgc = is_leader ? cs / (double)cnt : 0.0;
-    // variance of all confidences (tiebreak.py:104-106): sequential sums
+    // variance of all confidences (tiebreak.py:108-110): sequential sums
+    // (c - mean) ** 2 is libm pow, not d*d (glibc_pow.hpp): every lane squares its own
+    // agent's deviation, then the squares are summed in agent order
     const double mean = csum_all / (double)n;
+    const double sq = v ? bce_pow::pow2(c - mean) : 0.0;
     double vs = 0.0;
-    for (int j = 0; j < n; ++j) {
-      const double d = rl_f64(c, j) - mean;
-      vs += d * d;
-    }
+    for (int j = 0; j < n; ++j) vs += rl_f64(sq, j);
     const unsigned long long lm = ballot(is_leader);
     const int ng = __popcll(lm);
     // winner: lexicographic max over leaders
@@ -320,16 +321,25 @@ __global__ __launch_bounds__(kTbThreads) void tiebreak_block_kernel(TbArgs a, co
       }
       if (tot / (double)cnt == wd && mx == wm) sFlag = 1;
     }
-    // confidence variance (tiebreak.py:104-106): sequential, one lane
+    // confidence variance (tiebreak.py:108-110): the mean and the sum of squares run in
+    // agent order on one lane; the squares -- libm pow(d, 2.0), glibc_pow.hpp -- are
+    // computed by every thread for its agents into the (now dead) sort keys
     if (tid == 0) {
       double csum = 0.0;
       for (int i = 0; i < n; ++i) csum += a.conf[off + i];
-      const double mean = csum / (double)n;
+      sVar = csum / (double)n;
+    }
+    __syncthreads();
+    {
+      const double mean = sVar;
+      double* const sq = reinterpret_cast<double*>(sk);
+      for (int i = tid; i < n; i += kTbThreads) sq[i] = bce_pow::pow2(a.conf[off + i] - mean);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const double* const sq = reinterpret_cast<const double*>(sk);
       double vs = 0.0;
-      for (int i = 0; i < n; ++i) {
-        const double d = a.conf[off + i] - mean;
-        vs += d * d;
-      }
+      for (int i = 0; i < n; ++i) vs += sq[i];
       sVar = vs / (double)n;
     }
     __syncthreads();

@@ -26,7 +26,7 @@ Also measured here:
                 its outputs are also the full-size parity check (all eight outputs).
 Before the W warmup steps the device runs the step for --prewarm-s seconds so the clocks
 have ramped (a 20-step run then matches a 200-step one); that time is reported.
-Other configs (--config c3|c4|c5|ns|agg) are secondary bench lines; the default is c2.
+Other configs (--config c3|c4|c5|ns|agg|tb) are secondary bench lines; the default is c2.
 """
 from __future__ import annotations
 
@@ -56,7 +56,7 @@ def parse(argv=None):
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=50)
     p.add_argument("--prewarm-s", type=float, default=1.0, help="clock ramp before the warmup steps")
-    p.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5", "ns", "agg"])
+    p.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5", "ns", "agg", "tb"])
     p.add_argument("--markets", type=int, default=1_000_000)
     p.add_argument("--len", type=int, default=32)
     p.add_argument("--sources", type=int, default=10_000)
@@ -65,6 +65,9 @@ def parse(argv=None):
                         "the north star's fixed-order trees within 1e-9 -- for c3, with the exact-mode "
                         "time reported beside it)")
     p.add_argument("--agents", type=int, default=16384, help="config 5 agents")
+    p.add_argument("--compact", action="store_true",
+                   help="c2: scalars only (consensus, confidence, total weight, uniqueSources, validation) -- "
+                        "no per-unique sourceWeights outputs (SURVEY.md d2 compact mode, 0.420e9 B)")
     p.add_argument("--events", default="region", choices=["step", "region"],
                    help="one HIP event pair around the timed region (default: per-step average "
                         "incl. the launch boundaries), or a pair around every step (~6 us per step)")
@@ -72,6 +75,9 @@ def parse(argv=None):
     p.add_argument("--cpu-seconds", type=float, default=2.0, help="wall-clock budget of the CPU baseline")
     p.add_argument("--no-parity", action="store_true")
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
+    p.add_argument("--shard", default=None,
+                   help="c3 only: R/N or all/N -- time rank R's (or every rank's) market shard of an N-rank "
+                        "run in this one process, no process group (predicted strong scaling)")
     p.add_argument("--stub", action="store_true",
                    help="launcher self-test: a CPU no-op step under gloo (no GPU, no library)")
     return p.parse_args(argv)
@@ -284,15 +290,18 @@ def cpu_baseline_c2(offsets, sid, prob, rel, conf, present, budget_s):
                        f"oracle/bce_oracle.c on {threads} threads, {reps} passes in {dt:.2f} s"), out
 
 
-def parity_all_outputs(res, cpu, offsets):
-    """All eight outputs vs the CPU restatement, bit for bit (per-unique slots < n_unique)."""
-    got = {k: getattr(res, k).cpu().numpy() for k in
-           ("consensus", "confidence", "total_weight", "n_unique", "err_idx", "usid", "weight", "nweight")}
+def parity_all_outputs(res, cpu, offsets, unique=True):
+    """All eight outputs vs the CPU restatement, bit for bit (per-unique slots < n_unique);
+    the five per-market ones in compact mode."""
+    keys = ("consensus", "confidence", "total_weight", "n_unique", "err_idx")
+    got = {k: getattr(res, k).cpu().numpy() for k in keys + (("usid", "weight", "nweight") if unique else ())}
     ok = {}
     for k in ("n_unique", "err_idx"):
         ok[k] = bool(np.array_equal(got[k], cpu[k]))
     for k in ("consensus", "confidence", "total_weight"):
         ok[k] = bool(np.array_equal(got[k], cpu[k], equal_nan=True))
+    if not unique:
+        return ok
     u = cpu["n_unique"].astype(np.int64)
     pos = np.repeat(offsets[:-1], u) + (np.arange(int(u.sum())) - np.repeat(np.cumsum(u) - u, u))
     for k in ("usid", "weight", "nweight"):
@@ -325,11 +334,13 @@ def bench_c2(args, world, rank):
     d_prob = torch.from_numpy(prob).to(dev)
     table = batch.SourceTable.from_arrays(torch.from_numpy(rel).to(dev), torch.from_numpy(conf).to(dev),
                                           torch.from_numpy(present).to(dev))
-    res = batch._alloc(M, M * L, dev, True, True)
+    uniq = not args.compact
+    res = batch._alloc(M, M * L, dev, uniq, True)
     stream = torch.cuda.current_stream(dev)
 
     def step():
-        batch.consensus(d_off, d_sid, d_prob, table, max_len=L, mode=args.mode or "exact", out=res)
+        batch.consensus(d_off, d_sid, d_prob, table, max_len=L, mode=args.mode or "exact", out=res,
+                        unique_outputs=uniq)
 
     wall, avg_kernel_s, prewarm = timed_loop(step, args, world, stream)
     N.check_faults(dev, "c2 timed steps")  # a kernel that gave up would leave stale outputs
@@ -337,11 +348,15 @@ def bench_c2(args, world, rank):
     # algorithmic bytes per launch
     sum_u = int(res.n_unique.sum().item())
     n_sig = M * L
-    bytes_per_launch = 12 * n_sig + (8 * (M + 1)) + 32 * M + 20 * sum_u + 16 * S + (S + 7) // 8
+    bytes_per_launch = (12 * n_sig + (8 * (M + 1)) + 32 * M + (20 * sum_u if uniq else 0) + 16 * S
+                        + (S + 7) // 8)
     achieved_gbs = bytes_per_launch / avg_kernel_s / 1e9
-    kernel = ("consensus_tab32_kernel" if 16 < L <= 32 and S <= 10112 else "consensus_pipe_kernel"
-              if L <= 32 else "consensus_seg_kernel")
-    traffic, _ = read_pmc("pmc_c2.json", markets=M, signals_per_market=L, kernel=kernel)
+    # the kernel bce_consensus_csr picks (consensus.hip launch_seg_for_len)
+    kernel = ("consensus_tab32_kernel" if 16 < L <= 32 and S <= 10112 else
+              "consensus_pipe_kernel" if L <= 32 and S <= 16384 and uniq else
+              "consensus_flat_kernel" if L <= 32 else "consensus_seg_kernel")
+    traffic, _ = (read_pmc("pmc_c2.json", markets=M, signals_per_market=L, sources=S, kernel=kernel)
+                  if uniq else (None, None))
 
     total_signals = sum_over_ranks(float(n_sig * args.steps), world)
     value = total_signals / wall
@@ -361,7 +376,8 @@ def bench_c2(args, world, rank):
         "dtype": "f64",
         "data": "synthetic (SURVEY.md d2 distributions, PCG64 seed 2+rank)",
         "config": {"workload": f"c2: {M} markets x {L} signals, {S} sources, batched consensus + "
-                               f"validation + sourceWeights outputs, mode={args.mode or 'exact'}",
+                               f"validation{' + sourceWeights outputs' if uniq else ' (compact: scalars only)'}, "
+                               f"mode={args.mode or 'exact'}",
                    "markets_per_gpu": M, "signals_per_market": L, "sources": S,
                    "parallelism": f"markets sharded, {world} independent rank(s), no collective"},
         "world_size": world,
@@ -376,7 +392,7 @@ def bench_c2(args, world, rank):
         cb, cpu_out = cpu_baseline_c2(offsets, sid, prob, rel, conf, present, args.cpu_seconds)
         out["cpu_baseline"] = cb
         if not args.no_parity:
-            ok = parity_all_outputs(res, cpu_out, offsets)
+            ok = parity_all_outputs(res, cpu_out, offsets, uniq)
             out["parity_vs_oracle"] = {"all_equal": all(ok.values()), "outputs": ok}
     return out
 
@@ -398,6 +414,10 @@ def main(argv=None):
     world, rank, _ = dist_setup(args)
     if args.stub:
         out = bench_stub(args, world, rank)
+    elif args.shard:
+        from bench_extra import c3_shards
+
+        out = c3_shards(args)
     elif args.config != "c2":
         from bench_extra import run_extra  # secondary configs
 

@@ -22,6 +22,11 @@ process may use (kind "port"), over a bounded sample of the same workload, rank 
       global scopes, each holding a row for ~50% of sources, 10% unparseable stamps),
       decay on.  Step = one bce_namespace_resolve launch producing the packed consensus
       table.  Sources shard by owner (weak scaling), no collective.
+  tb  SURVEY §8(a) a8: DeterministicTieBreaker.resolve over the config-2 batch (1M markets
+      x 32 agents, 10% of markets on the {0.1..0.9} grid so their groups tie): prediction =
+      the signal's probability, confidence / reliability = its source's table row, weight =
+      the reliability.  Step = one batched tie-break (winner, label, group count, variance,
+      per-group diagnostics and every agent's group ordinal).
   agg SURVEY §8(f) f4: aggregate_consensus over 10k member groups of 1000 markets each
       (contiguous pattern-matched ranges of a 1M-market batch, 20% without consensus).
       Step = one bce_aggregate_groups launch (weighted_average, majority, confidence;
@@ -63,7 +68,7 @@ def _pmc(name, **match):
 def run_extra(args, world, rank):
     from bench import barrier, max_over_ranks, sum_over_ranks  # noqa: E402
 
-    fn = {"c3": _c3, "c4": _c4, "c5": _c5, "ns": _ns, "agg": _agg}[args.config]
+    fn = {"c3": _c3, "c4": _c4, "c5": _c5, "ns": _ns, "agg": _agg, "tb": _tb}[args.config]
     return fn(args, world, rank, barrier, max_over_ranks, sum_over_ranks)
 
 
@@ -388,8 +393,8 @@ def _c4(args, world, rank, barrier, max_over, sum_over):
 
 def _parity_c4(step, state, pool, arrays, S, now0, day, args):
     """One more replay step on all S sources vs the restatement on a host snapshot of the
-    table: rel / conf / t / present bit for bit, the decayed view within 2 ulp (exp2 vs
-    glibc pow) with the bit-exact share reported."""
+    table: rel / conf / t / present and the decayed view bit for bit (the view's 2.0 ** x
+    is glibc pow restated)."""
     if args.no_parity or args.no_cpu_baseline:
         return None
     import sys
@@ -413,7 +418,7 @@ def _parity_c4(step, state, pool, arrays, S, now0, day, args):
           "conf": bool(np.array_equal(conf[:S].cpu().numpy(), c2)),
           "t_us": bool(np.array_equal(t_us[:S].cpu().numpy(), t2)),
           "present": bool(np.array_equal(present[:S].cpu().numpy(), p2)),
-          "view_2ulp": bool(np.all(ulps <= 2.0))}
+          "view": bool(np.array_equal(v, v_exp))}
     return {"all_ok": all(ok.values()), "outputs": ok, "sources": S, "participants": int((flags & 1).sum()),
             "view_bit_exact_share": float(np.mean(v == v_exp)), "view_max_ulps": float(ulps.max())}
 
@@ -625,3 +630,163 @@ def _agg(args, world, rank, barrier, max_over, sum_over):
                      "bytes_per_launch": bpm * G * K, "avg_launch_ms": per * 1e3},
         "cpu_baseline": None,
     }
+
+
+# ---------------------------------------------------------------------------------------
+def _cpu_tb(off, pred, conf, weight, rel, args):
+    """orc_tiebreak_csr (libm pow / round like the reference) over market chunks on host
+    threads.  Returns (cpu_baseline dict, outputs of the first pass) or (None, None)."""
+    if args.no_cpu_baseline:
+        return None, None
+    import sys
+    from concurrent.futures import ThreadPoolExecutor
+
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as orc
+
+    T = _threads()
+    M = len(off) - 1
+    cuts = np.linspace(0, M, T + 1).astype(np.int64)
+
+    def part(i):
+        m0, m1 = int(cuts[i]), int(cuts[i + 1])
+        a, b = int(off[m0]), int(off[m1])
+        return m0, a, orc.tiebreak_csr(off[m0:m1 + 1] - a, pred[a:b], conf[a:b], weight[a:b], rel[a:b])
+
+    t0, reps, first = time.perf_counter(), 0, None
+    with ThreadPoolExecutor(T) as ex:
+        while True:
+            parts = list(ex.map(part, range(T)))
+            first = first or parts
+            reps += 1
+            dt = time.perf_counter() - t0
+            if dt >= args.cpu_seconds:
+                break
+    N = int(off[-1])
+    out = {k: np.zeros(M, parts[0][2][k].dtype) for k in ("winner", "label", "n_groups", "variance")}
+    for k in ("g_key", "g_count", "g_total", "g_avgconf", "g_maxrel"):
+        out[k] = np.zeros(N, parts[0][2][k].dtype)
+    for m0, a, o in first:
+        mm = len(o["winner"])
+        for k in ("winner", "label", "n_groups", "variance"):
+            out[k][m0:m0 + mm] = o[k]
+        for k in ("g_key", "g_count", "g_total", "g_avgconf", "g_maxrel"):
+            out[k][a:a + len(o[k])] = o[k]
+    return ({"value": N * reps / dt, "unit": "signals/s", "cores": T, "kind": "port", "label": "restatement",
+             "sample": f"the full workload ({M} markets x {N // max(M, 1)} agents, seed-identical), "
+                       f"orc_tiebreak_csr on {T} threads, {reps} passes in {dt:.2f} s"}, out)
+
+
+def _tb(args, world, rank, barrier, max_over, sum_over):
+    from bayesian_engine import _native as N
+    from bayesian_engine import batch
+    from bench import make_c2
+
+    M, L, S = args.markets, args.len, args.sources
+    off, sid, prob, rel_t, conf_t, present = make_c2(M, L, S, seed=2 + rank)
+    pred, conf, rel = prob, conf_t[sid], rel_t[sid]
+    weight = rel
+    dev = torch.device("cuda", torch.cuda.current_device())
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    d = [T(off), T(pred), T(conf), T(weight), T(rel)]
+    res = batch.tiebreak(*d, offsets_host=off)
+
+    def step():
+        batch.tiebreak(*d, offsets_host=off, out=res)
+
+    wall, per = _timed(step, args, world, torch.cuda.current_stream(dev), barrier, max_over)
+    n = M * L
+    ng = res.n_groups.cpu().numpy().astype(np.int64)
+    sum_g = int(ng.sum())
+    # in: pred, conf, weight, rel (32 B per agent) + offsets; out per market: winner,
+    # variance (8 B each), label, n_groups (4 B each); per group: key, density, avg
+    # confidence, max reliability (8 B each), count (4 B); per agent: group ordinal (4 B)
+    bytes_step = 32 * n + 8 * (M + 1) + 24 * M + 36 * sum_g + 4 * n
+    achieved = bytes_step / per / 1e9
+    parity, cpu_line = None, None
+    if rank == 0 and world == 1:
+        cpu_line, cpu = _cpu_tb(off, pred, conf, weight, rel, args)
+        if cpu is not None and not args.no_parity:
+            got = {k: getattr(res, k).cpu().numpy() for k in ("winner", "label", "n_groups", "variance", "g_key",
+                                                            "g_count", "g_avgconf", "g_maxrel")}
+            pos = np.repeat(off[:-1], ng) + (np.arange(sum_g) - np.repeat(np.cumsum(ng) - ng, ng))
+            ok = {k: bool(np.array_equal(got[k], cpu[k], equal_nan=True))
+                  for k in ("winner", "label", "n_groups", "variance")}
+            for k in ("g_key", "g_count", "g_avgconf", "g_maxrel"):
+                ok[k] = bool(np.array_equal(got[k][pos], cpu[k][pos], equal_nan=True))
+            lab = got["label"]
+            parity = {"all_equal": all(ok.values()), "outputs": ok,
+                      "labels": {"unanimous": int((lab == 0).sum()), "weight_density": int((lab == 1).sum()),
+                                 "prediction_value_smallest": int((lab == 2).sum())},
+                      "round6_variance_equal": bool(np.array_equal(np.round(got["variance"], 6),
+                                                                   np.round(cpu["variance"], 6)))}
+    N.check_faults(dev, "tb timed steps")
+    tot = sum_over(float(n * args.steps), world)
+    return {
+        "metric": "signals tie-broken/sec (node), DeterministicTieBreaker.resolve over 1M markets x 32 agents",
+        "value": tot / wall, "unit": "signals/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic (the c2 batch; 10% grid markets force ties)",
+        "config": {"workload": f"tb: {M} markets x {L} agents, precision 6", "groups_per_market_mean": sum_g / M,
+                   "parallelism": f"markets sharded over {world} rank(s), no collective"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc("pmc_tb.json", markets=M),
+                     "kernel": "tiebreak_wave_kernel", "bytes_per_launch": bytes_step, "avg_launch_ms": per * 1e3},
+        "cpu_baseline": cpu_line,
+        "parity_vs_oracle": parity,
+    }
+
+
+# ---------------------------------------------------------------------------------------
+def c3_shards(args):
+    """8-GPU C3 strong scaling predicted on one GPU (``bench.py --config c3 --shard all/N``):
+    every rank's market shard of make_c3(world=N, rank=R) (sharding.shard_markets) is
+    timed in turn in this one process, no process group, with the bench's own loop, then
+    the full batch.  Predicted efficiency = t_full / (N * max_R t_R): a rank's step on its
+    own GPU is its shard alone, and the step ends with the slowest rank."""
+    from bayesian_engine import _native as N
+    from bayesian_engine import batch
+    import copy
+
+    spec = args.shard.split("/")
+    world = int(spec[1])
+    ranks = range(world) if spec[0] == "all" else [int(spec[0])]
+    dev = torch.device("cuda", torch.cuda.current_device())
+    mode = args.mode or "fast"
+    a2 = copy.copy(args)
+
+    def time_one(w, r):
+        M, off, sid, prob, (rel_h, conf_h, present) = make_c3(w, r)
+        T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+        table = batch.SourceTable.from_arrays(T(rel_h), T(conf_h), T(present))
+        d_off, d_sid, d_prob = T(off), T(sid), T(prob)
+        plan = batch.Plan.build(off, dev)
+        res = batch._alloc(len(off) - 1, int(off[-1]), dev, True, True)
+
+        def step():
+            batch.consensus(d_off, d_sid, d_prob, table, plan=plan, mode=mode, out=res)
+
+        wall, per = _timed(step, a2, 1, torch.cuda.current_stream(dev))
+        N.check_faults(dev, f"c3 shard {r}/{w}")
+        lens = np.diff(off)
+        bins = np.searchsorted([8, 16, 32, 64, 128, 256, 512, 1024, 2048, 4096], lens, side="left")
+        out = {"rank": r, "markets": int(len(lens)), "signals": int(off[-1]), "kernel_ms": per * 1e3,
+               "wall_ms": wall / a2.steps * 1e3, "signals_per_bin": np.bincount(bins, weights=lens,
+                                                                              minlength=11).astype(int).tolist()}
+        del table, d_off, d_sid, d_prob, plan, res
+        torch.cuda.empty_cache()
+        return out
+
+    import sys
+    shards = []
+    for r in ranks:
+        shards.append(time_one(world, r))
+        print(f"[c3 shards] {r}/{world}: {shards[-1]['kernel_ms']:.4f} ms", file=sys.stderr, flush=True)
+    full = time_one(1, 0)
+    ms = [s["kernel_ms"] for s in shards]
+    out = {"metric": "c3 per-shard step time (predicted strong scaling)", "mode": mode, "world": world,
+           "shards": shards, "full_batch": full,
+           "max_ms": max(ms), "mean_ms": float(np.mean(ms)), "max_over_mean": max(ms) / float(np.mean(ms)),
+           "predicted_efficiency": full["kernel_ms"] / (world * max(ms)) if spec[0] == "all" else None,
+           "split": "sharding.shard_markets (equal signal counts)"}
+    return out

@@ -182,3 +182,24 @@ def test_cli_config1_matches_reference_stdout():
                            env=env, timeout=300)
     assert p.returncode == case["rc"] == 0
     assert p.stdout == case["stdout"]
+
+
+def test_glibc_pow2_restatement_matches_libm(tmp_path):
+    """csrc/glibc_pow.hpp restates this libm's pow(x, 2.0) (the tie-break variance's
+    `(c - mean) ** 2`, tiebreak.py:110) and pow(2.0, y) (the decay factor, decay.py:58) bit
+    for bit: 4M inputs each incl. exact-midpoint squares, subnormals, huge and underflowing
+    values, decay exponents from float and integer-microsecond elapsed times
+    (tools/pow2_check.cpp)."""
+    import subprocess
+    exe = str(tmp_path / "pow2_check")
+    subprocess.run(["g++", "-O2", "-ffp-contract=off", "-DBCE_POW_HOST_TEST", "-w",
+                    "-I", os.path.join(ROOT, "bayesian-consensus-engine_amd", "csrc"),
+                    os.path.join(ROOT, "tools", "pow2_check.cpp"), "-o", exe, "-lm"], check=True)
+    out = subprocess.run([exe, "1000000"], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout
+    f = {t.split("=")[0]: int(t.split("=")[1]) for t in out.stdout.split()}
+    assert f["tested"] > 3_900_000 and f["mismatches"] == 0
+    assert f["d_mul_differs"] > 1000  # d*d alone would not do: libm's pow is not correctly rounded
+    # pow(2.0, y) of the decay factor (decay.py:58) too: bit-exact where exp2 is not
+    assert f["pow2_tested"] > 3_900_000 and f["pow2_mismatches"] == 0
+    assert f["exp2_differs"] > 100

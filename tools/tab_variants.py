@@ -1,18 +1,19 @@
 #!/usr/bin/env python3
-"""Experiment harness (not product code): build variants of libbce_hip.so with compile-time
-switches of the LDS-table kernel (consensus_tab.hip) and time them on the config-2 workload.
+"""Experiment harness (not product code): build variants of libbce_hip.so as SOURCE PATCHES of
+csrc/ (the product source carries no experiment switches) and time them on the config-2
+workload.
 
   python tools/tab_variants.py build [names...]     # here (hipcc cross-compiles)
   python tools/tab_variants.py run [--rounds 3]      # on the GPU box: one process per variant
                                                      # and round, interleaved; JSON lines out
 
-A variant named *prof* is built with -DBCE_TAB_PROF=1 and also reports the per-phase cycle
-split of the kernel's waves (s_memtime deltas summed over waves, per tile).
+A variant is a list of (file, old text, new text) replacements applied to a copy of csrc/;
+a replacement whose old text is missing fails the build (the patch went stale).
 """
 import argparse
-import ctypes as C
 import json
 import os
+import shutil
 import subprocess
 import sys
 import time
@@ -23,52 +24,60 @@ OUT = os.path.join(ROOT, "tools", "ablate_build")
 SRCS = ["capi.hip", "consensus.hip", "consensus_tab.hip", "consensus_wide.hip", "elementwise.hip", "tiebreak.hip",
         "stats.hip", "aggregate.hip"]
 
+_XPOSE_NEW = """  for (int i = 0; i < N; ++i)
+    if (!(i & 4)) bfly_r8(r[i], r[i | 4], lane);
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+    if (!(i & 8)) bfly_pl16(r[i], r[i | 8]);
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+    if (!(i & 16)) bfly_pl32(r[i], r[i | 16]);
+}"""
+_XPOSE_OLD = """  for (int i = 0; i < N; ++i)
+    if (!(i & 16)) bfly_pl32(r[i], r[i | 16]);
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+    if (!(i & 8)) bfly_pl16(r[i], r[i | 8]);
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+    if (!(i & 4)) bfly_r8(r[i], r[i | 4], lane);
+}"""
+
 VARIANTS = {
-    "base": [],  # the product defaults (8 waves, BCE_TAB_NT=3, BCE_EW_NT=2)
-    "w4": ["-DBCE_TAB_WAVES=4"],
-    "w8": ["-DBCE_TAB_WAVES=8"],
-    "w4_prof": ["-DBCE_TAB_WAVES=4", "-DBCE_TAB_PROF=1"],
-    "w8_prof": ["-DBCE_TAB_WAVES=8", "-DBCE_TAB_PROF=1"],
-    "p64": ["-DBCE_TAB_PIECE=64"],
-    "p64_prof": ["-DBCE_TAB_PIECE=64", "-DBCE_TAB_PROF=1"],
-    "nt1": ["-DBCE_TAB_NT=1"],  # nontemporal signal loads
-    "nt2": ["-DBCE_TAB_NT=2"],  # nontemporal per-unique stores
-    "nt3": ["-DBCE_TAB_NT=3"],
-    "nt7": ["-DBCE_TAB_NT=7"],
-    "nt3_w8": ["-DBCE_TAB_NT=3", "-DBCE_TAB_WAVES=8"],
-    "nt3_p64": ["-DBCE_TAB_NT=3", "-DBCE_TAB_PIECE=64"],
-    "nt3_prof": ["-DBCE_TAB_NT=3", "-DBCE_TAB_PROF=1"],
-    "base_prof": ["-DBCE_TAB_PROF=1"],
-    "map0": ["-DBCE_TAB_MAP=0"],
-    "prio0": ["-DBCE_TAB_PRIO=0"],
-    "plx": ["-DBCE_TAB_PLX=1"],
-    "xord_old": ["-DBCE_TAB_XORD_OLD=1"],
-    "ewg16": ["-DBCE_EW_GRID_CAP=16"],
-    "agg8": ["-DBCE_AGG_CAP=8"],  # f4: 8 workgroups per CU looping over groups (bench --config agg)  # elementwise kernels: 16 workgroups per CU (bench --config c4 / ns)
-    "ew1": ["-DBCE_EW_NT=1"],  # config-4 replay_step variants (bench.py --config c4)
-    "ew2": ["-DBCE_EW_NT=2"],
-    "ew3": ["-DBCE_EW_NT=3"],
-    "ew6": ["-DBCE_EW_NT=6"],
-    "nt7_w8": ["-DBCE_TAB_NT=7", "-DBCE_TAB_WAVES=8"],
-    "nt3_w8_r4": ["-DBCE_TAB_NT=3", "-DBCE_TAB_WAVES=8", "-DBCE_TAB_RING=4"],
-    "nt3_w8_r6": ["-DBCE_TAB_NT=3", "-DBCE_TAB_WAVES=8", "-DBCE_TAB_RING=6"],
-    "wide_nt": ["-DBCE_WIDE_AUX=2"],  # config-3 wide kernel: nontemporal sid/prob buffer loads
+    "base": [],  # the product source as is
+    # round-2 order of the transposes (row_ror:8 first): fewer spills, measured slower
+    "xord_r8first": [("consensus_tab.hip", _XPOSE_OLD, _XPOSE_NEW)],
+    "w4": [("consensus_tab.hip", "constexpr int kTabWaves = 8;", "constexpr int kTabWaves = 4;")],
+    "prio0": [("consensus_tab.hip", "__builtin_amdgcn_s_setprio(", "(void)(")],
 }
-PHASES = ["load+xpose", "valid+sort", "walk", "per_market", "compaction", "per_unique_stores"]
+
+
+def _patched_src(name):
+    d = os.path.join(OUT, name, "src")
+    if os.path.isdir(d):
+        shutil.rmtree(d)
+    shutil.copytree(CSRC, d)
+    for fn, old, new in VARIANTS[name]:
+        path = os.path.join(d, fn)
+        text = open(path).read()
+        if old not in text:
+            raise SystemExit(f"variant {name}: patch for {fn} does not apply (stale)")
+        with open(path, "w") as f:
+            f.write(text.replace(old, new))
+    return d
 
 
 def build(names):
     procs = []
     for name in names:
         d = os.path.join(OUT, name)
-        os.makedirs(d, exist_ok=True)
+        src = _patched_src(name)
         objs = []
-        for src in SRCS:
-            o = os.path.join(d, src.replace(".hip", ".o"))
+        for fn in SRCS:
+            o = os.path.join(d, fn.replace(".hip", ".o"))
             objs.append(o)
             cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
-                   "-fno-fast-math", "-munsafe-fp-atomics", "-w", *VARIANTS[name], "-c", os.path.join(CSRC, src),
-                   "-o", o]
+                   "-fno-fast-math", "-munsafe-fp-atomics", "-w", "-I", src, "-c", os.path.join(src, fn), "-o", o]
             procs.append((name, subprocess.Popen(cmd)))
         for _, p in procs:
             if p.wait() != 0:
@@ -97,11 +106,6 @@ def one(name, reps):
     for _ in range(300):  # clock ramp
         batch.consensus(*d, table, max_len=L, out=res)
     torch.cuda.synchronize()
-    lib = N.lib()
-    prof = hasattr(lib, "bce_tab_prof_read")
-    buf = (C.c_ulonglong * 8)()
-    if prof:
-        lib.bce_tab_prof_read(buf)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
     for e0, e1 in ev:
         e0.record()
@@ -110,13 +114,6 @@ def one(name, reps):
     torch.cuda.synchronize()
     ms = sorted(a.elapsed_time(b) for a, b in ev)
     out = {"variant": name, "median_ms": ms[len(ms) // 2], "min_ms": ms[0]}
-    if prof:
-        lib.bce_tab_prof_read(buf)
-        v = list(buf)[:6]
-        tiles = (M + 63) // 64
-        tot = sum(v)
-        out["phases_cyc_per_tile"] = {k: round(x / reps / tiles) for k, x in zip(PHASES, v)}
-        out["phases_pct"] = {k: round(100 * x / max(tot, 1), 1) for k, x in zip(PHASES, v)}
     if os.environ.get("TAB_NOCHECK") is None:
         N.check_faults()
     print(json.dumps(out), flush=True)
