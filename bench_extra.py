@@ -569,6 +569,9 @@ def _ns(args, world, rank, barrier, max_over, sum_over):
                                         N.ptr(code), C.c_void_p(st.cuda_stream)), "bce_namespace_resolve")
 
     wall, per = _timed(step, args, world, st, barrier, max_over)
+    N.check_faults(dev, "ns timed steps")
+    cpu_line, parity = (_cpu_ns(scopes, relconf, code, now_us, args) if rank == 0 and world == 1
+                        else (None, None))
     # per source: 3 has bytes + the chosen scope's rel/conf/t (24 B, non-cold only) +
     # relconf 16 B + scope code 1 B + 1/8 B present bit
     noncold = float((code != 3).float().mean().item())
@@ -583,9 +586,10 @@ def _ns(args, world, rank, barrier, max_over, sum_over):
         "config": {"workload": f"ns: {S} sources x 3 scopes per rank, decay on, mark_cold",
                    "noncold_fraction": noncold, "parallelism": f"sources sharded over {world} rank(s), no collective"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "namespace_resolve_kernel",
-                     "bytes_per_launch": bps * S, "avg_launch_ms": per * 1e3},
-        "cpu_baseline": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc("pmc_ns.json", sources=S),
+                     "kernel": "namespace_resolve_kernel", "bytes_per_launch": bps * S, "avg_launch_ms": per * 1e3},
+        "cpu_baseline": cpu_line,
+        "parity_vs_oracle": parity,
     }
 
 
@@ -614,6 +618,11 @@ def _agg(args, world, rank, barrier, max_over, sum_over):
 
     wall, per = _timed(lambda: launch(False), args, world, st, barrier, max_over)
     _, per_med = _timed(lambda: launch(True), args, world, st, barrier, max_over)
+    cpu_line, parity = (_cpu_agg(goff, members, cons, conf, has, (wavg, med, maj, mc, nin), args)
+                        if rank == 0 and world == 1 else (None, None))
+    # per-group latency chain (the kernel is not HBM-bound): one workgroup
+    # holds a group from its first index load to its last ordered sum
+    groups_per_wave_slot = G / torch.cuda.get_device_properties(dev).multi_processor_count
     bpm = 8 + 1 + 16  # member index, has byte, consensus + confidence
     achieved = bpm * G * K / per / 1e9
     tot = sum_over(float(G * K * args.steps), world)
@@ -626,9 +635,15 @@ def _agg(args, world, rank, barrier, max_over, sum_over):
                                f"weighted_average+majority+confidence {per * 1e3:.4f} ms, +median {per_med * 1e3:.4f} ms",
                    "parallelism": f"groups sharded over {world} rank(s), no collective"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "aggregate_kernel",
-                     "bytes_per_launch": bpm * G * K, "avg_launch_ms": per * 1e3},
-        "cpu_baseline": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc("pmc_agg.json", groups=G),
+                     "kernel": "aggregate_kernel", "bytes_per_launch": bpm * G * K, "avg_launch_ms": per * 1e3,
+                     "latency": {"note": "latency-chain bound: per group, index loads -> gathers -> "
+                                         "compaction -> three ordered sums of ~800 dependent fp64 adds",
+                                 "groups_per_cu": groups_per_wave_slot,
+                                 "us_per_group_per_cu": per * 1e6 / groups_per_wave_slot,
+                                 "dependent_adds_per_group": int(3 * 0.8 * K)}},
+        "cpu_baseline": cpu_line,
+        "parity_vs_oracle": parity,
     }
 
 
@@ -790,3 +805,89 @@ def c3_shards(args):
            "predicted_efficiency": full["kernel_ms"] / (world * max(ms)) if spec[0] == "all" else None,
            "split": "sharding.shard_markets (equal signal counts)"}
     return out
+
+
+def _cpu_ns(scopes, relconf, code, now_us, args, S_sample=2_000_000):
+    """orc_namespace_resolve on host threads over the first S_sample sources of the three
+    scopes (same per-source work as the kernel), plus parity of the kernel's table and scope
+    codes on that sample.  Returns (cpu_baseline, parity) or (None, None)."""
+    if args.no_cpu_baseline:
+        return None, None
+    import sys
+    from concurrent.futures import ThreadPoolExecutor
+
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as orc
+
+    n = min(S_sample, int(relconf.shape[0]))
+    host = [tuple(x[:n].cpu().numpy() for x in (sc.rel, sc.conf, sc.t_us, sc.has)) for sc in scopes]
+    T = _threads()
+    cuts = np.linspace(0, n, T + 1).astype(np.int64)
+
+    def part(i):
+        a, b = int(cuts[i]), int(cuts[i + 1])
+        return orc.namespace_resolve([tuple(x[a:b] for x in sc) for sc in host], True, now_us)
+
+    t0, reps, first = time.perf_counter(), 0, None
+    with ThreadPoolExecutor(T) as ex:
+        while True:
+            parts = list(ex.map(part, range(T)))
+            first = first or parts
+            reps += 1
+            dt = time.perf_counter() - t0
+            if dt >= args.cpu_seconds:
+                break
+    rel_o = np.concatenate([p[0] for p in first])
+    conf_o = np.concatenate([p[1] for p in first])
+    scope_o = np.concatenate([p[2] for p in first])
+    rc = relconf[:n].cpu().numpy()
+    ok = {"rel": bool(np.array_equal(rc[:, 0], rel_o)), "conf": bool(np.array_equal(rc[:, 1], conf_o)),
+          "scope": bool(np.array_equal(code[:n].cpu().numpy(), scope_o))}
+    return ({"value": n * reps / dt, "unit": "sources/s", "cores": T, "kind": "port", "label": "restatement",
+             "sample": f"the first {n} sources of the 3 scopes (decay on), orc_namespace_resolve on {T} threads, "
+                       f"{reps} passes in {dt:.2f} s"},
+            {"all_equal": all(ok.values()), "outputs": ok, "sample": f"first {n} sources, bit for bit"})
+
+
+def _cpu_agg(goff, members, cons, conf, has, outs, args):
+    """orc_aggregate_groups on host threads over every group (same work as the kernel, the
+    median included), plus full-size parity of the kernel's outputs."""
+    if args.no_cpu_baseline:
+        return None, None
+    import sys
+    from concurrent.futures import ThreadPoolExecutor
+
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as orc
+
+    go, mem = goff.cpu().numpy(), members.cpu().numpy()
+    c, f, h = cons.cpu().numpy(), conf.cpu().numpy(), has.cpu().numpy()
+    G = len(go) - 1
+    T = _threads()
+    cuts = np.linspace(0, G, T + 1).astype(np.int64)
+
+    def part(i):
+        g0, g1 = int(cuts[i]), int(cuts[i + 1])
+        return orc.aggregate_groups(go[g0:g1 + 1] - go[g0], mem[go[g0]:go[g1]], c, f, h)
+
+    t0, reps, first = time.perf_counter(), 0, None
+    with ThreadPoolExecutor(T) as ex:
+        while True:
+            parts = list(ex.map(part, range(T)))
+            first = first or parts
+            reps += 1
+            dt = time.perf_counter() - t0
+            if dt >= args.cpu_seconds:
+                break
+    exp = {k: np.concatenate([p[k] for p in first]) for k in ("wavg", "median", "majority", "mean_conf", "n_included")}
+    wavg, med, maj, mc, nin = (x.cpu().numpy() for x in outs)
+    ok = {"wavg": bool(np.array_equal(wavg, exp["wavg"], equal_nan=True)),
+          "median": bool(np.array_equal(med, exp["median"], equal_nan=True)),
+          "majority": bool(np.array_equal(maj, exp["majority"], equal_nan=True)),
+          "mean_conf": bool(np.array_equal(mc, exp["mean_conf"], equal_nan=True)),
+          "n_included": bool(np.array_equal(nin, exp["n_included"]))}
+    n = int(go[-1])
+    return ({"value": n * reps / dt, "unit": "members/s", "cores": T, "kind": "port", "label": "restatement",
+             "sample": f"all {G} groups ({n} members, median included), orc_aggregate_groups on {T} threads, "
+                       f"{reps} passes in {dt:.2f} s"},
+            {"all_equal": all(ok.values()), "outputs": ok, "sample": "every group, bit for bit"})

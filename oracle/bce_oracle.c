@@ -99,11 +99,15 @@ int orc_consensus_csr(const int64_t* offsets, int64_t n_markets, const int32_t* 
     return 0;
 }
 
+/* libm pow, never folded or rewritten by the compiler (pow(x, 2.0) -> x*x is not what CPython
+ * computes) */
+static double (*volatile libm_pow)(double, double) = pow;
+
 /* decay.py:52-58 */
 double orc_decay_factor(double elapsed_days, double half_life_days) {
     if (elapsed_days <= 0) return 1.0;
     const double exponent = -elapsed_days / half_life_days;
-    return pow(2.0, exponent);
+    return libm_pow(2.0, exponent);
 }
 
 /* decay.py:90-100 */
@@ -225,12 +229,15 @@ int orc_tiebreak_csr(const int64_t* offsets, int64_t n_markets, const double* pr
             g[j].confsum += conf[a + i];
             g[j].count += 1;
         }
-        /* confidence variance, tiebreak.py:104-106 */
+        /* confidence variance, tiebreak.py:108-110 */
         double csum = 0.0;
         for (int64_t i = 0; i < n; ++i) csum += conf[a + i];
         const double mean = csum / (double)n;
         double vs = 0.0;
-        for (int64_t i = 0; i < n; ++i) vs += pow(conf[a + i] - mean, 2.0);
+        /* `(c - mean_conf) ** 2` is CPython float_pow -> libm pow, which is not correctly
+         * rounded (it differs from d*d for ~0.08% of d); GCC folds pow(x, 2.0) into x*x, so
+         * the call goes through a volatile pointer to stay a libm call */
+        for (int64_t i = 0; i < n; ++i) vs += libm_pow(conf[a + i] - mean, 2.0);
         variance[m] = vs / (double)n;
         /* lexicographic argmax of (density, max_rel, -key); stable => first wins ties */
         int64_t best = 0;

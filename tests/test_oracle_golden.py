@@ -180,3 +180,27 @@ def test_c5_reestimate():
     assert np.array_equal(cons, g["consensus"])
     assert np.array_equal(agree, g["agree"])
     assert np.array_equal(w, g["weights"][-1])
+
+
+def test_oracle_tiebreak_variance_is_cpython_pow():
+    """tiebreak.py:108-110 evaluates `sum((c - mean_conf) ** 2 for c in ...) / n` with
+    CPython's float ** (libm pow, not d*d).  The oracle must reproduce it bit for bit on
+    markets whose confidences sit on a 2^-28 grid, where pow and d*d disagree most often
+    (GCC folds a literal pow(x, 2.0) into x*x, so the oracle calls libm through a pointer)."""
+    rng = np.random.default_rng(110)
+    M = 4000
+    lens = rng.integers(2, 65, M)
+    off = np.zeros(M + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    n = int(off[-1])
+    conf = rng.integers(0, 1 << 28, n) * 2.0 ** -28
+    pred = rng.integers(0, 9, n) / 8.0
+    e = orc.tiebreak_csr(off, pred, conf, rng.random(n), rng.random(n))
+    differs = 0
+    for m in range(M):
+        c = conf[off[m]:off[m + 1]].tolist()
+        mean_conf = sum(c) / len(c)
+        v = sum((x - mean_conf) ** 2 for x in c) / len(c)  # the reference's expression
+        assert v == e["variance"][m], m
+        differs += v != sum((x - mean_conf) * (x - mean_conf) for x in c) / len(c)
+    assert differs > 5  # the case matters: d*d would have failed this test
