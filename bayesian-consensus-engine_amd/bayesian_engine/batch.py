@@ -345,11 +345,13 @@ def tiebreak(offsets: torch.Tensor, pred: torch.Tensor, conf: torch.Tensor, weig
         N.check(L.bce_tiebreak_csr(N.ptr(offsets), M, N.ptr(None), 0, *ins, int(max(int(lens.max(initial=1)), 1)),
                                    int(precision), *outs, st), "bce_tiebreak_csr")
         return r
-    short = np.nonzero(lens <= 64)[0].astype(np.int32)
-    if len(short):
-        sl = torch.from_numpy(short).to(dev)
-        N.check(L.bce_tiebreak_csr(N.ptr(offsets), M, N.ptr(sl), len(short), *ins, 64, int(precision), *outs, st),
-                "bce_tiebreak_csr")
+    # n <= 32: the lane-per-market kernel; 33..64: wave per market; longer: workgroup per market
+    for lo, hi in ((0, 32), (33, 64)):
+        short = np.nonzero((lens >= lo) & (lens <= hi))[0].astype(np.int32)
+        if len(short):
+            sl = torch.from_numpy(short).to(dev)
+            N.check(L.bce_tiebreak_csr(N.ptr(offsets), M, N.ptr(sl), len(short), *ins, hi, int(precision), *outs,
+                                       st), "bce_tiebreak_csr")
     ll = torch.from_numpy(long_.astype(np.int32)).to(dev)
     N.check(L.bce_tiebreak_csr_long(N.ptr(offsets), M, N.ptr(ll), len(long_), int(precision), *ins,
                                     int(lens[long_].max()), *outs, st), "bce_tiebreak_csr_long")

@@ -1,7 +1,8 @@
 // tiebreak.hip -- DeterministicTieBreaker.resolve (tiebreak.py:73-152) per CSR market.
 //
-// One wave per market (n <= 64 agents; lane = agent), or one 256-thread workgroup per
-// market with the agents staged in LDS (64 < n <= 4096).  Grouping key = CPython
+// One lane per market (n <= 32 agents, tiebreak_lpm_kernel), one wave per market
+// (n <= 64; lane = agent), or one 256-thread workgroup per market with the agents staged
+// in LDS (64 < n <= 4096) or in a global scratch slice (any length).  Grouping key = CPython
 // round(prediction, 6) (tiebreak.py:54) restated exactly (bce::py_round_nd).  A group's
 // leader is its first-seen member, so groups come out in dict insertion order for free.
 // Group sums (weight, confidence) run in input order, max reliability keeps the first
@@ -10,6 +11,7 @@
 // reduction order selects the same winner.
 #include "bce_device.hpp"
 #include "bce_internal.hpp"
+#include "consensus_common.hpp"
 #include "glibc_pow.hpp"
 
 #pragma clang fp contract(off)
@@ -166,6 +168,144 @@ __global__ __launch_bounds__(256) void tiebreak_wave_kernel(TbArgs a, const int3
       if (a.g_density) a.g_density[g] = dens;
       if (a.g_avgconf) a.g_avgconf[g] = avgc;
       if (a.g_maxrel) a.g_maxrel[g] = mx;
+    }
+  }
+}
+
+// n <= 32, lane = market (64 markets per wave): every per-market step runs in one lane's
+// registers, so none of the wave kernel's serial readlane loops exist and a wave's
+// instructions serve 64 markets at once.  Per lane:
+//   1. variance (tiebreak.py:108-110): confidences in input order -> mean, then the squares
+//      (libm pow restated, glibc_pow.hpp) summed in input order;
+//   2. keys round(pred, precision) (tiebreak.py:54) and each agent's group ordinal in
+//      first-seen (dict insertion) order: O(n^2) key compares, == semantics (-0.0 == 0.0,
+//      NaN never equal);
+//   3. 32-bit keys (ordinal << 5 | agent) sorted with the odd-even merge network: every
+//      group becomes a run, groups in first-seen order, members in input order;
+//   4. walk: weight / confidence / reliability gathered per member, the group's sums run in
+//      input order from +0.0 (builtin sum from int 0), builtin max keeps the first maximum;
+//      at a run's end the group's outputs are stored and the winner (lexicographic max of
+//      (density, max_rel, -key), tiebreak.py:113-117) and the top-two tie flag
+//      (tiebreak.py:123-133) are updated.
+constexpr int kTbLpmMax = 32;
+
+__global__ __launch_bounds__(256) void tiebreak_lpm_kernel(TbArgs a, const int32_t* list, int64_t n_list,
+                                                           int* fault) {
+  const int lane = lane_id();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t tile = wave; tile * 64 < n_list; tile += nwaves) {
+    const int64_t li = tile * 64 + lane;
+    const bool has = li < n_list;
+    const int64_t m = has ? (list ? (int64_t)list[li] : li) : 0;
+    const int64_t off = has ? a.offsets[m] : 0;
+    int n = has ? (int)(a.offsets[m + 1] - off) : 0;
+    if (ballot(n > kTbLpmMax || n < 0)) {
+      raise_fault(fault, kFaultTooLong);
+      if (n > kTbLpmMax || n < 0) n = 0;
+    }
+    if (!ballot(n > 0)) {
+      if (has) {
+        a.winner[m] = 0.0; a.label[m] = -1; a.n_groups[m] = -1; a.variance[m] = 0.0;
+      }
+      continue;
+    }
+    // every lane reads inside its own row (positions past n re-read the last agent); a lane
+    // with an empty market reads row 0 of a market that has agents (masked later)
+    const int last = n > 0 ? n - 1 : 0;
+    const int fl = __builtin_ctzll(ballot(n > 0));
+    const int64_t offl = ((int64_t)__builtin_amdgcn_readlane((int)(off >> 32), fl) << 32) |
+                         (uint32_t)__builtin_amdgcn_readlane((int)off, fl);
+    const int64_t base = n > 0 ? off : offl;
+    const double nd = (double)(n > 0 ? n : 1);
+
+    // ---- 1. confidence variance (input order) ---------------------------------------
+    double variance;
+    {
+      double c[kTbLpmMax];
+#pragma unroll
+      for (int t = 0; t < kTbLpmMax; ++t) c[t] = a.conf[base + min(t, last)];
+      double cs = 0.0;
+#pragma unroll
+      for (int t = 0; t < kTbLpmMax; ++t) cs += (t < n) ? c[t] : 0.0;
+      const double mean = cs / nd;
+      double vs = 0.0;
+#pragma unroll
+      for (int t = 0; t < kTbLpmMax; ++t) vs += (t < n) ? bce_pow::pow2(c[t] - mean) : 0.0;
+      variance = vs / nd;
+    }
+
+    // ---- 2. keys and group ordinals (first-seen order) --------------------------------
+    unsigned u[kTbLpmMax];
+    int ng = 0;
+    {
+      double k[kTbLpmMax];
+#pragma unroll
+      for (int t = 0; t < kTbLpmMax; ++t) k[t] = tb_round(a.pred[base + min(t, last)], a);
+      int go[kTbLpmMax];
+#pragma unroll
+      for (int t = 0; t < kTbLpmMax; ++t) {
+        int g = -1;
+#pragma unroll
+        for (int s2 = 0; s2 < t; ++s2) g = key_eq(k[s2], k[t]) ? go[s2] : g;  // earlier equal key: its group
+        const bool fresh = (t < n) && g < 0;
+        go[t] = fresh ? ng : g;
+        ng += fresh ? 1 : 0;
+        if (a.g_of && t < n) a.g_of[off + t] = go[t];
+        u[t] = (t < n) ? (((unsigned)go[t] << 5) | (unsigned)t) : 0xFFFFFFFFu;
+      }
+    }
+    oem_sort<kTbLpmMax>(u);
+
+    // ---- 3. walk the groups: sums in input order, outputs, winner ------------------------
+    double tot = 0.0, cs = 0.0, mx = 0.0, bd = 0.0, bm = 0.0, bk = 0.0;
+    int cnt = 0, lead = 0;
+    bool tie = false;
+#pragma unroll
+    for (int p = 0; p < kTbLpmMax; ++p) {
+      if (p < n) {
+        const unsigned v = u[p];
+        const int t = (int)(v & 31u);
+        const unsigned g = v >> 5;
+        const bool start = (p == 0) || (g != (u[p > 0 ? p - 1 : 0] >> 5));
+        const bool end = (p + 1 >= n) || (g != (u[p + 1 < kTbLpmMax ? p + 1 : p] >> 5));
+        const double w = a.weight[off + t], c = a.conf[off + t], r = a.rel[off + t];
+        tot = (start ? 0.0 : tot) + w;     // tiebreak.py:60, sum from int 0
+        cs = (start ? 0.0 : cs) + c;       // tiebreak.py:61
+        cnt = (start ? 0 : cnt) + 1;
+        mx = start ? r : ((r > mx) ? r : mx);  // tiebreak.py:62, first maximum kept
+        lead = start ? t : lead;
+        if (end) {
+          const double praw = a.pred[off + lead];
+          const double key = (n == 1) ? praw : tb_round(praw, a);  // single agent: raw (tiebreak.py:89-96)
+          const double dens = tot / (double)cnt, avgc = cs / (double)cnt;
+          const int64_t go_ = off + (int64_t)g;
+          if (a.g_key) a.g_key[go_] = key;
+          if (a.g_count) a.g_count[go_] = cnt;
+          if (a.g_density) a.g_density[go_] = dens;
+          if (a.g_avgconf) a.g_avgconf[go_] = avgc;
+          if (a.g_maxrel) a.g_maxrel[go_] = mx;
+          const bool same = (dens == bd) && (mx == bm);
+          if (g == 0 || tb_better(dens, mx, key, bd, bm, bk)) {
+            tie = (g != 0) && same;
+            bd = dens; bm = mx; bk = key;
+          } else {
+            tie = tie || same;
+          }
+        }
+      }
+    }
+    if (has) {
+      if (n == 0) {  // tiebreak.py:86-87 (ValueError)
+        a.winner[m] = 0.0; a.label[m] = -1; a.n_groups[m] = -1; a.variance[m] = 0.0;
+      } else {
+        a.winner[m] = bk;
+        a.label[m] = (n == 1) ? BCE_TB_SINGLE_AGENT
+                              : (ng == 1) ? BCE_TB_UNANIMOUS
+                                          : tie ? BCE_TB_PREDICTION_VALUE_SMALLEST : BCE_TB_WEIGHT_DENSITY;
+        a.n_groups[m] = ng;
+        a.variance[m] = (n == 1) ? 0.0 : variance;
+      }
     }
   }
 }
@@ -411,6 +551,17 @@ extern "C" int bce_tiebreak_csr(const int64_t* offsets, int64_t n_markets, const
   }
   TbArgs a{offsets, n_markets, pred, conf, weight, rel, winner, label, n_groups, variance,
            g_key, g_count, g_density, g_avgconf, g_maxrel, g_of, rs, rt, rmode};
+  if (max_len <= kTbLpmMax) {  // lane per market: 64 markets per wave, 4 waves per workgroup
+    const int64_t tiles = (nl + 63) / 64;
+    int64_t blocks = (tiles + 3) / 4;
+    const int per_cu = blocks_per_cu(reinterpret_cast<const void*>(&tiebreak_lpm_kernel), 256, 0, 4,
+                                     "tiebreak_lpm_kernel");
+    const int64_t cap = (int64_t)cu_count() * per_cu;
+    if (blocks > cap) blocks = cap;
+    hipLaunchKernelGGL(tiebreak_lpm_kernel, dim3((int)blocks), dim3(256), 0, as_stream(stream), a, market_list,
+                       nl, fault_word());
+    return check_launch("tiebreak_lpm_kernel");
+  }
   int64_t blocks = (nl + 3) / 4;
   const int64_t cap = (int64_t)cu_count() * 16;
   if (blocks > cap) blocks = cap;

@@ -53,10 +53,13 @@ VARIANTS = {
 
 
 def _patched_src(name):
-    d = os.path.join(OUT, name, "src")
-    if os.path.isdir(d):
-        shutil.rmtree(d)
+    # pkg/csrc + include side by side, as in the repo (csrc includes ../../include/bce.h)
+    top = os.path.join(OUT, name, "tree")
+    if os.path.isdir(top):
+        shutil.rmtree(top)
+    d = os.path.join(top, "pkg", "csrc")
     shutil.copytree(CSRC, d)
+    shutil.copytree(os.path.join(ROOT, "include"), os.path.join(top, "include"))
     for fn, old, new in VARIANTS[name]:
         path = os.path.join(d, fn)
         text = open(path).read()
