@@ -746,7 +746,7 @@ def _tb(args, world, rank, barrier, max_over, sum_over):
                    "parallelism": f"markets sharded over {world} rank(s), no collective"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc("pmc_tb.json", markets=M),
-                     "kernel": "tiebreak_wave_kernel", "bytes_per_launch": bytes_step, "avg_launch_ms": per * 1e3},
+                     "kernel": "tiebreak_lpm_kernel" if L <= 32 else "tiebreak_wave_kernel", "bytes_per_launch": bytes_step, "avg_launch_ms": per * 1e3},
         "cpu_baseline": cpu_line,
         "parity_vs_oracle": parity,
     }
