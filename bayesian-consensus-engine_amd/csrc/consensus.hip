@@ -838,8 +838,12 @@ void consensus_pipe_kernel(ConsArgs a) {
 
   const int lane = lane_id();
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int nwords = (a.n_sources + 31) >> 5;  // <= kBitsLds (launcher)
-  for (int i = threadIdx.x; i < nwords; i += 64 * (C + NL)) sBits[i] = a.pbits[i];
+  // present bits staged in LDS up to 16384 sources; larger tables read them from global
+  // memory (one 4-B gather per unique source, L2-resident: S/8 bytes)
+  const int nwords = (a.n_sources + 31) >> 5;
+  const bool bits_in_lds = nwords <= kBitsLds;
+  if (bits_in_lds)
+    for (int i = threadIdx.x; i < nwords; i += 64 * (C + NL)) sBits[i] = a.pbits[i];
   if (threadIdx.x < R) {
     sReady[threadIdx.x] = 0;
     sFree[threadIdx.x] = 0;
@@ -1223,8 +1227,9 @@ void consensus_pipe_kernel(ConsArgs a) {
             u1[b] = pk1[b] & ((1u << kPackSlot) - 1);
             w0[b] = iP[dP + r[b] + (int)((pk0[b] >> kPackSlot) & (G - 1))];
             w1[b] = (NPL == 2) ? iP[dP + r[b] + (int)((pk1[b] >> kPackSlot) & (G - 1))] : 0.0;
-            bw0[b] = sBits[min(u0[b], smax) >> 5];
-            bw1[b] = (NPL == 2) ? sBits[min(u1[b], smax) >> 5] : 0u;
+            const unsigned i0 = min(u0[b], smax) >> 5, i1 = min(u1[b], smax) >> 5;
+            bw0[b] = bits_in_lds ? sBits[i0] : a.pbits[i0];
+            bw1[b] = (NPL == 2) ? (bits_in_lds ? sBits[i1] : a.pbits[i1]) : 0u;
           }
           // materialise the batch here: left alone, loads used only under the store
           // branches are sunk into them and serialise again
@@ -1531,14 +1536,15 @@ int launch_flat(const ConsArgs& a, hipStream_t st) {
 
 // Markets with n <= 64 (a.list == NULL: contiguous CSR; else a planned market list).
 //   contiguous, 16 < n <= 32, S <= kTabMaxSources   consensus_tab32_kernel (table in LDS)
-//   contiguous, n <= 32, S <= 16384, all outputs     consensus_pipe_kernel<G> (loader + compute waves)
+//   ... S <= kTabHybMaxSources                       consensus_tab32_kernel<hybrid> (LDS rows + global rest)
+//   contiguous, n <= 32, S < 2^25, all outputs       consensus_pipe_kernel<G> (loader + compute waves)
 //   contiguous, n <= 32, otherwise                   consensus_flat_kernel<G>
 //   market list, n <= 32                             consensus_lpm_kernel<G> (lane per market)
 //   33 <= n <= 64                                    consensus_seg_kernel<64, 8>
 int launch_seg_for_len(int max_len, const ConsArgs& a, hipStream_t st) {
   if (a.list == nullptr && max_len <= 32) {
-    if (max_len > 16 && a.n_sources <= kTabMaxSources) return launch_tab32(a, st);
-    if (a.n_sources <= 32 * kBitsLds && a.n_signals >= 4 && a.usid && a.weight && a.nweight) {
+    if (max_len > 16 && a.n_sources <= kTabHybMaxSources) return launch_tab32(a, st);
+    if (a.n_sources < (1 << 25) && a.n_signals >= 4 && a.usid && a.weight && a.nweight) {
       if (max_len <= 8) return launch_pipe<8>(a, st);
       if (max_len <= 16) return launch_pipe<16>(a, st);
       return launch_pipe<32>(a, st);

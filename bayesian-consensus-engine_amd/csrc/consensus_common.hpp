@@ -32,6 +32,7 @@ struct ConsArgs {
   int64_t scratch_stride;  // elements (keys) per workgroup slice
   int* fault;         // device word: set to a kFault* code by a wave that gave up
   int spin_cap;       // bounded waits of the persistent pipe kernel (polls before giving up)
+  int32_t tab_rows;   // tab kernel, hybrid table: rows [0, tab_rows) staged in LDS, the rest read from relconf
 };
 
 // Device fault codes (bce_fault_check reports them).
@@ -147,6 +148,10 @@ int spin_cap();
 // LDS-table kernel (consensus_tab.hip): contiguous markets with n <= 32 and
 // n_sources <= kTabMaxSources.
 constexpr int kTabMaxSources = 10112;  // 16 B per source + the bitmask fit the 160 KiB LDS
+// Larger tables (up to kTabHybMaxSources): the first rows that fit beside the whole present
+// bitmask are staged in LDS, the rest are gathered from the global table (hybrid mode).
+constexpr int kTabHybMaxSources = 1 << 18;
+constexpr int kTabLdsBytes = 160 * 1024;
 int launch_tab32(const ConsArgs& a, hipStream_t st);
 
 // Register-sort kernel (consensus_wide.hip) for 64 < n <= 4096: ib = log2 of the key's

@@ -46,6 +46,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "consensus_common.hpp"
 
 #pragma clang fp contract(off)
@@ -160,23 +162,27 @@ __device__ __forceinline__ double dbl(uint32_t lo, uint32_t hi) {
 __device__ __forceinline__ uint32_t lo32(double x) { return (uint32_t)__double_as_longlong(x); }
 __device__ __forceinline__ uint32_t hi32(double x) { return (uint32_t)((uint64_t)__double_as_longlong(x) >> 32); }
 
+// HYB: the table is larger than the LDS; rows [0, a.tab_rows) are staged (with the whole
+// present bitmask) and the walk gathers the others from the global relconf table.
+template <bool HYB>
 __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char tab_smem[];
   const int S = a.n_sources > 0 ? a.n_sources : 1;
   const int nwords = (S + 31) >> 5;
+  const int rows = HYB ? a.tab_rows : S;  // rows staged in LDS
   double2* const sT = reinterpret_cast<double2*>(tab_smem);
-  uint32_t* const sB = reinterpret_cast<uint32_t*>(tab_smem + 16 * (size_t)S);
+  uint32_t* const sB = reinterpret_cast<uint32_t*>(tab_smem + 16 * (size_t)rows);
   // ---- stage the table once per workgroup ----------------------------------------------
   if (a.n_sources > 0) {
     int i = threadIdx.x;
-    for (; i + 3 * 64 * kTabWaves < S; i += 4 * 64 * kTabWaves) {
+    for (; i + 3 * 64 * kTabWaves < rows; i += 4 * 64 * kTabWaves) {
       double2 v[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) v[q] = a.relconf[i + q * 64 * kTabWaves];
 #pragma unroll
       for (int q = 0; q < 4; ++q) sT[i + q * 64 * kTabWaves] = v[q];
     }
-    for (; i < S; i += 64 * kTabWaves) sT[i] = a.relconf[i];
+    for (; i < rows; i += 64 * kTabWaves) sT[i] = a.relconf[i];
     for (int j = threadIdx.x; j < nwords; j += 64 * kTabWaves) sB[j] = a.pbits[j];
   } else if (threadIdx.x == 0) {
     sT[0] = make_double2(0.5, 0.25);  // DEFAULT_RELIABILITY / _CONFIDENCE (config.py:17-18)
@@ -361,10 +367,17 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
     __builtin_amdgcn_s_setprio(1);
     double2 ring[kTabRing];
     uint32_t rbits[kTabRing];
+    // one table row: LDS, or (hybrid, rows past the staged ones) the global table
+    auto row = [&](unsigned ix) -> double2 {
+      if constexpr (HYB) {
+        if (ix >= (unsigned)rows) return a.relconf[ix];
+      }
+      return sT[ix];
+    };
 #pragma unroll
     for (int t = 0; t < kTabRing; ++t) {
       const unsigned ix = min(key[t] >> 5, smax);
-      ring[t] = sT[ix];
+      ring[t] = row(ix);
       rbits[t] = sB[ix >> 5];
     }
     double total = 0.0, ws = 0.0, cs = 0.0;
@@ -375,7 +388,7 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
       const uint32_t bw = rbits[t % kTabRing];
       if (t + kTabRing < 32) {
         const unsigned ix = min(key[t + kTabRing < 32 ? t + kTabRing : t] >> 5, smax);
-        ring[t % kTabRing] = sT[ix];
+        ring[t % kTabRing] = row(ix);
         rbits[t % kTabRing] = sB[ix >> 5];
       }
       // p[t] at a run's last position is the source's average (a single signal: p itself;
@@ -513,21 +526,29 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
 }  // namespace
 
 
-int launch_tab32(const ConsArgs& a, hipStream_t st) {
+template <bool HYB>
+int launch_tab32_t(ConsArgs a, hipStream_t st) {
   const int64_t tiles = (a.n_list + 63) / 64;
   if (tiles == 0) return BCE_OK;
   const int S = a.n_sources > 0 ? a.n_sources : 1;
-  const size_t lds = 16 * (size_t)S + 4 * (size_t)((S + 31) / 32);
-  const size_t cap_lds = 16 * (size_t)kTabMaxSources + 4 * (size_t)(kTabMaxSources / 32);
-  const int rc = ensure_dynamic_lds(reinterpret_cast<const void*>(&consensus_tab32_kernel), (int)cap_lds);
+  const size_t bits = 4 * (size_t)((S + 31) / 32);
+  // hybrid: as many rows as fit beside the whole bitmask (16-B aligned)
+  a.tab_rows = HYB ? (int)std::min<size_t>(((size_t)kTabLdsBytes - bits) / 16, (size_t)S) : S;
+  const size_t lds = 16 * (size_t)a.tab_rows + bits;
+  const void* fn = reinterpret_cast<const void*>(&consensus_tab32_kernel<HYB>);
+  const int rc = ensure_dynamic_lds(fn, kTabLdsBytes);
   if (rc) return rc;
-  const int per_cu = blocks_per_cu(reinterpret_cast<const void*>(&consensus_tab32_kernel), 64 * kTabWaves, lds, 1,
-                                   "consensus_tab32_kernel");
+  const int per_cu = blocks_per_cu(fn, 64 * kTabWaves, lds, 1, HYB ? "consensus_tab32_kernel<hybrid>"
+                                                                  : "consensus_tab32_kernel");
   const int64_t blocks = (tiles + kTabWaves - 1) / kTabWaves;
   const int64_t cap = (int64_t)cu_count() * per_cu;
   const int grid = (int)(blocks < cap ? blocks : cap);
-  hipLaunchKernelGGL(consensus_tab32_kernel, dim3(grid), dim3(64 * kTabWaves), lds, st, a);
+  hipLaunchKernelGGL((consensus_tab32_kernel<HYB>), dim3(grid), dim3(64 * kTabWaves), lds, st, a);
   return check_launch("consensus_tab32_kernel");
+}
+
+int launch_tab32(const ConsArgs& a, hipStream_t st) {
+  return (a.n_sources <= kTabMaxSources) ? launch_tab32_t<false>(a, st) : launch_tab32_t<true>(a, st);
 }
 
 }  // namespace bce

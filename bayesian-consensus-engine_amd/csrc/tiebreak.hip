@@ -174,24 +174,42 @@ __global__ __launch_bounds__(256) void tiebreak_wave_kernel(TbArgs a, const int3
 
 // n <= 32, lane = market (64 markets per wave): every per-market step runs in one lane's
 // registers, so none of the wave kernel's serial readlane loops exist and a wave's
-// instructions serve 64 markets at once.  Per lane:
-//   1. variance (tiebreak.py:108-110): confidences in input order -> mean, then the squares
-//      (libm pow restated, glibc_pow.hpp) summed in input order;
-//   2. keys round(pred, precision) (tiebreak.py:54) and each agent's group ordinal in
+// instructions serve 64 markets at once.
+//
+// Data movement (STAGED, contiguous markets): a wave's 64 markets are one contiguous CSR
+// range of <= 2048 agents, so each input array is read ONCE with coalesced 16-B loads into
+// a wave-private LDS buffer (one pad double per 32, so lanes reading their own rows hit
+// distinct bank pairs) and the lanes read their rows from there.  (Per-lane global reads of
+// the rows -- the !STAGED path, kept for market lists -- touch 64 lines per instruction and
+// thrash L1/L2: 16.7 GB of HBM reads for the 1 GB the config-2 batch holds.)
+// Per lane:
+//   1. keys round(pred, precision) (tiebreak.py:54) and each agent's group ordinal in
 //      first-seen (dict insertion) order: O(n^2) key compares, == semantics (-0.0 == 0.0,
-//      NaN never equal);
-//   3. 32-bit keys (ordinal << 5 | agent) sorted with the odd-even merge network: every
-//      group becomes a run, groups in first-seen order, members in input order;
-//   4. walk: weight / confidence / reliability gathered per member, the group's sums run in
-//      input order from +0.0 (builtin sum from int 0), builtin max keeps the first maximum;
-//      at a run's end the group's outputs are stored and the winner (lexicographic max of
-//      (density, max_rel, -key), tiebreak.py:113-117) and the top-two tie flag
-//      (tiebreak.py:123-133) are updated.
+//      NaN never equal); keys (ordinal << 5 | agent) sorted by the odd-even merge network
+//      with the rounded key as payload: every group becomes a run, groups in first-seen
+//      order, members in input order;
+//   2. walk 1 (weight, reliability): the group's weight sum runs in input order from +0.0
+//      (builtin sum from int 0), builtin max keeps the first maximum; at a run's end the
+//      group's count / density / max reliability are stored and the winner (lexicographic
+//      max of (density, max_rel, -key), tiebreak.py:113-117) and the top-two tie flag
+//      (tiebreak.py:123-133) updated;
+//   3. confidences: the variance (tiebreak.py:108-110; mean, then the squares -- libm pow
+//      restated, glibc_pow.hpp -- summed in input order) and walk 2, the per-group
+//      confidence sums (tiebreak.py:61).
 constexpr int kTbLpmMax = 32;
+constexpr int kTbLpmWaves = 4;
+constexpr int kTbStage = 64 * kTbLpmMax + 64;  // doubles per buffer: a tile's agents + pads
 
-__global__ __launch_bounds__(256) void tiebreak_lpm_kernel(TbArgs a, const int32_t* list, int64_t n_list,
-                                                           int* fault) {
+__device__ __forceinline__ int tb_pad(int i) { return i + (i >> 5); }
+
+template <bool STAGED>
+__global__ __launch_bounds__(64 * kTbLpmWaves) void tiebreak_lpm_kernel(TbArgs a, const int32_t* list,
+                                                                         int64_t n_list, int* fault) {
+  __shared__ double sBuf[STAGED ? kTbLpmWaves : 1][2][STAGED ? kTbStage : 1];
   const int lane = lane_id();
+  const int wv = STAGED ? (int)(threadIdx.x >> 6) : 0;
+  double* const bufA = sBuf[wv][0];
+  double* const bufB = sBuf[wv][1];
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t tile = wave; tile * 64 < n_list; tile += nwaves) {
@@ -210,44 +228,55 @@ __global__ __launch_bounds__(256) void tiebreak_lpm_kernel(TbArgs a, const int32
       }
       continue;
     }
+    // STAGED: the tile's agents [B, E) (lane 0's market starts it, the last lane's ends it)
+    const int64_t B = ((int64_t)__builtin_amdgcn_readfirstlane((int)(off >> 32)) << 32) |
+                      (uint32_t)__builtin_amdgcn_readfirstlane((int)off);
+    const int last_lane = 63 - __builtin_clzll(ballot(has));
+    const int64_t endl = off + n;
+    const int64_t E = ((int64_t)__builtin_amdgcn_readlane((int)(endl >> 32), last_lane) << 32) |
+                      (uint32_t)__builtin_amdgcn_readlane((int)endl, last_lane);
+    const int cnt_tile = (int)(E - B);  // <= 64 * 32
+    const int lrow = (int)(off - B);    // this lane's row in the staged buffer
     // every lane reads inside its own row (positions past n re-read the last agent); a lane
-    // with an empty market reads row 0 of a market that has agents (masked later)
+    // with an empty market reads the tile's first agent (masked later)
     const int last = n > 0 ? n - 1 : 0;
-    const int fl = __builtin_ctzll(ballot(n > 0));
-    const int64_t offl = ((int64_t)__builtin_amdgcn_readlane((int)(off >> 32), fl) << 32) |
-                         (uint32_t)__builtin_amdgcn_readlane((int)off, fl);
-    const int64_t base = n > 0 ? off : offl;
+    const int rbase = n > 0 ? lrow : 0;
+    const int64_t gbase = n > 0 ? off : B;
+    auto stage = [&](double* buf, const double* src) {
+      wave_sync_lds();  // the buffer's previous readers (this wave) are done
+      for (int e = 2 * lane; e < cnt_tile; e += 128) {
+        if (e + 1 < cnt_tile && ((uintptr_t)(src + B + e) & 15) == 0) {
+          const double2 v = *reinterpret_cast<const double2*>(src + B + e);
+          buf[tb_pad(e)] = v.x;
+          buf[tb_pad(e + 1)] = v.y;
+        } else {
+          buf[tb_pad(e)] = src[B + e];
+          if (e + 1 < cnt_tile) buf[tb_pad(e + 1)] = src[B + e + 1];
+        }
+      }
+      wave_sync_lds();
+    };
+    // agent t of this lane's market
+    auto at = [&](const double* buf, const double* src, int t) -> double {
+      if constexpr (STAGED) return buf[tb_pad(rbase + t)];
+      else return src[gbase + t];
+    };
     const double nd = (double)(n > 0 ? n : 1);
 
-    // ---- 1. confidence variance (input order) ---------------------------------------
-    double variance;
-    {
-      double c[kTbLpmMax];
-#pragma unroll
-      for (int t = 0; t < kTbLpmMax; ++t) c[t] = a.conf[base + min(t, last)];
-      double cs = 0.0;
-#pragma unroll
-      for (int t = 0; t < kTbLpmMax; ++t) cs += (t < n) ? c[t] : 0.0;
-      const double mean = cs / nd;
-      double vs = 0.0;
-#pragma unroll
-      for (int t = 0; t < kTbLpmMax; ++t) vs += (t < n) ? bce_pow::pow2(c[t] - mean) : 0.0;
-      variance = vs / nd;
-    }
-
-    // ---- 2. keys and group ordinals (first-seen order) --------------------------------
+    // ---- 1. keys, group ordinals (first-seen order), sort with the key as payload ---------
     unsigned u[kTbLpmMax];
+    double kp[kTbLpmMax];
     int ng = 0;
+    if constexpr (STAGED) stage(bufA, a.pred);
     {
-      double k[kTbLpmMax];
 #pragma unroll
-      for (int t = 0; t < kTbLpmMax; ++t) k[t] = tb_round(a.pred[base + min(t, last)], a);
+      for (int t = 0; t < kTbLpmMax; ++t) kp[t] = tb_round(at(bufA, a.pred, min(t, last)), a);
       int go[kTbLpmMax];
 #pragma unroll
       for (int t = 0; t < kTbLpmMax; ++t) {
         int g = -1;
 #pragma unroll
-        for (int s2 = 0; s2 < t; ++s2) g = key_eq(k[s2], k[t]) ? go[s2] : g;  // earlier equal key: its group
+        for (int s2 = 0; s2 < t; ++s2) g = key_eq(kp[s2], kp[t]) ? go[s2] : g;  // earlier equal key: its group
         const bool fresh = (t < n) && g < 0;
         go[t] = fresh ? ng : g;
         ng += fresh ? 1 : 0;
@@ -255,43 +284,80 @@ __global__ __launch_bounds__(256) void tiebreak_lpm_kernel(TbArgs a, const int32
         u[t] = (t < n) ? (((unsigned)go[t] << 5) | (unsigned)t) : 0xFFFFFFFFu;
       }
     }
-    oem_sort<kTbLpmMax>(u);
+    oem_sort_kv(u, kp);
 
-    // ---- 3. walk the groups: sums in input order, outputs, winner ------------------------
-    double tot = 0.0, cs = 0.0, mx = 0.0, bd = 0.0, bm = 0.0, bk = 0.0;
-    int cnt = 0, lead = 0;
+    // ---- 2. walk 1: weights and reliabilities by group --------------------------------------
+    if constexpr (STAGED) {
+      stage(bufA, a.weight);
+      stage(bufB, a.rel);
+    }
+    double bd = 0.0, bm = 0.0, bk = 0.0;
     bool tie = false;
+    {
+      double tot = 0.0, mx = 0.0;
+      int cnt = 0;
 #pragma unroll
-    for (int p = 0; p < kTbLpmMax; ++p) {
-      if (p < n) {
-        const unsigned v = u[p];
-        const int t = (int)(v & 31u);
-        const unsigned g = v >> 5;
-        const bool start = (p == 0) || (g != (u[p > 0 ? p - 1 : 0] >> 5));
-        const bool end = (p + 1 >= n) || (g != (u[p + 1 < kTbLpmMax ? p + 1 : p] >> 5));
-        const double w = a.weight[off + t], c = a.conf[off + t], r = a.rel[off + t];
-        tot = (start ? 0.0 : tot) + w;     // tiebreak.py:60, sum from int 0
-        cs = (start ? 0.0 : cs) + c;       // tiebreak.py:61
-        cnt = (start ? 0 : cnt) + 1;
-        mx = start ? r : ((r > mx) ? r : mx);  // tiebreak.py:62, first maximum kept
-        lead = start ? t : lead;
-        if (end) {
-          const double praw = a.pred[off + lead];
-          const double key = (n == 1) ? praw : tb_round(praw, a);  // single agent: raw (tiebreak.py:89-96)
-          const double dens = tot / (double)cnt, avgc = cs / (double)cnt;
-          const int64_t go_ = off + (int64_t)g;
-          if (a.g_key) a.g_key[go_] = key;
-          if (a.g_count) a.g_count[go_] = cnt;
-          if (a.g_density) a.g_density[go_] = dens;
-          if (a.g_avgconf) a.g_avgconf[go_] = avgc;
-          if (a.g_maxrel) a.g_maxrel[go_] = mx;
-          const bool same = (dens == bd) && (mx == bm);
-          if (g == 0 || tb_better(dens, mx, key, bd, bm, bk)) {
-            tie = (g != 0) && same;
-            bd = dens; bm = mx; bk = key;
-          } else {
-            tie = tie || same;
+      for (int p = 0; p < kTbLpmMax; ++p) {
+        if (p < n) {
+          const unsigned v = u[p];
+          const int t = (int)(v & 31u);
+          const unsigned g = v >> 5;
+          const bool start = (p == 0) || (g != (u[p > 0 ? p - 1 : 0] >> 5));
+          const bool end = (p + 1 >= n) || (g != (u[p + 1 < kTbLpmMax ? p + 1 : p] >> 5));
+          const double w = at(bufA, a.weight, t), r = at(bufB, a.rel, t);
+          tot = (start ? 0.0 : tot) + w;          // tiebreak.py:60, sum from int 0
+          cnt = (start ? 0 : cnt) + 1;
+          mx = start ? r : ((r > mx) ? r : mx);  // tiebreak.py:62, first maximum kept
+          if (end) {
+            // the group's key: the leader's rounded prediction (the run's first entry carries
+            // it, as do all the others); a single agent keeps its raw prediction (tiebreak.py:89-96)
+            const double key = (n == 1) ? a.pred[off] : kp[p];
+            const double dens = tot / (double)cnt;
+            const int64_t go_ = off + (int64_t)g;
+            if (a.g_key) a.g_key[go_] = key;
+            if (a.g_count) a.g_count[go_] = cnt;
+            if (a.g_density) a.g_density[go_] = dens;
+            if (a.g_maxrel) a.g_maxrel[go_] = mx;
+            const bool same = (dens == bd) && (mx == bm);
+            if (g == 0 || tb_better(dens, mx, key, bd, bm, bk)) {
+              tie = (g != 0) && same;
+              bd = dens; bm = mx; bk = key;
+            } else {
+              tie = tie || same;
+            }
           }
+        }
+      }
+    }
+
+    // ---- 3. confidences: variance (input order) and walk 2 (per-group sums) -----------------
+    if constexpr (STAGED) stage(bufA, a.conf);
+    double variance;
+    {
+      double cs = 0.0;
+#pragma unroll
+      for (int t = 0; t < kTbLpmMax; ++t) cs += (t < n) ? at(bufA, a.conf, t < n ? t : last) : 0.0;
+      const double mean = cs / nd;
+      double vs = 0.0;
+#pragma unroll
+      for (int t = 0; t < kTbLpmMax; ++t)
+        vs += (t < n) ? bce_pow::pow2(at(bufA, a.conf, t < n ? t : last) - mean) : 0.0;
+      variance = vs / nd;
+    }
+    {
+      double gcs = 0.0;
+      int cnt = 0;
+#pragma unroll
+      for (int p = 0; p < kTbLpmMax; ++p) {
+        if (p < n) {
+          const unsigned v = u[p];
+          const int t = (int)(v & 31u);
+          const unsigned g = v >> 5;
+          const bool start = (p == 0) || (g != (u[p > 0 ? p - 1 : 0] >> 5));
+          const bool end = (p + 1 >= n) || (g != (u[p + 1 < kTbLpmMax ? p + 1 : p] >> 5));
+          gcs = (start ? 0.0 : gcs) + at(bufA, a.conf, t);  // tiebreak.py:61
+          cnt = (start ? 0 : cnt) + 1;
+          if (end && a.g_avgconf) a.g_avgconf[off + (int64_t)g] = gcs / (double)cnt;
         }
       }
     }
@@ -551,15 +617,21 @@ extern "C" int bce_tiebreak_csr(const int64_t* offsets, int64_t n_markets, const
   }
   TbArgs a{offsets, n_markets, pred, conf, weight, rel, winner, label, n_groups, variance,
            g_key, g_count, g_density, g_avgconf, g_maxrel, g_of, rs, rt, rmode};
-  if (max_len <= kTbLpmMax) {  // lane per market: 64 markets per wave, 4 waves per workgroup
+  if (max_len <= kTbLpmMax) {  // lane per market: 64 markets per wave, kTbLpmWaves per workgroup
     const int64_t tiles = (nl + 63) / 64;
-    int64_t blocks = (tiles + 3) / 4;
-    const int per_cu = blocks_per_cu(reinterpret_cast<const void*>(&tiebreak_lpm_kernel), 256, 0, 4,
-                                     "tiebreak_lpm_kernel");
+    int64_t blocks = (tiles + kTbLpmWaves - 1) / kTbLpmWaves;
+    // contiguous markets stage each wave's agent range in LDS; a market list gathers rows
+    const void* fn = market_list ? reinterpret_cast<const void*>(&tiebreak_lpm_kernel<false>)
+                                 : reinterpret_cast<const void*>(&tiebreak_lpm_kernel<true>);
+    const int per_cu = blocks_per_cu(fn, 64 * kTbLpmWaves, 0, 1, "tiebreak_lpm_kernel");
     const int64_t cap = (int64_t)cu_count() * per_cu;
     if (blocks > cap) blocks = cap;
-    hipLaunchKernelGGL(tiebreak_lpm_kernel, dim3((int)blocks), dim3(256), 0, as_stream(stream), a, market_list,
-                       nl, fault_word());
+    if (market_list)
+      hipLaunchKernelGGL((tiebreak_lpm_kernel<false>), dim3((int)blocks), dim3(64 * kTbLpmWaves), 0,
+                         as_stream(stream), a, market_list, nl, fault_word());
+    else
+      hipLaunchKernelGGL((tiebreak_lpm_kernel<true>), dim3((int)blocks), dim3(64 * kTbLpmWaves), 0,
+                         as_stream(stream), a, market_list, nl, fault_word());
     return check_launch("tiebreak_lpm_kernel");
   }
   int64_t blocks = (nl + 3) / 4;

@@ -200,10 +200,11 @@ def _c2_like(M, S, seed, L=32, base=0):
     return dict(offsets=off, sid=sid, prob=prob, rel=rel, conf=conf, present=present)
 
 
-@pytest.mark.parametrize("S", [10000, 10112, 12000, 16384, 20000, 100000])
+@pytest.mark.parametrize("S", [10000, 10112, 10113, 12000, 16384, 20000, 100000, 262144, 262145, 1000000])
 def test_c2_shape_every_table_size(S):
-    """n = 32 contiguous markets: LDS-table kernel (S <= 10112), pipe kernel (S <= 16384),
-    flat kernel (larger tables) -- all bit-exact, all eight outputs."""
+    """n = 32 contiguous markets: LDS-table kernel (S <= 10112), hybrid LDS + global table
+    (S <= 2^18: the first ~10k rows in LDS beside the whole bitmask), pipe kernel beyond
+    (present bits from global memory past 16384 sources) -- all bit-exact, all eight outputs."""
     g = _c2_like(20000, S, S)
     exp = orc.consensus_csr(g["offsets"], g["sid"], g["prob"], g["rel"], g["conf"], g["present"])
     _compare_vec(_run(g, max_len=32), exp, g["offsets"])
@@ -352,3 +353,29 @@ def test_pipe_kernel_spin_cap_reports_fault():
     exp = orc.consensus_csr(g["offsets"], g["sid"], g["prob"], g["rel"], g["conf"], g["present"])
     _compare_vec(_run(g, max_len=32), exp, g["offsets"])
     N.check_faults()
+
+
+@pytest.mark.parametrize("S", [12000, 40000])
+def test_c2_hybrid_table_ragged_and_compact(S):
+    """Hybrid LDS/global table on irregular tiles (lengths 17..32, duplicates, cold sources,
+    a shard that starts mid-batch) and in compact mode (no per-unique outputs): bit-exact."""
+    from bayesian_engine import batch
+    rng = np.random.default_rng(S)
+    M = 5000
+    lens = rng.integers(17, 33, M)
+    off = np.zeros(M + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    n = int(off[-1])
+    hot = rng.integers(0, S, 64)
+    sid = np.where(rng.random(n) < 0.3, hot[rng.integers(0, 64, n)], rng.integers(0, S, n)).astype(np.int32)
+    prob = rng.random(n)
+    rel, conf = rng.uniform(0.1, 1.0, S), rng.random(S)
+    present = (rng.random(S) < 0.8).astype(np.uint8)
+    rel[present == 0], conf[present == 0] = 0.5, 0.25
+    g = dict(offsets=off, sid=sid, prob=prob, rel=rel, conf=conf, present=present)
+    exp = orc.consensus_csr(off, sid, prob, rel, conf, present)
+    _compare_vec(_run(g, max_len=32), exp, off)
+    table = batch.SourceTable.from_arrays(_dev(rel), _dev(conf), _dev(present))
+    r = batch.consensus(_dev(off), _dev(sid), _dev(prob), table, max_len=32, unique_outputs=False, check=True)
+    for k in ("consensus", "confidence", "total_weight", "n_unique", "err_idx"):
+        assert np.array_equal(getattr(r, k).cpu().numpy(), exp[k], equal_nan=True), k
