@@ -26,7 +26,9 @@ Also measured here:
                 its outputs are also the full-size parity check (all eight outputs).
 Before the W warmup steps the device runs the step for --prewarm-s seconds so the clocks
 have ramped (a 20-step run then matches a 200-step one); that time is reported.
-Other configs (--config c3|c4|c5|ns|agg|tb) are secondary bench lines; the default is c2.
+Other configs (--config c3|c4|c5|ns|agg|tb) are secondary bench lines; the default is c2,
+and at N=1 the default run also appends c3, c4, tb and c5 (reduced steps, each with its
+roofline, CPU baseline and full-size parity) under "secondary" (--no-secondary skips them).
 """
 from __future__ import annotations
 
@@ -78,6 +80,9 @@ def parse(argv=None):
     p.add_argument("--shard", default=None,
                    help="c3 only: R/N or all/N -- time rank R's (or every rank's) market shard of an N-rank "
                         "run in this one process, no process group (predicted strong scaling)")
+    p.add_argument("--no-secondary", action="store_true",
+                   help="c2 at N=1 only: skip the secondary lines (c3, c4, c5, tb) the default run appends "
+                        "under 'secondary' (each a reduced-step run of its own --config line)")
     p.add_argument("--stub", action="store_true",
                    help="launcher self-test: a CPU no-op step under gloo (no GPU, no library)")
     return p.parse_args(argv)
@@ -397,6 +402,44 @@ def bench_c2(args, world, rank):
     return out
 
 
+SECONDARY = (("c3", 20, 3), ("c4", 100, 10), ("tb", 10, 2), ("c5", 4, 1))  # (config, steps, warmup)
+
+
+def run_secondary(args, world, rank) -> dict:
+    """The other BASELINE.json configs, each timed exactly like its own ``--config`` line
+    (reduced steps, same CPU baseline and full-size parity), summarised under the headline
+    line so the default run measures every config.  N = 1 only: configs 4 and 5 exchange
+    per-source flags / per-agent counts over RCCL when N > 1 (``--config c4|c5 --gpus N``)."""
+    import copy
+    import gc
+
+    from bench_extra import run_extra
+
+    out = {}
+    for cfg, steps, warmup in SECONDARY:
+        a2 = copy.copy(args)
+        a2.config, a2.steps, a2.warmup, a2.prewarm_s, a2.mode = cfg, steps, warmup, 0.3, None
+        t0 = time.perf_counter()
+        try:
+            j = run_extra(a2, world, rank)
+            r = j.get("roofline") or {}
+            cb = j.get("cpu_baseline") or {}
+            par = j.get("parity_vs_oracle")
+            out[cfg] = {"metric": j["metric"], "value": j["value"], "unit": j["unit"], "steps": steps,
+                        "ms_per_step": j["ms_per_step"], "dtype": j.get("dtype"), "config": j.get("config"),
+                        "roofline": {k: r.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic",
+                                                           "kernel", "bytes_per_launch", "avg_launch_ms", "mfma",
+                                                           "exact_mode", "fast_mode") if k in r},
+                        "cpu_baseline": cb or None, "parity_vs_oracle": par,
+                        "wall_s": round(time.perf_counter() - t0, 1)}
+        except Exception as exc:  # a secondary line never takes the headline down
+            out[cfg] = {"error": f"{type(exc).__name__}: {exc}"}
+        gc.collect()
+        torch.cuda.empty_cache()
+        print(f"[bench] secondary {cfg}: {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
+    return out
+
+
 def bench_stub(args, world, rank):
     """Launcher self-test (tests/test_bench_launcher.py): same timing skeleton, CPU no-op step."""
     wall, per, prewarm = timed_loop(lambda: None, args, world)
@@ -424,6 +467,8 @@ def main(argv=None):
         out = run_extra(args, world, rank)
     else:
         out = bench_c2(args, world, rank)
+        if world == 1 and not args.no_secondary:
+            out["secondary"] = run_secondary(args, world, rank)
     if rank == 0:
         if isinstance(out.get("roofline"), dict):  # how avg_launch_ms was taken
             out["roofline"]["timing"] = ("HIP events around the timed region / steps (launches + boundaries)"

@@ -336,22 +336,23 @@ def test_fault_word_wide_kernel(mode):
 
 def test_pipe_kernel_spin_cap_reports_fault():
     """A persistent wave that exhausts its bounded wait records a fault instead of silently
-    leaving its tiles unwritten (forced with a tiny cap on the pipe kernel, S = 12000)."""
+    leaving its tiles unwritten (forced with a tiny cap on the pipe kernel: markets of 16,
+    which the LDS-table kernel does not take)."""
     from bayesian_engine import _native as N, batch
     L = N.lib()
-    g = _c2_like(50000, 12000, 9)
+    g = _c2_like(50000, 12000, 9, L=16)
     table = batch.SourceTable.from_arrays(_dev(g["rel"]), _dev(g["conf"]), _dev(g["present"]))
     args = (_dev(g["offsets"]), _dev(g["sid"], np.int32), _dev(g["prob"]), table)
     N.check_faults()
     try:
         N.check(L.bce_debug_set_spin_cap(1))
-        batch.consensus(*args, max_len=32)
+        batch.consensus(*args, max_len=16)
         with pytest.raises(N.BCEError, match="timed out"):
             N.check_faults()
     finally:
         L.bce_debug_set_spin_cap(0)
     exp = orc.consensus_csr(g["offsets"], g["sid"], g["prob"], g["rel"], g["conf"], g["present"])
-    _compare_vec(_run(g, max_len=32), exp, g["offsets"])
+    _compare_vec(_run(g, max_len=16), exp, g["offsets"])
     N.check_faults()
 
 
