@@ -71,6 +71,9 @@ _SIGS = {
     "bce_reestimate_weights": (C.c_int, [_i64, _vp, _vp, _vp, _vp]),
     "bce_reestimate_consensus_votes": (C.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "bce_reestimate_agreement_votes": (C.c_int, [_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp]),
+    "bce_reestimate_consensus_votes_mfma": (C.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                                      _i64, _vp]),
+    "bce_reestimate_mfma_scratch_bytes": (_i64, [_i64]),
     "bce_namespace_resolve": (C.c_int, [_i64] + [_vp] * 12 + [_i32, _i64, _f64, _f64, _f64, _f64, _i32,
                                                                _vp, _vp, _vp, _vp]),
     "bce_aggregate_groups": (C.c_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),

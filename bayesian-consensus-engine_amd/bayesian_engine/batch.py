@@ -457,12 +457,14 @@ def aggregate(group_offsets: torch.Tensor, members: torch.Tensor, consensus: tor
 
 
 def reestimate(P: torch.Tensor, iters: int, w0: float = 0.5, w: Optional[torch.Tensor] = None,
-               keep_history: bool = False):
+               keep_history: bool = False, mode: str = "exact"):
     """Config 5: ``iters`` rounds of consensus <-> reliability on agent-major P [A, M].
 
     Each round reads P once: the consensus pass records every cell's vote as one bit and the
     agreement pass counts from those bits (bce_reestimate_consensus_votes /
-    bce_reestimate_agreement_votes; A*ceil(M/64)*8 bytes of scratch)."""
+    bce_reestimate_agreement_votes; A*ceil(M/64)*8 bytes of scratch).  ``mode="fast"``
+    runs the consensus pass on the matrix cores (bce_reestimate_consensus_votes_mfma:
+    consensus within 2*A*2^-53, votes and agreement counts identical to exact)."""
     L = N.require_gpu()
     A, M = P.shape
     dev = P.device
@@ -478,10 +480,22 @@ def reestimate(P: torch.Tensor, iters: int, w0: float = 0.5, w: Optional[torch.T
     words = torch.empty((2, K), dtype=torch.int64, device=dev)  # cvote, ok
     hist = []
     st = N.stream(dev)
+    if mode not in _MODES:
+        raise ValueError(f"mode must be one of {sorted(_MODES)}")
+    scratch = None
+    if mode == "fast":
+        nb = int(L.bce_reestimate_mfma_scratch_bytes(M))
+        scratch = torch.empty((nb + 7) // 8, dtype=torch.int64, device=dev)
     for _ in range(iters):
-        N.check(L.bce_reestimate_consensus_votes(N.ptr(P, row_strided=True), A, M, ld, N.ptr(w), N.ptr(cons),
-                                                 N.ptr(nul), N.ptr(votes), N.ptr(words[0]), N.ptr(words[1]), st),
-                "bce_reestimate_consensus_votes")
+        if scratch is None:
+            N.check(L.bce_reestimate_consensus_votes(N.ptr(P, row_strided=True), A, M, ld, N.ptr(w), N.ptr(cons),
+                                                     N.ptr(nul), N.ptr(votes), N.ptr(words[0]), N.ptr(words[1]),
+                                                     st), "bce_reestimate_consensus_votes")
+        else:
+            N.check(L.bce_reestimate_consensus_votes_mfma(N.ptr(P, row_strided=True), A, M, ld, N.ptr(w),
+                                                          N.ptr(cons), N.ptr(nul), N.ptr(votes), N.ptr(words[0]),
+                                                          N.ptr(words[1]), N.ptr(scratch), scratch.numel() * 8, st),
+                    "bce_reestimate_consensus_votes_mfma")
         agree.zero_()
         resolved.zero_()
         N.check(L.bce_reestimate_agreement_votes(N.ptr(votes), A, M, N.ptr(words[0]), N.ptr(words[1]),

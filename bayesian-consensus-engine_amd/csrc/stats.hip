@@ -229,6 +229,136 @@ __global__ __launch_bounds__(256) void reestimate_agreement_votes_kernel(
   }
 }
 
+// ---- BCE_MODE_FAST pass 1 on the matrix cores ---------------------------------------
+// w^T P as v_mfma_f64_16x16x4_f64: A = w broadcast over the 16 rows (lane l holds
+// w[a + (l >> 4)]), B = a 4-agent x 16-market block of P (lane l holds
+// P[a + (l >> 4)][m0 + 16j + (l & 15)]), so every row of D is the block's 16 column sums (a
+// GEMV leaves 15 of 16 rows redundant; the kernel is HBM-bound either way).  A wave owns 64
+// markets (four 16-column accumulators), 16 agents per step (16 loads in flight).  The
+// vote bits come from the same loads: ballot j holds bit 16k + n = (P[a+k][m0+16j+n] >=
+// 0.5), regrouped per agent into the vote_bits word layout of the exact kernel.
+// The sums are in MFMA order, not agent order (within 2*A*2^-53 of the exact consensus);
+// markets whose consensus lies within 4*A*2^-53 of 0.5 -- where the vote could differ --
+// are listed for reestimate_fixup_kernel, which redoes them in exact agent order, so the
+// votes and therefore the agreement counts are identical to the exact path.
+typedef double mfma_d4 __attribute__((ext_vector_type(4)));
+constexpr int kMfmaSteps = 4;  // 4-agent MFMA steps per loop iteration (16 agents)
+
+__global__ __launch_bounds__(256) void reestimate_total_kernel(const double* __restrict__ w, int64_t A,
+                                                               double* __restrict__ total_fast,
+                                                               int32_t* __restrict__ nflag) {
+  __shared__ double part[256];
+  double s = 0.0;
+  for (int64_t a = threadIdx.x; a < A; a += 256) s += w[a];  // fixed order: deterministic
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) part[threadIdx.x] += part[threadIdx.x + h];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    *total_fast = part[0];
+    *nflag = 0;
+  }
+}
+
+__global__ __launch_bounds__(256) void reestimate_votes_mfma_kernel(
+    const double* __restrict__ P, int64_t A, int64_t M, int64_t ld, const double* __restrict__ w,
+    const double* __restrict__ total_fast, double* __restrict__ cons, uint8_t* __restrict__ null_out,
+    unsigned long long* __restrict__ vote_bits, unsigned long long* __restrict__ cvote_words,
+    unsigned long long* __restrict__ ok_words, int32_t* __restrict__ nflag, int32_t* __restrict__ flags) {
+  const int lane = lane_id();
+  const int64_t k = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;  // vote word = 64 markets
+  const int64_t m0 = k << 6;
+  if (m0 >= M) return;  // wave-uniform
+  const int ka = lane >> 4, n = lane & 15;
+  mfma_d4 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = mfma_d4{0.0, 0.0, 0.0, 0.0};
+  bool inm[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) inm[j] = m0 + 16 * j + n < M;
+  unsigned long long* vb = vote_bits + k * A;
+  for (int64_t a = 0; a < A; a += 4 * kMfmaSteps) {
+    double v[kMfmaSteps][4], wa[kMfmaSteps];
+#pragma unroll
+    for (int q = 0; q < kMfmaSteps; ++q) {
+      const int64_t ag = a + 4 * q + ka;
+      const bool ain = ag < A;
+      wa[q] = ain ? w[ag] : 0.0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[q][j] = (ain && inm[j]) ? P[ag * ld + m0 + 16 * j + n] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < kMfmaSteps; ++q) {
+      unsigned long long bal[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(wa[q], v[q][j], acc[j], 0, 0, 0);
+        bal[j] = ballot(a + 4 * q + ka < A && inm[j] && v[q][j] >= 0.5);  // market.py:298-299
+      }
+      // agent a + 4q + lane's vote word (lanes 0..3): its 16-bit slice of every ballot
+      unsigned long long word = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) word |= ((bal[j] >> (16 * (lane & 3))) & 0xFFFFull) << (16 * j);
+      if (lane < 4 && a + 4 * q + lane < A) vb[a + 4 * q + lane] = word;
+    }
+  }
+  // lane L = 16j + n' holds market m0 + L's sum in acc[j] (every row of D is the same)
+  const int jj = lane >> 4;
+  const double ws = (jj == 0) ? acc[0][0] : (jj == 1) ? acc[1][0] : (jj == 2) ? acc[2][0] : acc[3][0];
+  const int64_t m = m0 + lane;
+  const bool in = m < M;
+  const double total = *total_fast;
+  const bool isnull = (total == 0.0);  // w >= 0: zero in every order iff every weight is zero
+  const double c = isnull ? 0.0 : ws / total;
+  const double bound = 4.0 * (double)(A + 2) * 0x1p-53;
+  const bool near = in && !isnull && fabs(c - 0.5) <= bound;
+  if (in) {
+    cons[m] = c;
+    null_out[m] = isnull ? 1 : 0;
+  }
+  if (near) flags[atomicAdd(nflag, 1)] = (int32_t)m;
+  const unsigned long long okw = ballot(in && !isnull);
+  const unsigned long long cvw = ballot(in && !isnull && c >= 0.5);
+  if (lane == 0) {
+    ok_words[k] = okw;
+    cvote_words[k] = cvw;
+  }
+}
+
+// Exact redo of the flagged markets (agent-order sums, as reestimate_consensus_votes_kernel):
+// one wave per flagged market, lanes load 64 agents at a time, lane 0 adds in agent order.
+__global__ __launch_bounds__(64) void reestimate_fixup_kernel(const double* __restrict__ P, int64_t A, int64_t ld,
+                                                              const double* __restrict__ w,
+                                                              const int32_t* __restrict__ nflag,
+                                                              const int32_t* __restrict__ flags,
+                                                              double* __restrict__ cons,
+                                                              unsigned long long* __restrict__ cvote_words) {
+  const int lane = lane_id();
+  for (int f = blockIdx.x; f < *nflag; f += gridDim.x) {
+    const int64_t m = flags[f];
+    double ws = 0.0, total = 0.0;
+    for (int64_t a0 = 0; a0 < A; a0 += 64) {
+      const int64_t a = a0 + lane;
+      const double v = a < A ? P[a * ld + m] : 0.0, wq = a < A ? w[a] : 0.0;
+      const int cnt = (A - a0 < 64) ? (int)(A - a0) : 64;
+      for (int q = 0; q < cnt; ++q) {
+        const double vq = __shfl(v, q), wqq = __shfl(wq, q);
+        ws += (0.0 + vq) * wqq;  // core.py:116,136
+        total += wqq;
+      }
+    }
+    if (lane == 0) {
+      const double c = ws / total;  // total > 0: flagged markets are not null
+      cons[m] = c;
+      const unsigned long long bit = 1ull << (m & 63);
+      if (c >= 0.5) atomicOr(&cvote_words[m >> 6], bit);
+      else atomicAnd(&cvote_words[m >> 6], ~bit);
+    }
+  }
+}
+
 __global__ void reestimate_weights_kernel(int64_t A, const long long* agree, const long long* resolved,
                                           double* w) {
   for (int64_t a = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; a < A;
@@ -333,3 +463,35 @@ extern "C" int bce_reestimate_agreement_votes(const uint64_t* vote_bits, int64_t
                      reinterpret_cast<long long*>(resolved));
   return check_launch("reestimate_agreement_votes_kernel");
 }
+
+extern "C" int bce_reestimate_consensus_votes_mfma(const double* P, int64_t A, int64_t M, int64_t ld,
+                                                   const double* w, double* consensus, uint8_t* null_out,
+                                                   uint64_t* vote_bits, uint64_t* cvote_words, uint64_t* ok_words,
+                                                   void* scratch, int64_t scratch_bytes, void* stream) {
+  BCE_REQUIRE(A > 0 && M >= 0 && ld >= M, "reestimate_votes_mfma: bad shape");
+  if (M == 0) return BCE_OK;
+  BCE_REQUIRE(P && w && consensus && null_out && vote_bits && cvote_words && ok_words && scratch,
+              "reestimate_votes_mfma: NULL argument");
+  BCE_REQUIRE(scratch_bytes >= bce_reestimate_mfma_scratch_bytes(M),
+              "reestimate_votes_mfma: scratch too small (%lld < %lld)", (long long)scratch_bytes,
+              (long long)bce_reestimate_mfma_scratch_bytes(M));
+  BCE_REQUIRE((uintptr_t)scratch % 8 == 0, "reestimate_votes_mfma: scratch must be 8-byte aligned");
+  hipStream_t st = as_stream(stream);
+  double* total = reinterpret_cast<double*>(scratch);
+  int32_t* nflag = reinterpret_cast<int32_t*>(total + 1);
+  int32_t* flags = nflag + 2;
+  hipLaunchKernelGGL(reestimate_total_kernel, dim3(1), dim3(256), 0, st, w, A, total, nflag);
+  int rc = check_launch("reestimate_total_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(reestimate_votes_mfma_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, P, A, M, ld,
+                     w, total, consensus, null_out, reinterpret_cast<unsigned long long*>(vote_bits),
+                     reinterpret_cast<unsigned long long*>(cvote_words), reinterpret_cast<unsigned long long*>(ok_words),
+                     nflag, flags);
+  rc = check_launch("reestimate_votes_mfma_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(reestimate_fixup_kernel, dim3(64), dim3(64), 0, st, P, A, ld, w, nflag, flags, consensus,
+                     reinterpret_cast<unsigned long long*>(cvote_words));
+  return check_launch("reestimate_fixup_kernel");
+}
+
+extern "C" int64_t bce_reestimate_mfma_scratch_bytes(int64_t M) { return 16 + 4 * (M > 0 ? M : 1); }

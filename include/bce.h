@@ -271,6 +271,17 @@ int bce_reestimate_consensus_votes(const double* P, int64_t A, int64_t M, int64_
 int bce_reestimate_agreement_votes(const uint64_t* vote_bits, int64_t A, int64_t M, const uint64_t* cvote_words,
                                    const uint64_t* ok_words, int64_t* agreement, int64_t* resolved,
                                    void* stream);
+/* BCE_MODE_FAST pass 1 of the single-read iteration on the matrix cores: w^T P with
+ * v_mfma_f64_16x16x4_f64 (the north star's "MFMA contraction"), same outputs as
+ * bce_reestimate_consensus_votes.  consensus within 2*A*2^-53 of the agent-order value;
+ * markets within 4*A*2^-53 of 0.5 are redone in agent order, so vote_bits / cvote_words /
+ * ok_words -- and the agreement counts -- are identical to the exact pass.  scratch: device
+ * buffer of bce_reestimate_mfma_scratch_bytes(M) bytes (8-byte aligned). */
+int bce_reestimate_consensus_votes_mfma(const double* P, int64_t A, int64_t M, int64_t ld, const double* w,
+                                        double* consensus, uint8_t* null_out, uint64_t* vote_bits,
+                                        uint64_t* cvote_words, uint64_t* ok_words, void* scratch,
+                                        int64_t scratch_bytes, void* stream);
+int64_t bce_reestimate_mfma_scratch_bytes(int64_t M);
 
 #ifdef __cplusplus
 }

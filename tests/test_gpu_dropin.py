@@ -573,3 +573,57 @@ def test_tiebreak_variance_bit_exact_1m_markets():
         dd[m] = sum((x - mu) * (x - mu) for x in c.tolist()) / len(c)
     sel = np.arange(0, M, 997)
     assert np.any(dd[sel] != exp["variance"][sel]), "no market where d*d differs: test lost its teeth"
+
+
+@pytest.mark.parametrize("A,M", [(5, 70), (17, 190), (300, 4097), (4100, 1000)])
+def test_reestimate_mfma_fast_mode_matches_exact_votes(A, M):
+    """BCE_MODE_FAST pass 1 on the matrix cores (bce_reestimate_consensus_votes_mfma):
+    consensus within 2*A*2^-53 of the agent-order value (<= 1e-9), and -- because markets
+    within 4*A*2^-53 of 0.5 are redone in agent order -- vote bits, consensus votes,
+    resolved masks, null flags and agreement counts identical to the exact pass.  Columns
+    of mirrored pairs (x, 1-x) put the consensus at 0.5 up to rounding, so the redo runs."""
+    import torch
+    from bayesian_engine import _native as N
+    rng = np.random.default_rng(A * 31 + M)
+    P = rng.beta(2, 2, size=(A, M))
+    mir = rng.random(M) < 0.2
+    half = A // 2
+    P[half:2 * half, mir] = 1.0 - P[:half, mir]
+    if A % 2:
+        P[-1, mir] = 0.5
+    P[rng.random((A, M)) < 0.003] = np.nan
+    Pt = torch.from_numpy(P).cuda()
+    L = N.lib()
+    st = N.stream(Pt.device)
+    K = (M + 63) // 64
+    nb = int(L.bce_reestimate_mfma_scratch_bytes(M))
+    scratch = torch.empty((nb + 7) // 8, dtype=torch.int64, device="cuda")
+    for wmode in ("half", "mixed", "zero"):
+        w = torch.full((A,), 0.5, dtype=torch.float64, device="cuda")
+        if wmode == "mixed":
+            w = torch.from_numpy(rng.random(A)).cuda()
+        elif wmode == "zero":
+            w.zero_()
+        out = []
+        for fn in ("bce_reestimate_consensus_votes", "bce_reestimate_consensus_votes_mfma"):
+            c = torch.empty(M, dtype=torch.float64, device="cuda")
+            nu = torch.empty(M, dtype=torch.uint8, device="cuda")
+            votes = torch.empty((K, A), dtype=torch.int64, device="cuda")
+            words = torch.empty((2, K), dtype=torch.int64, device="cuda")
+            g = torch.zeros(A + 1, dtype=torch.int64, device="cuda")
+            extra = (N.ptr(scratch), scratch.numel() * 8) if fn.endswith("mfma") else ()
+            N.check(getattr(L, fn)(N.ptr(Pt), A, M, M, N.ptr(w), N.ptr(c), N.ptr(nu), N.ptr(votes), N.ptr(words[0]),
+                                   N.ptr(words[1]), *extra, st), fn)
+            N.check(L.bce_reestimate_agreement_votes(N.ptr(votes), A, M, N.ptr(words[0]), N.ptr(words[1]),
+                                                     N.ptr(g[:A]), N.ptr(g[A:]), st))
+            torch.cuda.synchronize()
+            out.append((c.cpu().numpy(), nu.cpu().numpy(), votes.cpu().numpy(), words.cpu().numpy(), g.cpu().numpy()))
+        (ce, ne, ve, we, ge), (cf, nf, vf, wf, gf) = out
+        assert np.array_equal(ne, nf) and np.array_equal(ve, vf) and np.array_equal(we, wf), wmode
+        assert np.array_equal(ge, gf), wmode
+        fin = np.isfinite(ce)
+        assert np.array_equal(fin, np.isfinite(cf))
+        dev = np.abs(cf[fin] - ce[fin])
+        assert dev.max(initial=0.0) <= 2 * (A + 2) * 2.0 ** -53 and dev.max(initial=0.0) <= 1e-9, wmode
+        near = fin & (np.abs(ce - 0.5) <= 2 * (A + 2) * 2.0 ** -53)
+        assert np.array_equal(cf[near], ce[near])  # the redone markets are exact
