@@ -237,9 +237,9 @@ __global__ __launch_bounds__(256) void reestimate_agreement_votes_kernel(
 // markets (four 16-column accumulators), 16 agents per step (16 loads in flight).  The
 // vote bits come from the same loads: ballot j holds bit 16k + n = (P[a+k][m0+16j+n] >=
 // 0.5), regrouped per agent into the vote_bits word layout of the exact kernel.
-// The sums are in MFMA order, not agent order (within 2*A*2^-53 of the exact consensus);
-// markets whose consensus lies within 4*A*2^-53 of 0.5 -- where the vote could differ --
-// are listed for reestimate_fixup_kernel, which redoes them in exact agent order, so the
+// The sums are in MFMA order, not agent order (within 4*A*2^-53 of the exact consensus);
+// markets whose consensus lies within 8*A*2^-53 of 0.5 -- where the vote could differ --
+// (or whose column holds a cell outside [0, 1] or NaN) are listed for reestimate_fixup_kernel, which redoes them in exact agent order, so the
 // votes and therefore the agreement counts are identical to the exact path.
 typedef double mfma_d4 __attribute__((ext_vector_type(4)));
 constexpr int kMfmaSteps = 4;  // 4-agent MFMA steps per loop iteration (16 agents)
@@ -279,6 +279,7 @@ __global__ __launch_bounds__(256) void reestimate_votes_mfma_kernel(
 #pragma unroll
   for (int j = 0; j < 4; ++j) inm[j] = m0 + 16 * j + n < M;
   unsigned long long* vb = vote_bits + k * A;
+  bool odd[4] = {false, false, false, false};  // a cell outside [0, 1] (or NaN) in this lane's column
   for (int64_t a = 0; a < A; a += 4 * kMfmaSteps) {
     double v[kMfmaSteps][4], wa[kMfmaSteps];
 #pragma unroll
@@ -295,6 +296,7 @@ __global__ __launch_bounds__(256) void reestimate_votes_mfma_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(wa[q], v[q][j], acc[j], 0, 0, 0);
+        odd[j] = odd[j] || !(v[q][j] >= 0.0 && v[q][j] <= 1.0);
         bal[j] = ballot(a + 4 * q + ka < A && inm[j] && v[q][j] >= 0.5);  // market.py:298-299
       }
       // agent a + 4q + lane's vote word (lanes 0..3): its 16-bit slice of every ballot
@@ -312,8 +314,18 @@ __global__ __launch_bounds__(256) void reestimate_votes_mfma_kernel(
   const double total = *total_fast;
   const bool isnull = (total == 0.0);  // w >= 0: zero in every order iff every weight is zero
   const double c = isnull ? 0.0 : ws / total;
-  const double bound = 4.0 * (double)(A + 2) * 0x1p-53;
-  const bool near = in && !isnull && fabs(c - 0.5) <= bound;
+  // |fast - exact| <= ~4*A*2^-53 for cells in [0, 1] (both sums of non-negative terms within
+  // A*2^-53 relative of the true one, c <= 1); a column holding anything else (or NaN) is
+  // always redone
+  unsigned long long oddm = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    unsigned long long b = ballot(odd[j]);
+    b |= (b >> 16) | (b >> 32) | (b >> 48);
+    oddm |= (b & 0xFFFFull) << (16 * j);
+  }
+  const double bound = 8.0 * (double)(A + 2) * 0x1p-53;
+  const bool near = in && !isnull && (fabs(c - 0.5) <= bound || ((oddm >> lane) & 1ull));
   if (in) {
     cons[m] = c;
     null_out[m] = isnull ? 1 : 0;

@@ -177,25 +177,28 @@ __global__ __launch_bounds__(256) void tiebreak_wave_kernel(TbArgs a, const int3
 // instructions serve 64 markets at once.
 //
 // Data movement (STAGED, contiguous markets): a wave's 64 markets are one contiguous CSR
-// range of <= 2048 agents, so each input array is read ONCE with coalesced 16-B loads into
-// a wave-private LDS buffer (one pad double per 32, so lanes reading their own rows hit
-// distinct bank pairs) and the lanes read their rows from there.  (Per-lane global reads of
-// the rows -- the !STAGED path, kept for market lists -- touch 64 lines per instruction and
-// thrash L1/L2: 16.7 GB of HBM reads for the 1 GB the config-2 batch holds.)
+// range [B, E) of <= 2048 agents.  Every input array is read ONCE with coalesced 16-B loads
+// into a wave-private LDS buffer (one pad slot per 32, so lanes reading their own rows hit
+// distinct bank pairs), and every per-agent / per-group output is assembled in such a buffer
+// and leaves with coalesced 16-B stores (per-lane scattered stores wrote each line ~4 times:
+// 5.3 GB of HBM writes for the 1.3 GB of outputs).  A group's outputs go to slot g of the
+// market's row, overwriting the input of agent g in place: group g ends only after every
+// group <= g, and agent g belongs to one of those (ordinals are assigned in first-seen
+// order, so agent g's ordinal is <= g) -- its input has been consumed.  Slots g >= n_groups
+// of a market's row receive unspecified values (include/bce.h).
+// (The !STAGED path, for market lists, reads rows and writes outputs per lane.)
 // Per lane:
 //   1. keys round(pred, precision) (tiebreak.py:54) and each agent's group ordinal in
 //      first-seen (dict insertion) order: O(n^2) key compares, == semantics (-0.0 == 0.0,
 //      NaN never equal); keys (ordinal << 5 | agent) sorted by the odd-even merge network
 //      with the rounded key as payload: every group becomes a run, groups in first-seen
 //      order, members in input order;
-//   2. walk 1 (weight, reliability): the group's weight sum runs in input order from +0.0
+//   2. walk (weight, reliability): the group's weight sum runs in input order from +0.0
 //      (builtin sum from int 0), builtin max keeps the first maximum; at a run's end the
-//      group's count / density / max reliability are stored and the winner (lexicographic
-//      max of (density, max_rel, -key), tiebreak.py:113-117) and the top-two tie flag
-//      (tiebreak.py:123-133) updated;
-//   3. confidences: the variance (tiebreak.py:108-110; mean, then the squares -- libm pow
-//      restated, glibc_pow.hpp -- summed in input order) and walk 2, the per-group
-//      confidence sums (tiebreak.py:61).
+//      winner (lexicographic max of (density, max_rel, -key), tiebreak.py:113-117) and the
+//      top-two tie flag (tiebreak.py:123-133) are updated;
+//   3. variance (tiebreak.py:108-110; mean, then the squares -- libm pow restated,
+//      glibc_pow.hpp -- summed in input order) and the per-group confidence sums.
 constexpr int kTbLpmMax = 32;
 constexpr int kTbLpmWaves = 4;
 constexpr int kTbStage = 64 * kTbLpmMax + 64;  // doubles per buffer: a tile's agents + pads
@@ -210,6 +213,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) void tiebreak_lpm_kernel(TbArgs a
   const int wv = STAGED ? (int)(threadIdx.x >> 6) : 0;
   double* const bufA = sBuf[wv][0];
   double* const bufB = sBuf[wv][1];
+  int32_t* const ibufB = reinterpret_cast<int32_t*>(bufB);
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t tile = wave; tile * 64 < n_list; tile += nwaves) {
@@ -242,10 +246,12 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) void tiebreak_lpm_kernel(TbArgs a
     const int last = n > 0 ? n - 1 : 0;
     const int rbase = n > 0 ? lrow : 0;
     const int64_t gbase = n > 0 ? off : B;
+    // global [B, E) -> LDS (padded), coalesced 16-B loads
     auto stage = [&](double* buf, const double* src) {
       wave_sync_lds();  // the buffer's previous readers (this wave) are done
+      const bool al = ((uintptr_t)(src + B) & 15) == 0;
       for (int e = 2 * lane; e < cnt_tile; e += 128) {
-        if (e + 1 < cnt_tile && ((uintptr_t)(src + B + e) & 15) == 0) {
+        if (al && e + 1 < cnt_tile) {
           const double2 v = *reinterpret_cast<const double2*>(src + B + e);
           buf[tb_pad(e)] = v.x;
           buf[tb_pad(e + 1)] = v.y;
@@ -256,10 +262,44 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) void tiebreak_lpm_kernel(TbArgs a
       }
       wave_sync_lds();
     };
+    // LDS (padded) -> global [B, E), coalesced 16-B stores
+    auto flush = [&](const double* buf, double* dst) {
+      wave_sync_lds();
+      const bool al = ((uintptr_t)(dst + B) & 15) == 0;
+      for (int e = 2 * lane; e < cnt_tile; e += 128) {
+        if (al && e + 1 < cnt_tile) {
+          *reinterpret_cast<double2*>(dst + B + e) = make_double2(buf[tb_pad(e)], buf[tb_pad(e + 1)]);
+        } else {
+          dst[B + e] = buf[tb_pad(e)];
+          if (e + 1 < cnt_tile) dst[B + e + 1] = buf[tb_pad(e + 1)];
+        }
+      }
+    };
+    auto flush_i32 = [&](const int32_t* buf, int32_t* dst) {
+      wave_sync_lds();
+      const bool al = ((uintptr_t)(dst + B) & 15) == 0;
+      for (int e = 4 * lane; e < cnt_tile; e += 256) {
+        if (al && e + 3 < cnt_tile) {
+          *reinterpret_cast<int4*>(dst + B + e) =
+              make_int4(buf[tb_pad(e)], buf[tb_pad(e + 1)], buf[tb_pad(e + 2)], buf[tb_pad(e + 3)]);
+        } else {
+          for (int q = 0; q < 4 && e + q < cnt_tile; ++q) dst[B + e + q] = buf[tb_pad(e + q)];
+        }
+      }
+    };
     // agent t of this lane's market
     auto at = [&](const double* buf, const double* src, int t) -> double {
       if constexpr (STAGED) return buf[tb_pad(rbase + t)];
       else return src[gbase + t];
+    };
+    // this lane's slot g (an agent's or a group's output)
+    auto put = [&](double* buf, double* dst, int g, double v) {
+      if constexpr (STAGED) buf[tb_pad(lrow + g)] = v;
+      else dst[off + g] = v;
+    };
+    auto put_i32 = [&](int32_t* buf, int32_t* dst, int g, int v) {
+      if constexpr (STAGED) buf[tb_pad(lrow + g)] = v;
+      else dst[off + g] = v;
     };
     const double nd = (double)(n > 0 ? n : 1);
 
@@ -280,13 +320,18 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) void tiebreak_lpm_kernel(TbArgs a
         const bool fresh = (t < n) && g < 0;
         go[t] = fresh ? ng : g;
         ng += fresh ? 1 : 0;
-        if (a.g_of && t < n) a.g_of[off + t] = go[t];
+        if (a.g_of && t < n) put_i32(ibufB, a.g_of, t, go[t]);
         u[t] = (t < n) ? (((unsigned)go[t] << 5) | (unsigned)t) : 0xFFFFFFFFu;
       }
     }
+    if constexpr (STAGED) {
+      if (a.g_of) flush_i32(ibufB, a.g_of);
+    }
+    // a single agent keeps its raw prediction (tiebreak.py:89-96)
+    const double praw0 = at(bufA, a.pred, 0);
     oem_sort_kv(u, kp);
 
-    // ---- 2. walk 1: weights and reliabilities by group --------------------------------------
+    // ---- 2. walk: weights and reliabilities by group, the winner ---------------------------
     if constexpr (STAGED) {
       stage(bufA, a.weight);
       stage(bufB, a.rel);
@@ -309,15 +354,10 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) void tiebreak_lpm_kernel(TbArgs a
           cnt = (start ? 0 : cnt) + 1;
           mx = start ? r : ((r > mx) ? r : mx);  // tiebreak.py:62, first maximum kept
           if (end) {
-            // the group's key: the leader's rounded prediction (the run's first entry carries
-            // it, as do all the others); a single agent keeps its raw prediction (tiebreak.py:89-96)
-            const double key = (n == 1) ? a.pred[off] : kp[p];
+            const double key = (n == 1) ? praw0 : kp[p];  // the run's entries all carry the group key
             const double dens = tot / (double)cnt;
-            const int64_t go_ = off + (int64_t)g;
-            if (a.g_key) a.g_key[go_] = key;
-            if (a.g_count) a.g_count[go_] = cnt;
-            if (a.g_density) a.g_density[go_] = dens;
-            if (a.g_maxrel) a.g_maxrel[go_] = mx;
+            if (a.g_density) put(bufA, a.g_density, (int)g, dens);  // slot g's inputs are consumed
+            if (a.g_maxrel) put(bufB, a.g_maxrel, (int)g, mx);
             const bool same = (dens == bd) && (mx == bm);
             if (g == 0 || tb_better(dens, mx, key, bd, bm, bk)) {
               tie = (g != 0) && same;
@@ -329,8 +369,34 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) void tiebreak_lpm_kernel(TbArgs a
         }
       }
     }
+    if constexpr (STAGED) {
+      if (a.g_density) flush(bufA, a.g_density);
+      if (a.g_maxrel) flush(bufB, a.g_maxrel);
+    }
+    // group keys and counts from the sorted runs alone
+    if (a.g_key || a.g_count) {
+      if constexpr (STAGED) wave_sync_lds();  // the flushes above have read their buffers
+      int cnt = 0;
+#pragma unroll
+      for (int p = 0; p < kTbLpmMax; ++p) {
+        if (p < n) {
+          const unsigned g = u[p] >> 5;
+          const bool start = (p == 0) || (g != (u[p > 0 ? p - 1 : 0] >> 5));
+          const bool end = (p + 1 >= n) || (g != (u[p + 1 < kTbLpmMax ? p + 1 : p] >> 5));
+          cnt = (start ? 0 : cnt) + 1;
+          if (end) {
+            if (a.g_key) put(bufA, a.g_key, (int)g, (n == 1) ? praw0 : kp[p]);
+            if (a.g_count) put_i32(ibufB, a.g_count, (int)g, cnt);
+          }
+        }
+      }
+      if constexpr (STAGED) {
+        if (a.g_key) flush(bufA, a.g_key);
+        if (a.g_count) flush_i32(ibufB, a.g_count);
+      }
+    }
 
-    // ---- 3. confidences: variance (input order) and walk 2 (per-group sums) -----------------
+    // ---- 3. confidences: variance (input order) and the per-group sums ----------------------
     if constexpr (STAGED) stage(bufA, a.conf);
     double variance;
     {
@@ -344,7 +410,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) void tiebreak_lpm_kernel(TbArgs a
         vs += (t < n) ? bce_pow::pow2(at(bufA, a.conf, t < n ? t : last) - mean) : 0.0;
       variance = vs / nd;
     }
-    {
+    if (a.g_avgconf) {
       double gcs = 0.0;
       int cnt = 0;
 #pragma unroll
@@ -357,9 +423,10 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) void tiebreak_lpm_kernel(TbArgs a
           const bool end = (p + 1 >= n) || (g != (u[p + 1 < kTbLpmMax ? p + 1 : p] >> 5));
           gcs = (start ? 0.0 : gcs) + at(bufA, a.conf, t);  // tiebreak.py:61
           cnt = (start ? 0 : cnt) + 1;
-          if (end && a.g_avgconf) a.g_avgconf[off + (int64_t)g] = gcs / (double)cnt;
+          if (end) put(bufA, a.g_avgconf, (int)g, gcs / (double)cnt);
         }
       }
+      if constexpr (STAGED) flush(bufA, a.g_avgconf);
     }
     if (has) {
       if (n == 0) {  // tiebreak.py:86-87 (ValueError)

@@ -200,7 +200,7 @@ int bce_namespace_resolve(int64_t n, const double* rel0, const double* conf0, co
  * Per signal: pred (AgentSignal.prediction), conf, weight, rel (reliability_score).
  * Per market: winner (rounded group key, or the raw prediction for a single agent),
  * label (enum bce_tb_label; -1 for an empty market = the reference's ValueError),
- * n_groups, variance (unrounded population variance of conf, tiebreak.py:104-106).
+ * n_groups, variance (unrounded population variance of conf, tiebreak.py:108-110).
  * Per group, first-seen order, at CSR offsets: key, count, weight density, avg conf,
  * max reliability (tiebreak.py:58-71); per signal (nullable g_of) the ordinal of its group,
  * which lets a caller rebuild the reference's dict keys with their Python types (an int
@@ -208,8 +208,9 @@ int bce_namespace_resolve(int64_t n, const double* rel0, const double* conf0, co
  * DeterministicTieBreaker precision: CPython round(x, ndigits) restated exactly for
  * -15 <= ndigits <= 22, ndigits < -308 (signed zero) and ndigits > 323 (x itself); other
  * values return BCE_EUNSUPPORTED.
+ * Slots n_groups <= j < n of a market's per-group outputs are scratch (unspecified values).
  * bce_tiebreak_csr: markets market_list[0..n_list) (NULL = all), every length <= max_len
- * <= 64 (one wave per market).  bce_tiebreak_csr_long: markets of any length >= 1, max_len
+ * <= 64 (one lane per market up to 32 agents, one wave per market beyond).  bce_tiebreak_csr_long: markets of any length >= 1, max_len
  * >= every listed market's length (one workgroup per market; sorted in LDS up to 4096
  * agents, beyond that in a global scratch slice the library allocates on `stream`). */
 int bce_tiebreak_csr(const int64_t* offsets, int64_t n_markets, const int32_t* market_list,
@@ -273,8 +274,8 @@ int bce_reestimate_agreement_votes(const uint64_t* vote_bits, int64_t A, int64_t
                                    void* stream);
 /* BCE_MODE_FAST pass 1 of the single-read iteration on the matrix cores: w^T P with
  * v_mfma_f64_16x16x4_f64 (the north star's "MFMA contraction"), same outputs as
- * bce_reestimate_consensus_votes.  consensus within 2*A*2^-53 of the agent-order value;
- * markets within 4*A*2^-53 of 0.5 are redone in agent order, so vote_bits / cvote_words /
+ * bce_reestimate_consensus_votes.  consensus within 4*A*2^-53 of the agent-order value;
+ * markets within 8*A*2^-53 of 0.5 (or with a cell outside [0, 1]) are redone in agent order, so vote_bits / cvote_words /
  * ok_words -- and the agreement counts -- are identical to the exact pass.  scratch: device
  * buffer of bce_reestimate_mfma_scratch_bytes(M) bytes (8-byte aligned). */
 int bce_reestimate_consensus_votes_mfma(const double* P, int64_t A, int64_t M, int64_t ld, const double* w,

@@ -578,8 +578,8 @@ def test_tiebreak_variance_bit_exact_1m_markets():
 @pytest.mark.parametrize("A,M", [(5, 70), (17, 190), (300, 4097), (4100, 1000)])
 def test_reestimate_mfma_fast_mode_matches_exact_votes(A, M):
     """BCE_MODE_FAST pass 1 on the matrix cores (bce_reestimate_consensus_votes_mfma):
-    consensus within 2*A*2^-53 of the agent-order value (<= 1e-9), and -- because markets
-    within 4*A*2^-53 of 0.5 are redone in agent order -- vote bits, consensus votes,
+    consensus within 4*A*2^-53 of the agent-order value (<= 1e-9), and -- because markets
+    within 8*A*2^-53 of 0.5 (or with NaN cells) are redone in agent order -- vote bits, consensus votes,
     resolved masks, null flags and agreement counts identical to the exact pass.  Columns
     of mirrored pairs (x, 1-x) put the consensus at 0.5 up to rounding, so the redo runs."""
     import torch
@@ -624,6 +624,7 @@ def test_reestimate_mfma_fast_mode_matches_exact_votes(A, M):
         fin = np.isfinite(ce)
         assert np.array_equal(fin, np.isfinite(cf))
         dev = np.abs(cf[fin] - ce[fin])
-        assert dev.max(initial=0.0) <= 2 * (A + 2) * 2.0 ** -53 and dev.max(initial=0.0) <= 1e-9, wmode
-        near = fin & (np.abs(ce - 0.5) <= 2 * (A + 2) * 2.0 ** -53)
+        assert dev.max(initial=0.0) <= 4 * (A + 2) * 2.0 ** -53 and dev.max(initial=0.0) <= 1e-9, wmode
+        near = fin & (np.abs(ce - 0.5) <= 4 * (A + 2) * 2.0 ** -53)
         assert np.array_equal(cf[near], ce[near])  # the redone markets are exact
+        assert np.array_equal(np.isnan(cf), np.isnan(ce))  # NaN columns redone too
