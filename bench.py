@@ -358,7 +358,8 @@ def bench_c2(args, world, rank):
     achieved_gbs = bytes_per_launch / avg_kernel_s / 1e9
     # the kernel bce_consensus_csr picks (consensus.hip launch_seg_for_len)
     kernel = ("consensus_tab32_kernel" if 16 < L <= 32 and S <= 10112 else
-              "consensus_pipe_kernel" if L <= 32 and S <= 16384 and uniq else
+              "consensus_tab32_kernel<hybrid>" if 16 < L <= 32 and S <= (1 << 18) else
+              "consensus_pipe_kernel" if L <= 32 and uniq else
               "consensus_flat_kernel" if L <= 32 else "consensus_seg_kernel")
     traffic, _ = (read_pmc("pmc_c2.json", markets=M, signals_per_market=L, sources=S, kernel=kernel)
                   if uniq else (None, None))
