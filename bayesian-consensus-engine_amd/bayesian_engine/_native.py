@@ -21,7 +21,7 @@ LIB_PATH = os.environ.get("BCE_LIB", os.path.join(_PKG_ROOT, "lib", "libbce_hip.
 BCE_OK = 0
 MODE_EXACT = 0
 MODE_FAST = 1
-NBINS = 11
+NBINS = 13  # include/bce.h BCE_NBINS
 NO_TIMESTAMP = -(2**63)
 TB_LABELS = {0: "unanimous", 1: "weight_density", 2: "prediction_value_smallest", 3: "unanimous"}
 

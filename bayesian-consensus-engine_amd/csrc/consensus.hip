@@ -1571,7 +1571,7 @@ int launch_long_lds(const ConsArgs& a, hipStream_t st) {
 // packed 32-bit (sid, index) key fits, else the LDS-sort kernel.
 int launch_wide_for_len(int64_t max_len, const ConsArgs& a, hipStream_t st) {
   const int ib = wide_key_bits(max_len);
-  if ((int64_t)a.n_sources <= (1ll << (32 - ib))) return launch_wide_ib(ib, a, st);
+  if ((int64_t)a.n_sources <= (1ll << (32 - ib))) return launch_wide_len(max_len, a, st);
   return launch_long_lds(a, st);
 }
 
@@ -1682,8 +1682,8 @@ extern "C" int bce_consensus_csr(const int64_t* offsets, int64_t n_markets, cons
   return rc;
 }
 
-static_assert(BCE_NBINS == 11, "bin table");
-static const int64_t kBinMax[BCE_NBINS - 1] = {8, 16, 32, 64, 128, 256, 512, 1024, 2048, kLongMaxLds};
+static_assert(BCE_NBINS == 13, "bin table");
+static const int64_t kBinMax[BCE_NBINS - 1] = {8, 16, 32, 64, 128, 256, 512, 1024, 1536, 2048, 3072, kLongMaxLds};
 static int bin_of(int64_t n) {
   for (int b = 0; b < BCE_NBINS - 1; ++b)
     if (n <= kBinMax[b]) return b;

@@ -157,6 +157,6 @@ int launch_tab32(const ConsArgs& a, hipStream_t st);
 // Register-sort kernel (consensus_wide.hip) for 64 < n <= 4096: ib = log2 of the key's
 // index field (7..12, wide_key_bits(max_len)); needs n_sources <= 2^(32 - ib).
 int wide_key_bits(int64_t max_len);
-int launch_wide_ib(int ib, const ConsArgs& a, hipStream_t st);
+int launch_wide_len(int64_t max_len, const ConsArgs& a, hipStream_t st);
 
 }  // namespace bce

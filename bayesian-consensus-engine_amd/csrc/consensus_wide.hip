@@ -66,11 +66,16 @@ constexpr int ilog2c(int x) { return x <= 1 ? 0 : 1 + ilog2c(x >> 1); }
 #endif
 constexpr int kWaveRun = BCE_WIDE_KWR;  // FAST: duplicate runs longer than this are summed wave-wide
 
-template <int NW, int R, bool FAST>
+// NW waves (threads = 64*NW) hold P = 64*NW*R keys; the sort network spans NN >= NW waves
+// (PN = 64*NN*R, a power of two): NN > NW is a non-power-of-two bin -- the network's
+// missing waves hold +inf keys, so every exchange with them leaves the key in place and
+// they are never materialised (6 waves for 2049..3072 signals, 3 for 1025..1536).
+template <int NW, int R, bool FAST, int NN = NW>
 struct WideCfg {
   static constexpr int NT = 64 * NW;
   static constexpr int P = NT * R;
-  static constexpr int IB = ilog2c(P);
+  static constexpr int PN = 64 * NN * R;
+  static constexpr int IB = ilog2c(PN);
   static constexpr int XROW = R;      // exchange row (u32), two buffers
   static constexpr int HR = (R < BCE_WIDE_HR) ? R : BCE_WIDE_HR;
   // register budget: workgroups of >= 4 waves get 4 waves per SIMD (<= 128 VGPRs), so two
@@ -138,10 +143,11 @@ constexpr int xw_index(int K, int J, int R) {
   return idx;
 }
 
-// One stage of the flip-form bitonic network over P = 64*NW*R keys, position q = t*R + r:
+// One stage of the flip-form bitonic network over PN = 64*NN*R keys, position q = t*R + r:
 // the first stage of merge K pairs q with q ^ (K-1), the others pair q with q ^ J, and the
-// lower position always keeps the minimum -- no direction bits anywhere.
-template <int NW, int R, int K, int J>
+// lower position always keeps the minimum -- no direction bits anywhere.  Threads t >= 64*NW
+// (a non-power-of-two bin's missing waves) hold +inf: their partners keep their own keys.
+template <int NN, int NW, int R, int K, int J>
 __device__ __forceinline__ void wide_stage(unsigned (&key)[R], unsigned* sX, int t, int lane) {
   constexpr bool flip = (J == K / 2);
   if constexpr (flip ? (K <= R) : (J < R)) {  // inside a thread: min/max pairs
@@ -154,7 +160,7 @@ __device__ __forceinline__ void wide_stage(unsigned (&key)[R], unsigned* sX, int
         key[r2] = x < y ? y : x;
       }
     }
-  } else if constexpr (flip ? (K <= 64 * R) : (J < 64 * R)) {  // across lanes
+  } else if constexpr (flip ? (K <= 64 * R) : (J < 64 * R)) {  // across lanes (never crosses a wave)
     constexpr int MK = flip ? (K / R - 1) : (J / R);
     const bool lower = (lane & (flip ? (K / R / 2) : MK)) == 0;
     unsigned y[R];
@@ -172,9 +178,11 @@ __device__ __forceinline__ void wide_stage(unsigned (&key)[R], unsigned* sX, int
       *reinterpret_cast<uint4*>(buf + t * R + r) = make_uint4(key[r], key[r + 1], key[r + 2], key[r + 3]);
     __syncthreads();
     unsigned y[R];
+    const bool real = NN == NW || (t ^ MT) < 64 * NW;  // partner in a missing wave: +inf
 #pragma unroll
     for (int r = 0; r < R; r += 4) {
-      const uint4 y4 = *reinterpret_cast<const uint4*>(buf + (t ^ MT) * R + r);
+      const uint4 y4 = real ? *reinterpret_cast<const uint4*>(buf + (t ^ MT) * R + r)
+                            : make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
       y[r] = y4.x;
       y[r + 1] = y4.y;
       y[r + 2] = y4.z;
@@ -186,13 +194,13 @@ __device__ __forceinline__ void wide_stage(unsigned (&key)[R], unsigned* sX, int
       key[r] = ((key[r] < yr) == lower) ? key[r] : yr;
     }
   }
-  if constexpr (J > 1) wide_stage<NW, R, K, J / 2>(key, sX, t, lane);
+  if constexpr (J > 1) wide_stage<NN, NW, R, K, J / 2>(key, sX, t, lane);
 }
 
-template <int NW, int R, int K = 2>
+template <int NN, int NW, int R, int K = 2>
 __device__ __forceinline__ void wide_sort(unsigned (&key)[R], unsigned* sX, int t, int lane) {
-  wide_stage<NW, R, K, K / 2>(key, sX, t, lane);
-  if constexpr (K < 64 * NW * R) wide_sort<NW, R, 2 * K>(key, sX, t, lane);
+  wide_stage<NN, NW, R, K, K / 2>(key, sX, t, lane);
+  if constexpr (K < 64 * NN * R) wide_sort<NN, NW, R, 2 * K>(key, sX, t, lane);
 }
 
 // One fixed-order sum over the wave, returned in every lane: DPP rotations inside each
@@ -307,11 +315,11 @@ __device__ __forceinline__ void chain_add(double& acc, const double* src, int ce
   }
 }
 
-template <int NW, int R, bool FAST>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg<NW, R, FAST>::WPE, 8))) void consensus_wide_kernel(ConsArgs a) {
-  using Cfg = WideCfg<NW, R, FAST>;
+template <int NW, int R, bool FAST, int NN = NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg<NW, R, FAST, NN>::WPE, 8))) void consensus_wide_kernel(ConsArgs a) {
+  using Cfg = WideCfg<NW, R, FAST, NN>;
   constexpr int NT = Cfg::NT, P = Cfg::P, IB = Cfg::IB, HR = Cfg::HR;
-  constexpr unsigned QMASK = (unsigned)P - 1u;
+  constexpr unsigned QMASK = (unsigned)Cfg::PN - 1u;  // the input-index bits of a key
   constexpr int kNoErr = 0x7fffffff;
   __shared__ __attribute__((aligned(16))) double sA[Cfg::A_DBL];
   __shared__ __attribute__((aligned(16))) unsigned sB[Cfg::B_U32];
@@ -425,7 +433,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
     WMARK(0);
 
     // ---- 2. sort (core.py:103 order; ties in input order by the index bits) ----------
-    wide_sort<NW, R>(key, sX, t, lane);
+    wide_sort<NN, NW, R>(key, sX, t, lane);
     WMARK(1);
 
     // ---- 3. input-order probs + range check, sorted probs in place, leaders ----------
@@ -759,27 +767,29 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
 #endif
 }
 
-template <int NW, int R, bool FAST>
+template <int NW, int R, bool FAST, int NN = NW>
 int launch_wide(const ConsArgs& a, hipStream_t st) {
   if (a.n_list == 0) return BCE_OK;
-  const int per_cu = blocks_per_cu(reinterpret_cast<const void*>(&consensus_wide_kernel<NW, R, FAST>), 64 * NW, 0,
-                                   1, "consensus_wide_kernel");
+  const void* fn = reinterpret_cast<const void*>(&consensus_wide_kernel<NW, R, FAST, NN>);
+  const int per_cu = blocks_per_cu(fn, 64 * NW, 0, 1, "consensus_wide_kernel");
   const int64_t cap = (int64_t)cu_count() * per_cu;
   const int grid = (int)(a.n_list < cap ? a.n_list : cap);
-  hipLaunchKernelGGL((consensus_wide_kernel<NW, R, FAST>), dim3(grid), dim3(64 * NW), 0, st, a);
+  hipLaunchKernelGGL((consensus_wide_kernel<NW, R, FAST, NN>), dim3(grid), dim3(64 * NW), 0, st, a);
   return check_launch("consensus_wide_kernel");
 }
 
+// (NW, R[, NN]) per length bin: P = 64*NW*R >= max_len; the 1536 and 3072 bins run the
+// 2048 / 4096-key network on 3 / 6 waves
 template <bool FAST>
-int launch_wide_mode(int ib, const ConsArgs& a, hipStream_t st) {
-  switch (ib) {
-    case 7: return launch_wide<1, 2, FAST>(a, st);
-    case 8: return launch_wide<1, 4, FAST>(a, st);
-    case 9: return launch_wide<1, 8, FAST>(a, st);
-    case 10: return launch_wide<2, 8, FAST>(a, st);
-    case 11: return launch_wide<4, 8, FAST>(a, st);
-    default: return launch_wide<8, 8, FAST>(a, st);
-  }
+int launch_wide_mode(int64_t max_len, const ConsArgs& a, hipStream_t st) {
+  if (max_len <= 128) return launch_wide<1, 2, FAST>(a, st);
+  if (max_len <= 256) return launch_wide<1, 4, FAST>(a, st);
+  if (max_len <= 512) return launch_wide<1, 8, FAST>(a, st);
+  if (max_len <= 1024) return launch_wide<2, 8, FAST>(a, st);
+  if (max_len <= 1536) return launch_wide<3, 8, FAST, 4>(a, st);
+  if (max_len <= 2048) return launch_wide<4, 8, FAST>(a, st);
+  if (max_len <= 3072) return launch_wide<6, 8, FAST, 8>(a, st);
+  return launch_wide<8, 8, FAST>(a, st);
 }
 
 }  // namespace
@@ -826,8 +836,8 @@ int wide_key_bits(int64_t max_len) {
                                                                                                                  : 12;
 }
 
-int launch_wide_ib(int ib, const ConsArgs& a, hipStream_t st) {
-  return (a.mode == BCE_MODE_FAST) ? launch_wide_mode<true>(ib, a, st) : launch_wide_mode<false>(ib, a, st);
+int launch_wide_len(int64_t max_len, const ConsArgs& a, hipStream_t st) {
+  return (a.mode == BCE_MODE_FAST) ? launch_wide_mode<true>(max_len, a, st) : launch_wide_mode<false>(max_len, a, st);
 }
 
 }  // namespace bce

@@ -854,10 +854,10 @@ def c3_shards(args):
         wall, per = _timed(step, a2, 1, torch.cuda.current_stream(dev))
         N.check_faults(dev, f"c3 shard {r}/{w}")
         lens = np.diff(off)
-        bins = np.searchsorted([8, 16, 32, 64, 128, 256, 512, 1024, 2048, 4096], lens, side="left")
+        bins = np.searchsorted([8, 16, 32, 64, 128, 256, 512, 1024, 1536, 2048, 3072, 4096], lens, side="left")
         out = {"rank": r, "markets": int(len(lens)), "signals": int(off[-1]), "kernel_ms": per * 1e3,
                "wall_ms": wall / a2.steps * 1e3, "signals_per_bin": np.bincount(bins, weights=lens,
-                                                                              minlength=11).astype(int).tolist()}
+                                                                              minlength=13).astype(int).tolist()}
         del table, d_off, d_sid, d_prob, plan, res
         torch.cuda.empty_cache()
         return out

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define BCE_ABI_VERSION 2
+#define BCE_ABI_VERSION 3  /* 3: BCE_NBINS 13 (1536 and 3072 length bins), tie-break per-group scratch slots */
 
 enum bce_status {
     BCE_OK = 0,
@@ -127,7 +127,7 @@ int bce_validate_csr(const int64_t* offsets, int64_t n_markets, const double* pr
 /* Host-planned variant for ragged batches: the caller bins markets by length once
  * (bce_plan_bins on HOST offsets) and passes the device copy of the ordered market
  * list plus the bin boundaries.  bin_start has BCE_NBINS+1 entries (host array). */
-#define BCE_NBINS 11 /* n<=8, <=16, <=32, <=64, <=128, <=256, <=512, <=1024, <=2048, <=4096, >4096 */
+#define BCE_NBINS 13 /* n<=8, <=16, <=32, <=64, <=128, <=256, <=512, <=1024, <=1536, <=2048, <=3072, <=4096, >4096 */
 int bce_plan_bins(const int64_t* offsets_host, int64_t n_markets, int32_t* order_host,
                   int64_t* bin_start_host, int32_t* max_len_host);
 /* Bytes of device scratch bce_consensus_planned needs for the >4096 bin. */

@@ -57,7 +57,8 @@ def _check(g, mode="exact", **kw):
     _compare_vec(_run(g, mode=mode, **kw), exp, g["offsets"], exact=(mode == "exact"))
 
 
-EDGES = [65, 127, 128, 129, 255, 256, 257, 511, 512, 513, 1023, 1024, 1025, 2047, 2048, 2049, 4095, 4096]
+EDGES = [65, 127, 128, 129, 255, 256, 257, 511, 512, 513, 1023, 1024, 1025, 1535, 1536, 1537, 2047, 2048, 2049,
+         3071, 3072, 3073, 4095, 4096]
 
 
 MODES = ["exact", "fast"]
@@ -92,6 +93,19 @@ def test_wide_fast_mode_c3_shaped():
     again = _run(g, mode="fast")
     for k in ("consensus", "confidence", "total_weight", "nweight"):
         assert np.array_equal(out[k], again[k], equal_nan=True), k
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("top", [1536, 3072])
+def test_wide_non_power_of_two_bins_direct(top, mode):
+    """bce_consensus_csr with max_len 1536 / 3072 launches the 3- / 6-wave kernels whose
+    sort network has missing +inf waves (every market at most `top` long, hot sources,
+    NaN and out-of-range probabilities, empty markets)."""
+    rng = np.random.default_rng(top)
+    lens = rng.integers(top // 2 + 1, top + 1, 150)
+    lens[:6] = [top, top - 1, top // 2 + 1, 0, 65, 1]
+    g = _zipf_case(lens, 300_000, top, base=5)
+    _check(g, mode, max_len=top)
 
 
 def test_wide_key_limit_and_fallback():

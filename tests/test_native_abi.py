@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_device_count():
     lib = N.load_library()
-    assert lib.bce_abi_version() == 2
+    assert lib.bce_abi_version() == 3
     assert lib.bce_device_count() >= 0
 
 
@@ -47,16 +47,16 @@ def test_argument_errors_need_no_gpu():
 def test_plan_bins_host():
     lib = N.load_library()
     rng = np.random.default_rng(0)
-    lens = np.concatenate([[0, 8, 9, 16, 17, 32, 33, 64, 65, 128, 129, 256, 257, 512, 513, 1024, 1025, 2048,
-                            2049, 4096, 4097], rng.integers(0, 6000, 300)])
+    lens = np.concatenate([[0, 8, 9, 16, 17, 32, 33, 64, 65, 128, 129, 256, 257, 512, 513, 1024, 1025, 1536,
+                            1537, 2048, 2049, 3072, 3073, 4096, 4097], rng.integers(0, 6000, 300)])
     off = np.zeros(len(lens) + 1, np.int64)
     off[1:] = np.cumsum(lens)
     order = np.zeros(len(lens), np.int32)
     bins = np.zeros(N.NBINS + 1, np.int64)
     mx = np.zeros(1, np.int32)
     assert lib.bce_plan_bins(N.ptr(off), len(lens), N.ptr(order), N.ptr(bins), N.ptr(mx)) == 0
-    edges = [0, 8, 16, 32, 64, 128, 256, 512, 1024, 2048, 4096, 1 << 62]
-    assert N.NBINS == 11
+    edges = [0, 8, 16, 32, 64, 128, 256, 512, 1024, 1536, 2048, 3072, 4096, 1 << 62]
+    assert N.NBINS == 13
     for b in range(N.NBINS):
         ms = order[bins[b]:bins[b + 1]]
         assert np.all(np.diff(ms) > 0)  # ascending inside a bin
@@ -65,7 +65,7 @@ def test_plan_bins_host():
     assert sorted(order.tolist()) == list(range(len(lens)))
     assert mx[0] == lens.max()
     sb = lib.bce_consensus_scratch_bytes(N.ptr(off), N.ptr(order), N.ptr(bins))
-    n_huge = int(bins[11] - bins[10])
+    n_huge = int(bins[13] - bins[12])
     P = 1 << int(np.ceil(np.log2(lens[lens > 4096].max())))
     assert sb == min(n_huge, 512) * 4 * P * 8
 
