@@ -48,9 +48,7 @@ __device__ __forceinline__ double key_f64(uint64_t k) {
   return __longlong_as_double((long long)u);
 }
 
-#ifndef BCE_AGG_CAP
-#define BCE_AGG_CAP 0  // workgroups per CU (0: one workgroup per group: -15% against 8 per CU)
-#endif
+// One workgroup per group (no per-CU cap): -15% against 8 looping workgroups per CU.
 constexpr int kAggT = 256;
 constexpr int kAggPer = 4;                  // members per thread per chunk
 constexpr int kAggCh = kAggT * kAggPer;     // chunk = 1024 members, list order r-major
@@ -226,7 +224,7 @@ extern "C" int bce_aggregate_groups(const int64_t* group_offsets, int64_t n_grou
   AggArgs a{group_offsets, n_groups, members, n_markets, consensus, confidence, has_consensus,
             wavg, median, majority, mean_conf, n_included};
   int64_t grid = n_groups;
-  const int64_t cap = BCE_AGG_CAP > 0 ? (int64_t)cu_count() * BCE_AGG_CAP : ((int64_t)1 << 30);
+  const int64_t cap = (int64_t)1 << 30;
   if (grid > cap) grid = cap;
   hipLaunchKernelGGL(aggregate_kernel, dim3((unsigned)grid), dim3(kAggT), 0, as_stream(stream), a);
   return check_launch("aggregate_kernel");

@@ -27,21 +27,11 @@
 
 #pragma clang fp contract(off)
 
-#ifndef BCE_SEG_WPE
-#define BCE_SEG_WPE 1  // __launch_bounds__ min waves per SIMD for the segment kernel
-#endif
-#ifndef BCE_FLAT_TM
-#define BCE_FLAT_TM 64
-#endif
-#ifndef BCE_FLAT_RING
-#define BCE_FLAT_RING 8  // relconf gathers in flight per lane
-#endif
-#ifndef BCE_FLAT_WPE
-#define BCE_FLAT_WPE 1  // min waves per SIMD (register budget) for the flat kernel
-#endif
-#ifndef BCE_FLAT_WPB
-#define BCE_FLAT_WPB 2
-#endif
+constexpr int kSegWPE = 1;    // __launch_bounds__ min waves per SIMD for the segment kernel
+constexpr int kFlatTM = 64;   // flat kernel: markets per wave tile
+constexpr int kFlatRing = 8;  // flat kernel: relconf gathers in flight per lane
+constexpr int kFlatWPE = 1;   // flat kernel: min waves per SIMD (register budget)
+constexpr int kFlatWPB = 2;   // flat kernel: waves per workgroup
 
 namespace bce {
 
@@ -49,7 +39,7 @@ namespace bce {
 // short markets: wave-per-tile, lane-per-signal then lane-per-market
 // ------------------------------------------------------------------------------------
 template <int G, int TM>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BCE_SEG_WPE, 8)))
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kSegWPE, 8)))
 void consensus_seg_kernel(ConsArgs a) {
   static_assert(G == 8 || G == 16 || G == 32 || G == 64, "segment width");
   constexpr int SPR = kWave / G;   // segments (markets) per round
@@ -512,7 +502,7 @@ constexpr int kPackSlot = 25;  // packed = sid | slot << 25 (sid < 2^25)
 __device__ double2 kColdRow[1] = {{0.5, 0.25}};  // DEFAULT_RELIABILITY / _CONFIDENCE
 
 template <int G, int TM, int WPB>
-__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(BCE_FLAT_WPE, 8)))
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(kFlatWPE, 8)))
 void consensus_flat_kernel(ConsArgs a) {
   static_assert(G == 8 || G == 16 || G == 32, "flat widths");
   static_assert(TM == 32 || TM == 64, "markets per wave tile");
@@ -520,7 +510,7 @@ void consensus_flat_kernel(ConsArgs a) {
   constexpr int TS = TM * G;           // max signals per tile
   constexpr int SW = TS + 8 + G;       // sid image (dwords): alignment slack, row overrun, sink
   constexpr int PW = TS + 4 + G;       // prob image (doubles)
-  constexpr int RING = BCE_FLAT_RING;
+  constexpr int RING = kFlatRing;
   constexpr int P = G / 2;             // lanes per market in the copy-out (2 slots each)
   constexpr int MPI = kWave / P;       // markets per copy-out iteration
 
@@ -777,23 +767,17 @@ void consensus_flat_kernel(ConsArgs a) {
 // never touches registers the compute waves need.  Flags live in LDS (one workgroup).
 // Progress: the loader only waits for the release of sequence i-R, which a compute wave
 // is processing or has released (sequences are grabbed in order and R > C).
-#ifndef BCE_PIPE_RING
-#define BCE_PIPE_RING 16  // relconf gathers in flight per compute lane
-#endif
+constexpr int kPipeRing = 16;  // relconf gathers in flight per compute lane
 
-#ifndef BCE_PIPE_C32
-#define BCE_PIPE_C32 4  // compute waves at G = 32
-#endif
-#ifndef BCE_PIPE_R32
-#define BCE_PIPE_R32 6  // slots at G = 32 (LDS: ~25 KB each)
-#endif
+constexpr int kPipeC32 = 4;  // compute waves at G = 32
+constexpr int kPipeR32 = 6;  // slots at G = 32 (LDS: ~25 KB each)
 // Slots R >= C + 2: with one spare slot the ring is load-latency bound (a released slot
 // must be refilled within tile_time / C); two spares keep two tiles in flight.
 template <int G>
 struct PipeCfg {
   static constexpr int L = 1;  // one loader wave (two measured slower: TA contention)
-  static constexpr int C = (G == 32) ? BCE_PIPE_C32 : 6;
-  static constexpr int R = (G == 32) ? BCE_PIPE_R32 : C + 3;
+  static constexpr int C = (G == 32) ? kPipeC32 : 6;
+  static constexpr int R = (G == 32) ? kPipeR32 : C + 3;
 };
 
 template <int G>
@@ -821,7 +805,7 @@ void consensus_pipe_kernel(ConsArgs a) {
   constexpr int OW = OCH + 2;
   static_assert(4 * kWave * (NSI - 1) <= SW && 2 * kWave * (NPI - 1) <= PW && kWave * (NOI - 1) <= OW,
                 "every body-instruction lane lands inside its image");
-  constexpr int RING = BCE_PIPE_RING;
+  constexpr int RING = kPipeRing;
   constexpr int NG = (G < RING) ? G : RING;
   constexpr int PA = 4;          // probabilities read this many positions ahead
 
@@ -1522,7 +1506,7 @@ int launch_pipe(const ConsArgs& a, hipStream_t st) {
 
 template <int G>
 int launch_flat(const ConsArgs& a, hipStream_t st) {
-  constexpr int TM = BCE_FLAT_TM, WPB = BCE_FLAT_WPB;
+  constexpr int TM = kFlatTM, WPB = kFlatWPB;
   const int64_t tiles = (a.n_list + TM - 1) / TM;
   if (tiles == 0) return BCE_OK;
   const int per_cu = blocks_per_cu(reinterpret_cast<const void*>(&consensus_flat_kernel<G, TM, WPB>), 64 * WPB, 0, 2,

@@ -37,34 +37,15 @@
 
 #pragma clang fp contract(off)
 
-#ifndef BCE_WIDE_HR
-#define BCE_WIDE_HR 2  // rounds of NT uniques whose gathers are in flight together
-#endif
-#ifndef BCE_WIDE_WPE_BIG
-#define BCE_WIDE_WPE_BIG 4  // the same for workgroups of >= 4 waves
-#endif
-#ifndef BCE_WIDE_WPE
-#define BCE_WIDE_WPE 4  // min waves per SIMD (register budget; 4 vs 2: exact -1.3%, fast unchanged)
-#endif
-#ifndef BCE_WIDE_PROF
-#define BCE_WIDE_PROF 0  // experiment builds only (tools/wide_variants.py): per-phase s_memtime
-#endif
+constexpr int kWideHR = 2;       // rounds of NT uniques whose gathers are in flight together
+constexpr int kWideWPE = 4;      // min waves per SIMD (register budget; 4 vs 2: exact -1.3%, fast unchanged)
+constexpr int kWideNWBF = 4;     // FAST nweight read-backs per batch (1: 1.645, 2: 1.634, 4: 1.587 ms C3)
 
 namespace bce {
 namespace {
 
-#if BCE_WIDE_PROF
-__device__ unsigned long long g_wide_prof[8];
-#define WMARK(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); prof[k] += t_ - prof_t; prof_t = t_; } while (0)
-#else
-#define WMARK(k) do {} while (0)
-#endif
-
 constexpr int ilog2c(int x) { return x <= 1 ? 0 : 1 + ilog2c(x >> 1); }
-#ifndef BCE_WIDE_KWR
-#define BCE_WIDE_KWR 48
-#endif
-constexpr int kWaveRun = BCE_WIDE_KWR;  // FAST: duplicate runs longer than this are summed wave-wide
+constexpr int kWaveRun = 48;  // FAST: duplicate runs longer than this are summed wave-wide
 
 // NW waves (threads = 64*NW) hold P = 64*NW*R keys; the sort network spans NN >= NW waves
 // (PN = 64*NN*R, a power of two): NN > NW is a non-power-of-two bin -- the network's
@@ -77,10 +58,10 @@ struct WideCfg {
   static constexpr int PN = 64 * NN * R;
   static constexpr int IB = ilog2c(PN);
   static constexpr int XROW = R;      // exchange row (u32), two buffers
-  static constexpr int HR = (R < BCE_WIDE_HR) ? R : BCE_WIDE_HR;
+  static constexpr int HR = (R < kWideHR) ? R : kWideHR;
   // register budget: workgroups of >= 4 waves get 4 waves per SIMD (<= 128 VGPRs), so two
   // LDS-sized workgroups share a CU
-  static constexpr int WPE = (NW >= 4 && BCE_WIDE_WPE < BCE_WIDE_WPE_BIG) ? BCE_WIDE_WPE_BIG : BCE_WIDE_WPE;
+  static constexpr int WPE = kWideWPE;
   static constexpr int A_DBL = P + 64;  // + the run sums' read-ahead
   // region B (u32): sort exchange rows, then leaders [P] (+ exact: chain buffers
   // [2][3][NT] doubles + the chain's read-ahead)
@@ -260,15 +241,6 @@ __device__ __forceinline__ double run_sum(const double* rp, int len) {
 // other's dependent adds (the compiler would copy loop-carried batch registers behind an
 // lgkmcnt(0)).  The < 8-term tail is added in C++ with masked terms adding +0.0 -- exact,
 // because these chains never hold -0.0.  src is 16-B aligned; reads may run 8 past ce.
-#ifndef BCE_WIDE_PIPE
-#define BCE_WIDE_PIPE 1
-#endif
-#ifndef BCE_WIDE_NWB
-#define BCE_WIDE_NWB 1  // normalizedWeight: batched read-backs
-#endif
-#ifndef BCE_WIDE_NWBF
-#define BCE_WIDE_NWBF 4  // FAST: read-backs per batch (1: 1.645, 2: 1.634, 4: 1.587 ms C3)
-#endif
 __device__ __forceinline__ void chain_add(double& acc, const double* src, int ce) {
   const int nfull = ce & ~7;
   if (nfull) {
@@ -341,9 +313,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
   // in workgroups of several waves (it saves their barriers); a single wave parks w[j] in
   // region A (dead sorted-prob slot j), which is faster than the global round trip.
   const bool wback = (NW > 1) && a.weight != nullptr;
-#if BCE_WIDE_PROF
-  unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prof_t = __builtin_amdgcn_s_memtime();
-#endif
 
   // Market metadata for this workgroup's next 64 markets (li = base + G*k on lane k) is
   // loaded in one vector batch, so picking a market is a readlane, never a scalar-load
@@ -430,11 +399,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
       continue;
     }
     if (t == 0) sErr = kNoErr;
-    WMARK(0);
 
     // ---- 2. sort (core.py:103 order; ties in input order by the index bits) ----------
     wide_sort<NN, NW, R>(key, sX, t, lane);
-    WMARK(1);
 
     // ---- 3. input-order probs + range check, sorted probs in place, leaders ----------
     if (lane == 63) sLast[wv] = key[R - 1];
@@ -482,7 +449,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
       sDone = 0;
     }
     __syncthreads();  // (c) sorted probs + leaders visible
-    WMARK(2);
 
     // ---- 4. per-unique products --------------------------------------------------------
     double acc = 0.0;                     // exact: wave 0 lanes 0..2 carry the chains
@@ -491,7 +457,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
     // wave 0 only carries the chains while waves 1.. produce rounds of NP = NT - 64
     // uniques into a two-slot LDS ring, handed over with LDS counters instead of barriers,
     // so the serial chains overlap the gathers and run sums of the next rounds.
-    const bool piped = BCE_WIDE_PIPE && !FAST && NW > 1 && wback;
+    const bool piped = !FAST && NW > 1 && wback;
     if (piped) {
       constexpr int NP = (NW > 1) ? NT - 64 : NT;
       const int nrp = (u + NP - 1) / NP;
@@ -608,10 +574,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
           }
         }
       }
-#if BCE_WIDE_PROF
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // diagnostic: gather latency as its own phase
-      WMARK(7);
-#endif
       double vw[HR], va[HR], vc[HR];
 #pragma unroll
       for (int i = 0; i < HR; ++i) {
@@ -643,7 +605,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
           vc[i] = rc[i].y * w;    // core.py:142
         }
       }
-      WMARK(3);
       if constexpr (FAST) {
 #pragma unroll
         for (int i = 0; i < HR; ++i) {  // round order: fixed per thread
@@ -668,7 +629,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
             buf[NT + t] = va[i];
             buf[2 * NT + t] = vc[i];
             __syncthreads();  // round staged; every sorted-prob read of this group is done
-            WMARK(4);
             const int jj = (h + i) * NT + t;
             if (jj < u && !wback) sA[jj] = vw[i];  // slot jj is only read by uniques <= jj
             if (wv == 0) {
@@ -677,7 +637,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
               chain_add(acc, buf + (lane % 3) * NT, ce);
               __builtin_amdgcn_s_setprio(0);
             }
-            WMARK(5);
           }
         }
       }
@@ -692,7 +651,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
           if (a.weight) a.weight[p] = vw[i];
         }
       }
-      WMARK(3);
     }
 
     // ---- 5. next market's probabilities; totals, per-market outputs, nweight ---------
@@ -727,10 +685,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
       if (a.err_idx) a.err_idx[m] = (sErr == kNoErr) ? -1 : sErr;
     }
     if (a.nweight) {  // core.py:151
-      if constexpr (BCE_WIDE_NWB && !FAST) {
+      if constexpr (!FAST) {
         // every read-back issued before any nweight store: loads retire behind earlier
         // stores (vmcnt is in order), so a load/store per iteration waits out each store
-        // (C3 exact -2.6%; FAST: batches of BCE_WIDE_NWBF, a full batch costs it spills)
+        // (C3 exact -2.6%; FAST: batches of kWideNWBF, a full batch costs it spills)
         double wj[R];
 #pragma unroll
         for (int k = 0; k < R; ++k) {
@@ -743,7 +701,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
           if (jj < u) a.nweight[off + jj] = (tw > 0.0) ? wj[k] / tw : 0.0;
         }
       } else {
-        constexpr int NB = (BCE_WIDE_NWBF < R) ? BCE_WIDE_NWBF : R;  // read-backs per batch
+        constexpr int NB = (kWideNWBF < R) ? kWideNWBF : R;  // read-backs per batch
         for (int j0 = t; j0 < u; j0 += NB * NT) {
           double wj[NB];
 #pragma unroll
@@ -759,12 +717,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
         }
       }
     }
-    WMARK(6);
   }
-#if BCE_WIDE_PROF
-  if (lane_id() == 0)
-    for (int k = 0; k < 8; ++k) atomicAdd(&g_wide_prof[k], prof[k]);
-#endif
 }
 
 template <int NW, int R, bool FAST, int NN = NW>
@@ -794,14 +747,6 @@ int launch_wide_mode(int64_t max_len, const ConsArgs& a, hipStream_t st) {
 
 }  // namespace
 
-#if BCE_WIDE_PROF
-extern "C" int bce_wide_prof_read(unsigned long long* host8) {
-  BCE_HIP(hipMemcpyFromSymbol(host8, HIP_SYMBOL(g_wide_prof), 8 * sizeof(unsigned long long)));
-  unsigned long long z[8] = {0};
-  BCE_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_wide_prof), z, sizeof z));
-  return BCE_OK;
-}
-#endif
 
 namespace {
 __global__ void lane_xor_selftest_kernel(unsigned* out) {

@@ -110,39 +110,21 @@ __global__ __launch_bounds__(256) void outcome_update_kernel(int64_t n, double* 
   }
 }
 
-#ifndef BCE_EW_NT
-#define BCE_EW_NT 2  // nontemporal hints (build knob): bit 0 view stores, bit 1 rel/t loads (on), bit 2 conf load (with bit 1)
-#endif
+// Nontemporal rel / t loads (C4 0.085 -> 0.080 ms); nt view stores and an nt conf load
+// measured slower (measurements/c3_c4_nt_variants_r02.jsonl).
 typedef double ew_d2v __attribute__((ext_vector_type(2)));
 typedef long long ew_l2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ double2 ew_ld(const double2* p) {
-  if constexpr ((BCE_EW_NT & 2) != 0) {
-    const ew_d2v v = __builtin_nontemporal_load(reinterpret_cast<const ew_d2v*>(p));
-    return make_double2(v.x, v.y);
-  } else {
-    return *p;
-  }
+  const ew_d2v v = __builtin_nontemporal_load(reinterpret_cast<const ew_d2v*>(p));
+  return make_double2(v.x, v.y);
 }
 __device__ __forceinline__ longlong2 ew_ld(const longlong2* p) {
-  if constexpr ((BCE_EW_NT & 2) != 0) {
-    const ew_l2v v = __builtin_nontemporal_load(reinterpret_cast<const ew_l2v*>(p));
-    return make_longlong2(v.x, v.y);
-  } else {
-    return *p;
-  }
+  const ew_l2v v = __builtin_nontemporal_load(reinterpret_cast<const ew_l2v*>(p));
+  return make_longlong2(v.x, v.y);
 }
-__device__ __forceinline__ void ew_st_view(double2* p, double x0, double x1) {
-  if constexpr ((BCE_EW_NT & 1) != 0) {
-    const ew_d2v v = {x0, x1};
-    __builtin_nontemporal_store(v, reinterpret_cast<ew_d2v*>(p));
-  } else {
-    *p = make_double2(x0, x1);
-  }
-}
+__device__ __forceinline__ void ew_st_view(double2* p, double x0, double x1) { *p = make_double2(x0, x1); }
 
-#ifndef BCE_EW_GRID_CAP
-#define BCE_EW_GRID_CAP 0  // one thread per work item: C4 -4%, f3 -5.5% against 16 workgroups per CU
-#endif
+// Grids are one thread per work item (C4 -4%, f3 -5.5% against 16 workgroups per CU).
 
 // Config-4 step.  Absent rows must carry the baked cold-start values
 // (rel = default_rel, conf = default_conf, t = BCE_NO_TIMESTAMP), so the view needs no
@@ -162,8 +144,7 @@ __global__ __launch_bounds__(256) void replay_step_kernel(int64_t n, double* __r
     const unsigned f = (fb >> ((i & 1) * 4)) & 0xF;  // 2 bits per source, sources 2i, 2i+1
     ew_st_view(reinterpret_cast<double2*>(view) + i, decayed(r.x, t.x, k), decayed(r.y, t.y, k));
     if (f & 0x5) {  // any participant in the pair
-      double2 c = ((BCE_EW_NT & 4) != 0) ? ew_ld(reinterpret_cast<const double2*>(conf) + i)
-                                           : reinterpret_cast<const double2*>(conf)[i];
+      double2 c = reinterpret_cast<const double2*>(conf)[i];
       if (f & 1) {
         update_one(r.x, c.x, (f & 2) != 0);
         t.x = k.now_us;
@@ -257,9 +238,8 @@ __global__ __launch_bounds__(256) void namespace_resolve_kernel(int64_t n, NsArg
 
 static int grid_for(int64_t work, int threads) {
   int64_t g = (work + threads - 1) / threads;
-  // BCE_EW_GRID_CAP workgroups per CU (0: one thread per work item, the grid-stride loops
-  // run once)
-  const int64_t cap = BCE_EW_GRID_CAP > 0 ? (int64_t)cu_count() * BCE_EW_GRID_CAP : ((int64_t)1 << 30);
+  // one thread per work item (the grid-stride loops run once)
+  const int64_t cap = (int64_t)1 << 30;
   if (g > cap) g = cap;
   if (g < 1) g = 1;
   return (int)g;

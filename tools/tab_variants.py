@@ -52,7 +52,8 @@ VARIANTS = {
 }
 
 
-def _patched_src(name):
+def _patched_src(name, variants=None):
+    variants = VARIANTS if variants is None else variants
     # pkg/csrc + include side by side, as in the repo (csrc includes ../../include/bce.h)
     top = os.path.join(OUT, name, "tree")
     if os.path.isdir(top):
@@ -60,7 +61,7 @@ def _patched_src(name):
     d = os.path.join(top, "pkg", "csrc")
     shutil.copytree(CSRC, d)
     shutil.copytree(os.path.join(ROOT, "include"), os.path.join(top, "include"))
-    for fn, old, new in VARIANTS[name]:
+    for fn, old, new in variants[name]:
         path = os.path.join(d, fn)
         text = open(path).read()
         if old not in text:
@@ -70,11 +71,11 @@ def _patched_src(name):
     return d
 
 
-def build(names):
+def build(names, variants=None):
     procs = []
     for name in names:
         d = os.path.join(OUT, name)
-        src = _patched_src(name)
+        src = _patched_src(name, variants)
         objs = []
         for fn in SRCS:
             o = os.path.join(d, fn.replace(".hip", ".o"))
