@@ -19,6 +19,6 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $o/fetch -o run --output-forma
   python3 bench.py --no-cpu-baseline --steps 5 --warmup 2 --prewarm-s 0 "$@" > $o/fetch.log 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $o/write -o run --output-format csv -- \
   python3 bench.py --no-cpu-baseline --steps 5 --warmup 2 --prewarm-s 0 "$@" > $o/write.log 2>&1 || exit $?
-python3 tools/pmc_summary.py stats $o/stats "$kern" > $o/stats_summary.json
+python3 tools/pmc_summary.py stats $o/stats "$kern" 50 > $o/stats_summary.json
 cp $o/stats/run_kernel_stats.csv $o/kernel_stats.csv 2>/dev/null || find $o/stats -name '*kernel_stats.csv' -exec cp {} $o/kernel_stats.csv \;
 python3 tools/pmc_summary.py pmc $o/fetch $o/write "$kern" $o/pmc.json "${meta[@]}"

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 output for one kernel (experiment tooling, not product code).
 
-  python tools/pmc_summary.py stats <dir> <kernel-substring>
-      average duration (ms) from the *kernel_stats.csv of a --kernel-trace --stats run
+  python tools/pmc_summary.py stats <dir> <kernel-substring> [last]
+      average duration (ms) from the *kernel_stats.csv of a --kernel-trace --stats run (and of
+      the last `last` dispatches in the kernel trace: the timed steps)
   python tools/pmc_summary.py pmc <fetch-dir> <write-dir> <kernel-substring> <out.json> [k=v ...]
       (steps_total=N: sum every matching dispatch and divide by N -- per step of a
       multi-kernel config -- instead of averaging per dispatch)
@@ -40,6 +41,15 @@ def stats(d, kern):
     raise SystemExit(f"kernel {kern} not in stats")
 
 
+def steady(d, kern, last):
+    """Average duration (ms) of the last `last` dispatches of the kernel in the trace: the
+    timed steps, without the clock ramp and warmup dispatches the --stats average includes."""
+    rows = [r for r in _rows(d, "*kernel_trace.csv") if kern in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows[-last:]]
+    return sum(durs) / len(durs) if durs else None
+
+
 def counter(d, kern, name, per_step=None):
     vals = [float(r["Counter_Value"]) for r in _rows(d, "*counter_collection.csv")
             if kern in r.get("Kernel_Name", "") and r.get("Counter_Name") == name]
@@ -54,7 +64,10 @@ def counter(d, kern, name, per_step=None):
 def main():
     if sys.argv[1] == "stats":
         ms, calls, name = stats(sys.argv[2], sys.argv[3])
-        print(json.dumps({"kernel": name, "avg_ms": ms, "calls": calls}))
+        out = {"kernel": name, "avg_ms": ms, "calls": calls}
+        if len(sys.argv) > 4:  # the timed steps alone
+            out[f"avg_ms_last_{sys.argv[4]}"] = steady(sys.argv[2], sys.argv[3], int(sys.argv[4]))
+        print(json.dumps(out))
         return
     fdir, wdir, kern, out = sys.argv[2:6]
     meta = {}
