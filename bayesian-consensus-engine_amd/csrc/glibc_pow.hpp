@@ -107,8 +107,26 @@ BCE_POW_FN double exp_inline(double x, double xtail) {
   return __builtin_fma(scale, tmp, scale);
 }
 
-// pow(x, 2.0) as glibc 2.35 (x86_64, FMA build) returns it, for every double x
+// pow(x, 2.0) as glibc 2.35 (x86_64, FMA build) returns it, for every double x.
+// Fast path: the library's result is within 0.52 ulp of the exact square (its documented
+// bound; the approximation error is ~2^-64 relative), so when the exact square's rounding
+// error lo = fma(x, x, -hi) is below 0.4 ulp of hi = x*x -- and hi is a normal number that is
+// not a power of two (uniform spacing on both sides) -- hi is the only double within reach
+// and pow returns it.  Only ~0.1% of inputs (near-midpoint squares, tiny or huge results)
+// take the restated algorithm below; tools/pow2_check.cpp checks both paths against libm.
+BCE_POW_FN double pow2_full(double x);
 BCE_POW_FN double pow2(double x) {
+  const double hi = x * x;
+  const double lo = __builtin_fma(x, x, -hi);
+  const uint64_t b = asu(hi);
+  if (hi >= 0x1p-1000 && hi < 0x1p1000 && (b & 0xFFFFFFFFFFFFFull) != 0) {
+    const double ulp = asd(b + 1) - hi;
+    if (__builtin_fabs(lo) < 0.4 * ulp) return hi;
+  }
+  return pow2_full(x);
+}
+
+BCE_POW_FN double pow2_full(double x) {
   uint64_t ix = asu(x);
   uint32_t topx = top12(x);
   if (topx - 0x001 >= 0x7ff - 0x001) {  // x <= 0, subnormal, inf or nan
