@@ -154,15 +154,19 @@ __device__ __forceinline__ void wide_stage(unsigned (&key)[R], unsigned* sX, int
     constexpr int MT = flip ? (K / R - 1) : (J / R);
     unsigned* const buf = sX + (xw_index(K, J, R) & 1) * (64 * NW * R);
     const bool lower = (t & (flip ? (K / R / 2) : MT)) == 0;
+    // planes of 4 keys: key r of thread t at (r/4)*NT*4 + t*4 + r%4, so every 16-B access
+    // of a wave covers 1 KB of consecutive words (a thread-major row of R keys put lanes 32 B
+    // apart: two lanes per bank group, a 2-way conflict on every exchange)
+    constexpr int PL = 4 * 64 * NW;  // words per plane
 #pragma unroll
     for (int r = 0; r < R; r += 4)
-      *reinterpret_cast<uint4*>(buf + t * R + r) = make_uint4(key[r], key[r + 1], key[r + 2], key[r + 3]);
+      *reinterpret_cast<uint4*>(buf + (r >> 2) * PL + t * 4) = make_uint4(key[r], key[r + 1], key[r + 2], key[r + 3]);
     __syncthreads();
     unsigned y[R];
     const bool real = NN == NW || (t ^ MT) < 64 * NW;  // partner in a missing wave: +inf
 #pragma unroll
     for (int r = 0; r < R; r += 4) {
-      const uint4 y4 = real ? *reinterpret_cast<const uint4*>(buf + (t ^ MT) * R + r)
+      const uint4 y4 = real ? *reinterpret_cast<const uint4*>(buf + (r >> 2) * PL + (t ^ MT) * 4)
                             : make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
       y[r] = y4.x;
       y[r + 1] = y4.y;
