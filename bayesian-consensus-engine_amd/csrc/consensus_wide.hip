@@ -308,6 +308,15 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
   unsigned* const sX = sB;                                            // sort exchange rows
   unsigned* const sLead = sB;                                         // [u] sid<<IB | q0
   double* const sWAC = reinterpret_cast<double*>(sB + P);             // exact: [2][3][NT]
+  // FAST: the region past the leaders (the dead exchange rows) parks w[j] for normalizedWeight
+  // when the market's uniques fit -- C3's Zipf markets have u <= 0.55 n, which fits in ~all
+  // of them -- instead of reading the weight output back (each load there waits for this
+  // thread's earlier stores to retire: vmcnt is in order)
+  // (race-free: the next market's first wave-crossing stage writes exchange buffer 0 =
+  // sB[0, P); buffer 1 = sB[P, 2P) is written only after that stage's barrier, which every
+  // thread reaches after its own tail)
+  constexpr int WFREE = FAST ? (Cfg::B_U32 - P) / 2 : 0;
+  double* const sW = reinterpret_cast<double*>(sB + P);
 
   const int t = threadIdx.x;
   const int lane = lane_id();
@@ -557,6 +566,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
       }
     }
     const int nr = piped ? 0 : (u + NT - 1) / NT;
+    const bool park = FAST && wback && u <= WFREE;
     for (int h = 0; h < nr; h += HR) {
       double2 rc[HR];
       int q0s[HR], q1s[HR];
@@ -653,6 +663,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
           if (a.usid)
             a.usid[p] = (int32_t)sids[i] | (((pwd[i] >> (sids[i] & 31)) & 1u) ? 0 : (int32_t)0x80000000);
           if (a.weight) a.weight[p] = vw[i];
+          if (park) sW[jj] = vw[i];
         }
       }
     }
@@ -711,7 +722,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
 #pragma unroll
           for (int k = 0; k < NB; ++k) {
             const int jj = j0 + NT * k;
-            wj[k] = (jj < u) ? (wback ? a.weight[off + jj] : sA[jj]) : 0.0;
+            wj[k] = (jj < u) ? (park ? sW[jj] : wback ? a.weight[off + jj] : sA[jj]) : 0.0;
           }
 #pragma unroll
           for (int k = 0; k < NB; ++k) {

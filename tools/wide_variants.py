@@ -27,6 +27,8 @@ VARIANTS = {
     # round-2 thread-major exchange rows (2-way bank conflicts) instead of 4-key planes
     "wrows": [("consensus_wide.hip", "buf + (r >> 2) * PL + t * 4)", "buf + t * R + r)"),
               ("consensus_wide.hip", "buf + (r >> 2) * PL + (t ^ MT) * 4)", "buf + (t ^ MT) * R + r)")],
+    # FAST nweight from the weight output read-back instead of the LDS park (round 2)
+    "wnopark": [("consensus_wide.hip", "const bool park = FAST && wback && u <= WFREE;", "const bool park = false;")],
     # power-of-two bins only: 1025..2048 on 4 waves, 2049..4096 on 8 (round 2)
     "wpow2": [("consensus_wide.hip", "  if (max_len <= 1536) return launch_wide<3, 8, FAST, 4>(a, st);\n", ""),
               ("consensus_wide.hip", "  if (max_len <= 3072) return launch_wide<6, 8, FAST, 8>(a, st);\n", "")],
