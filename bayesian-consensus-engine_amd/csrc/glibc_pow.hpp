@@ -115,15 +115,22 @@ BCE_POW_FN double exp_inline(double x, double xtail) {
 // and pow returns it.  Only ~0.1% of inputs (near-midpoint squares, tiny or huge results)
 // take the restated algorithm below; tools/pow2_check.cpp checks both paths against libm.
 BCE_POW_FN double pow2_full(double x);
-BCE_POW_FN double pow2(double x) {
+// x*x and ok = true when it is libm's pow(x, 2.0) (the case above); ok = false otherwise.
+BCE_POW_FN double pow2_fast(double x, bool& ok) {
   const double hi = x * x;
   const double lo = __builtin_fma(x, x, -hi);
   const uint64_t b = asu(hi);
+  ok = false;
   if (hi >= 0x1p-1000 && hi < 0x1p1000 && (b & 0xFFFFFFFFFFFFFull) != 0) {
     const double ulp = asd(b + 1) - hi;
-    if (__builtin_fabs(lo) < 0.4 * ulp) return hi;
+    ok = __builtin_fabs(lo) < 0.4 * ulp;
   }
-  return pow2_full(x);
+  return hi;
+}
+BCE_POW_FN double pow2(double x) {
+  bool ok;
+  const double hi = pow2_fast(x, ok);
+  return ok ? hi : pow2_full(x);
 }
 
 BCE_POW_FN double pow2_full(double x) {

@@ -201,19 +201,19 @@ __global__ __launch_bounds__(256) void tiebreak_wave_kernel(TbArgs a, const int3
 //      glibc_pow.hpp -- summed in input order) and the per-group confidence sums.
 constexpr int kTbLpmMax = 32;
 constexpr int kTbLpmWaves = 4;
-constexpr int kTbStage = 64 * kTbLpmMax + 64;  // doubles per buffer: a tile's agents + pads
+constexpr int kTbStage = 64 * kTbLpmMax + 64;  // doubles per wave buffer: a tile's agents + pads
 
 __device__ __forceinline__ int tb_pad(int i) { return i + (i >> 5); }
 
 template <bool STAGED>
-__global__ __launch_bounds__(64 * kTbLpmWaves) void tiebreak_lpm_kernel(TbArgs a, const int32_t* list,
+__global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_eu(2, 2))) void tiebreak_lpm_kernel(TbArgs a, const int32_t* list,
                                                                          int64_t n_list, int* fault) {
-  __shared__ double sBuf[STAGED ? kTbLpmWaves : 1][2][STAGED ? kTbStage : 1];
+  // one buffer per wave (16.9 KB): two workgroups of four waves per CU
+  __shared__ double sBuf[STAGED ? kTbLpmWaves : 1][STAGED ? kTbStage : 1];
   const int lane = lane_id();
   const int wv = STAGED ? (int)(threadIdx.x >> 6) : 0;
-  double* const bufA = sBuf[wv][0];
-  double* const bufB = sBuf[wv][1];
-  int32_t* const ibufB = reinterpret_cast<int32_t*>(bufB);
+  double* const buf = sBuf[wv];
+  int32_t* const ibuf = reinterpret_cast<int32_t*>(buf);
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t tile = wave; tile * 64 < n_list; tile += nwaves) {
@@ -247,7 +247,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) void tiebreak_lpm_kernel(TbArgs a
     const int rbase = n > 0 ? lrow : 0;
     const int64_t gbase = n > 0 ? off : B;
     // global [B, E) -> LDS (padded), coalesced 16-B loads
-    auto stage = [&](double* buf, const double* src) {
+    auto stage = [&](const double* src) {
       wave_sync_lds();  // the buffer's previous readers (this wave) are done
       const bool al = ((uintptr_t)(src + B) & 15) == 0;
       for (int e = 2 * lane; e < cnt_tile; e += 128) {
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) void tiebreak_lpm_kernel(TbArgs a
       wave_sync_lds();
     };
     // LDS (padded) -> global [B, E), coalesced 16-B stores
-    auto flush = [&](const double* buf, double* dst) {
+    auto flush = [&](double* dst) {
       wave_sync_lds();
       const bool al = ((uintptr_t)(dst + B) & 15) == 0;
       for (int e = 2 * lane; e < cnt_tile; e += 128) {
@@ -275,31 +275,37 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) void tiebreak_lpm_kernel(TbArgs a
         }
       }
     };
-    auto flush_i32 = [&](const int32_t* buf, int32_t* dst) {
+    auto flush_i32 = [&](int32_t* dst) {
       wave_sync_lds();
       const bool al = ((uintptr_t)(dst + B) & 15) == 0;
       for (int e = 4 * lane; e < cnt_tile; e += 256) {
         if (al && e + 3 < cnt_tile) {
           *reinterpret_cast<int4*>(dst + B + e) =
-              make_int4(buf[tb_pad(e)], buf[tb_pad(e + 1)], buf[tb_pad(e + 2)], buf[tb_pad(e + 3)]);
+              make_int4(ibuf[tb_pad(e)], ibuf[tb_pad(e + 1)], ibuf[tb_pad(e + 2)], ibuf[tb_pad(e + 3)]);
         } else {
-          for (int q = 0; q < 4 && e + q < cnt_tile; ++q) dst[B + e + q] = buf[tb_pad(e + q)];
+          for (int q = 0; q < 4 && e + q < cnt_tile; ++q) dst[B + e + q] = ibuf[tb_pad(e + q)];
         }
       }
     };
     // agent t of this lane's market
-    auto at = [&](const double* buf, const double* src, int t) -> double {
+    auto at = [&](const double* src, int t) -> double {
       if constexpr (STAGED) return buf[tb_pad(rbase + t)];
       else return src[gbase + t];
     };
     // this lane's slot g (an agent's or a group's output)
-    auto put = [&](double* buf, double* dst, int g, double v) {
+    auto put = [&](double* dst, int g, double v) {
       if constexpr (STAGED) buf[tb_pad(lrow + g)] = v;
       else dst[off + g] = v;
     };
-    auto put_i32 = [&](int32_t* buf, int32_t* dst, int g, int v) {
-      if constexpr (STAGED) buf[tb_pad(lrow + g)] = v;
+    auto put_i32 = [&](int32_t* dst, int g, int v) {
+      if constexpr (STAGED) ibuf[tb_pad(lrow + g)] = v;
       else dst[off + g] = v;
+    };
+    auto run_start = [&](const unsigned (&u)[kTbLpmMax], int p) {
+      return (p == 0) || ((u[p] >> 5) != (u[p > 0 ? p - 1 : 0] >> 5));
+    };
+    auto run_end = [&](const unsigned (&u)[kTbLpmMax], int p) {
+      return (p + 1 >= n) || ((u[p] >> 5) != (u[p + 1 < kTbLpmMax ? p + 1 : p] >> 5));
     };
     const double nd = (double)(n > 0 ? n : 1);
 
@@ -307,10 +313,11 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) void tiebreak_lpm_kernel(TbArgs a
     unsigned u[kTbLpmMax];
     double kp[kTbLpmMax];
     int ng = 0;
-    if constexpr (STAGED) stage(bufA, a.pred);
+    if constexpr (STAGED) stage(a.pred);
+    const double praw0 = at(a.pred, 0);  // a single agent keeps its raw prediction (tiebreak.py:89-96)
     {
 #pragma unroll
-      for (int t = 0; t < kTbLpmMax; ++t) kp[t] = tb_round(at(bufA, a.pred, min(t, last)), a);
+      for (int t = 0; t < kTbLpmMax; ++t) kp[t] = tb_round(at(a.pred, min(t, last)), a);
       int go[kTbLpmMax];
 #pragma unroll
       for (int t = 0; t < kTbLpmMax; ++t) {
@@ -320,94 +327,130 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) void tiebreak_lpm_kernel(TbArgs a
         const bool fresh = (t < n) && g < 0;
         go[t] = fresh ? ng : g;
         ng += fresh ? 1 : 0;
-        if (a.g_of && t < n) put_i32(ibufB, a.g_of, t, go[t]);
         u[t] = (t < n) ? (((unsigned)go[t] << 5) | (unsigned)t) : 0xFFFFFFFFu;
       }
+      if (a.g_of) {  // agent t's prediction (slot t) is consumed: the ordinals go in place
+        if constexpr (STAGED) wave_sync_lds();
+#pragma unroll
+        for (int t = 0; t < kTbLpmMax; ++t)
+          if (t < n) put_i32(a.g_of, t, go[t]);
+        if constexpr (STAGED) flush_i32(a.g_of);
+      }
     }
-    if constexpr (STAGED) {
-      if (a.g_of) flush_i32(ibufB, a.g_of);
-    }
-    // a single agent keeps its raw prediction (tiebreak.py:89-96)
-    const double praw0 = at(bufA, a.pred, 0);
     oem_sort_kv(u, kp);
 
-    // ---- 2. walk: weights and reliabilities by group, the winner ---------------------------
-    if constexpr (STAGED) {
-      stage(bufA, a.weight);
-      stage(bufB, a.rel);
-    }
-    double bd = 0.0, bm = 0.0, bk = 0.0;
-    bool tie = false;
-    {
-      double tot = 0.0, mx = 0.0;
+    // ---- 2. group keys and counts (registers only) ------------------------------------------
+    if (a.g_key || a.g_count) {
       int cnt = 0;
 #pragma unroll
       for (int p = 0; p < kTbLpmMax; ++p) {
         if (p < n) {
-          const unsigned v = u[p];
-          const int t = (int)(v & 31u);
-          const unsigned g = v >> 5;
-          const bool start = (p == 0) || (g != (u[p > 0 ? p - 1 : 0] >> 5));
-          const bool end = (p + 1 >= n) || (g != (u[p + 1 < kTbLpmMax ? p + 1 : p] >> 5));
-          const double w = at(bufA, a.weight, t), r = at(bufB, a.rel, t);
-          tot = (start ? 0.0 : tot) + w;          // tiebreak.py:60, sum from int 0
-          cnt = (start ? 0 : cnt) + 1;
-          mx = start ? r : ((r > mx) ? r : mx);  // tiebreak.py:62, first maximum kept
-          if (end) {
-            const double key = (n == 1) ? praw0 : kp[p];  // the run's entries all carry the group key
-            const double dens = tot / (double)cnt;
-            if (a.g_density) put(bufA, a.g_density, (int)g, dens);  // slot g's inputs are consumed
-            if (a.g_maxrel) put(bufB, a.g_maxrel, (int)g, mx);
+          cnt = (run_start(u, p) ? 0 : cnt) + 1;
+          if (run_end(u, p) && a.g_key) put(a.g_key, (int)(u[p] >> 5), (n == 1) ? praw0 : kp[p]);
+        }
+      }
+      if constexpr (STAGED) {
+        if (a.g_key) flush(a.g_key);
+      }
+      if (a.g_count) {
+        if constexpr (STAGED) wave_sync_lds();
+        cnt = 0;
+#pragma unroll
+        for (int p = 0; p < kTbLpmMax; ++p) {
+          if (p < n) {
+            cnt = (run_start(u, p) ? 0 : cnt) + 1;
+            if (run_end(u, p)) put_i32(a.g_count, (int)(u[p] >> 5), cnt);
+          }
+        }
+        if constexpr (STAGED) flush_i32(a.g_count);
+      }
+    }
+
+    // ---- 3. weights: group densities, kept per run end for the winner -----------------------
+    // A group's outputs overwrite slot g of its market's row in place: group g ends only after
+    // every group <= g, and agent g (ordinal <= g) belongs to one of those -- consumed.
+    double densp[kTbLpmMax];
+    if constexpr (STAGED) stage(a.weight);
+    {
+      double tot = 0.0;
+      int cnt = 0;
+#pragma unroll
+      for (int p = 0; p < kTbLpmMax; ++p) {
+        densp[p] = 0.0;
+        if (p < n) {
+          const int t = (int)(u[p] & 31u);
+          const bool st = run_start(u, p);
+          tot = (st ? 0.0 : tot) + at(a.weight, t);  // tiebreak.py:60, sum from int 0
+          cnt = (st ? 0 : cnt) + 1;
+          densp[p] = tot / (double)cnt;
+          if (run_end(u, p) && a.g_density) put(a.g_density, (int)(u[p] >> 5), densp[p]);
+        }
+      }
+      if constexpr (STAGED) {
+        if (a.g_density) flush(a.g_density);
+      }
+    }
+
+    // ---- 4. reliabilities: max per group (first maximum kept), the winner ------------------
+    double bd = 0.0, bm = 0.0, bk = 0.0;
+    bool tie = false;
+    if constexpr (STAGED) stage(a.rel);
+    {
+      double mx = 0.0;
+#pragma unroll
+      for (int p = 0; p < kTbLpmMax; ++p) {
+        if (p < n) {
+          const int t = (int)(u[p] & 31u);
+          const unsigned g = u[p] >> 5;
+          const double r = at(a.rel, t);
+          mx = run_start(u, p) ? r : ((r > mx) ? r : mx);  // tiebreak.py:62
+          if (run_end(u, p)) {
+            if (a.g_maxrel) put(a.g_maxrel, (int)g, mx);
+            const double key = (n == 1) ? praw0 : kp[p], dens = densp[p];
             const bool same = (dens == bd) && (mx == bm);
-            if (g == 0 || tb_better(dens, mx, key, bd, bm, bk)) {
+            if (g == 0 || tb_better(dens, mx, key, bd, bm, bk)) {  // tiebreak.py:113-117
               tie = (g != 0) && same;
               bd = dens; bm = mx; bk = key;
             } else {
-              tie = tie || same;
+              tie = tie || same;  // tiebreak.py:123-133: does another group tie the winner?
             }
           }
         }
       }
-    }
-    if constexpr (STAGED) {
-      if (a.g_density) flush(bufA, a.g_density);
-      if (a.g_maxrel) flush(bufB, a.g_maxrel);
-    }
-    // group keys and counts from the sorted runs alone
-    if (a.g_key || a.g_count) {
-      if constexpr (STAGED) wave_sync_lds();  // the flushes above have read their buffers
-      int cnt = 0;
-#pragma unroll
-      for (int p = 0; p < kTbLpmMax; ++p) {
-        if (p < n) {
-          const unsigned g = u[p] >> 5;
-          const bool start = (p == 0) || (g != (u[p > 0 ? p - 1 : 0] >> 5));
-          const bool end = (p + 1 >= n) || (g != (u[p + 1 < kTbLpmMax ? p + 1 : p] >> 5));
-          cnt = (start ? 0 : cnt) + 1;
-          if (end) {
-            if (a.g_key) put(bufA, a.g_key, (int)g, (n == 1) ? praw0 : kp[p]);
-            if (a.g_count) put_i32(ibufB, a.g_count, (int)g, cnt);
-          }
-        }
-      }
       if constexpr (STAGED) {
-        if (a.g_key) flush(bufA, a.g_key);
-        if (a.g_count) flush_i32(ibufB, a.g_count);
+        if (a.g_maxrel) flush(a.g_maxrel);
       }
     }
 
-    // ---- 3. confidences: variance (input order) and the per-group sums ----------------------
-    if constexpr (STAGED) stage(bufA, a.conf);
+    // ---- 5. confidences: variance (input order), then the per-group means -----------------
+    if constexpr (STAGED) stage(a.conf);
     double variance;
     {
       double cs = 0.0;
 #pragma unroll
-      for (int t = 0; t < kTbLpmMax; ++t) cs += (t < n) ? at(bufA, a.conf, t < n ? t : last) : 0.0;
+      for (int t = 0; t < kTbLpmMax; ++t) cs += (t < n) ? at(a.conf, t < n ? t : last) : 0.0;
       const double mean = cs / nd;
+      // squares: pow(d, 2.0) restated (glibc_pow.hpp); the exact fast path first, the few
+      // near-midpoint squares (a bit in `slow`) redone one per lane per round afterwards
+      double sq[kTbLpmMax];
+      unsigned slow = 0;
+#pragma unroll
+      for (int t = 0; t < kTbLpmMax; ++t) {
+        const double d = at(a.conf, t < n ? t : last) - mean;
+        bool ok;
+        sq[t] = bce_pow::pow2_fast(d, ok);
+        slow |= ((t < n) && !ok) ? (1u << t) : 0u;
+      }
+      while (ballot(slow != 0u)) {
+        const int t1 = slow ? (int)__builtin_ctz(slow) : 0;
+        slow &= slow - 1u;
+        const double v = bce_pow::pow2_full(at(a.conf, t1) - mean);
+#pragma unroll
+        for (int t = 0; t < kTbLpmMax; ++t) sq[t] = (t == t1) ? v : sq[t];
+      }
       double vs = 0.0;
 #pragma unroll
-      for (int t = 0; t < kTbLpmMax; ++t)
-        vs += (t < n) ? bce_pow::pow2(at(bufA, a.conf, t < n ? t : last) - mean) : 0.0;
+      for (int t = 0; t < kTbLpmMax; ++t) vs += (t < n) ? sq[t] : 0.0;
       variance = vs / nd;
     }
     if (a.g_avgconf) {
@@ -416,17 +459,13 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) void tiebreak_lpm_kernel(TbArgs a
 #pragma unroll
       for (int p = 0; p < kTbLpmMax; ++p) {
         if (p < n) {
-          const unsigned v = u[p];
-          const int t = (int)(v & 31u);
-          const unsigned g = v >> 5;
-          const bool start = (p == 0) || (g != (u[p > 0 ? p - 1 : 0] >> 5));
-          const bool end = (p + 1 >= n) || (g != (u[p + 1 < kTbLpmMax ? p + 1 : p] >> 5));
-          gcs = (start ? 0.0 : gcs) + at(bufA, a.conf, t);  // tiebreak.py:61
-          cnt = (start ? 0 : cnt) + 1;
-          if (end) put(bufA, a.g_avgconf, (int)g, gcs / (double)cnt);
+          const bool st = run_start(u, p);
+          gcs = (st ? 0.0 : gcs) + at(a.conf, (int)(u[p] & 31u));  // tiebreak.py:61
+          cnt = (st ? 0 : cnt) + 1;
+          if (run_end(u, p)) put(a.g_avgconf, (int)(u[p] >> 5), gcs / (double)cnt);
         }
       }
-      if constexpr (STAGED) flush(bufA, a.g_avgconf);
+      if constexpr (STAGED) flush(a.g_avgconf);
     }
     if (has) {
       if (n == 0) {  // tiebreak.py:86-87 (ValueError)
