@@ -61,7 +61,9 @@ struct WideCfg {
   static constexpr int HR = (R < kWideHR) ? R : kWideHR;
   // register budget: workgroups of >= 4 waves get 4 waves per SIMD (<= 128 VGPRs), so two
   // LDS-sized workgroups share a CU
-  static constexpr int WPE = kWideWPE;
+  // a 6-wave workgroup needs 5 waves per SIMD (<= 102 VGPRs) for three of them to share a CU
+  // (LDS allows three); at 4 only two fit and the bin runs on 12 waves per CU
+  static constexpr int WPE = (NW == 6) ? 5 : kWideWPE;
   static constexpr int A_DBL = P + 64;  // + the run sums' read-ahead
   // region B (u32): sort exchange rows, then leaders [P] (+ exact: chain buffers
   // [2][3][NT] doubles + the chain's read-ahead)

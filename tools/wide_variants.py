@@ -27,6 +27,11 @@ VARIANTS = {
     # round-2 thread-major exchange rows (2-way bank conflicts) instead of 4-key planes
     "wrows": [("consensus_wide.hip", "buf + (r >> 2) * PL + t * 4)", "buf + t * R + r)"),
               ("consensus_wide.hip", "buf + (r >> 2) * PL + (t ^ MT) * 4)", "buf + (t ^ MT) * R + r)")],
+    # the 6-wave kernel at 4 waves per SIMD (two workgroups per CU) instead of 5 (three)
+    "w6wpe4": [("consensus_wide.hip", "static constexpr int WPE = (NW == 6) ? 5 : kWideWPE;",
+                "static constexpr int WPE = kWideWPE;")],
+    # tie-break lane-per-market kernel at the compiler's choice (1 wave per SIMD, no spills)
+    "tbocc1": [("tiebreak.hip", "__attribute__((amdgpu_waves_per_eu(2, 2))) ", "")],
     # FAST nweight from the weight output read-back instead of the LDS park (round 2)
     "wnopark": [("consensus_wide.hip", "const bool park = FAST && wback && u <= WFREE;", "const bool park = false;")],
     # power-of-two bins only: 1025..2048 on 4 waves, 2049..4096 on 8 (round 2)
