@@ -1667,7 +1667,10 @@ extern "C" int bce_consensus_csr(const int64_t* offsets, int64_t n_markets, cons
 }
 
 static_assert(BCE_NBINS == 13, "bin table");
-static const int64_t kBinMax[BCE_NBINS - 1] = {8, 16, 32, 64, 128, 256, 512, 1024, 1536, 2048, 3072, kLongMaxLds};
+static constexpr int64_t kBinMax[BCE_NBINS - 1] = {8, 16, 32, 64, 128, 256, 512, 1024, 1536, 2048, 3072, kLongMaxLds};
+constexpr int kBinNp2Lo = 8, kBinNp2Hi = 10;  // the 1536 and 3072 bins
+static_assert(kBinMax[kBinNp2Lo] == 1536 && kBinMax[kBinNp2Hi] == 3072, "non-power-of-two bins");
+constexpr int kPlanSideLast = 3;  // bins 0..3 (n <= 64) run on the side stream
 static int bin_of(int64_t n) {
   for (int b = 0; b < BCE_NBINS - 1; ++b)
     if (n <= kBinMax[b]) return b;
@@ -1740,20 +1743,23 @@ extern "C" int bce_consensus_planned(const int64_t* offsets, int64_t n_markets, 
   // The short-market bins (n <= 64) are small latency-bound launches: they run on a side
   // stream while the long bins run on st, longest first (joined before return).  Measured
   // on C3: 1.73 -> 1.65 ms; moving wide bins to the side stream too, or forking every bin
-  // over 2-8 streams, was slower (profiles/r02_c3_plan_streams.jsonl).  BCE_PLAN_SIDE = the
-  // last bin index on the side stream (default 3; -1 = everything on st).
+  // over 2-8 streams, was slower (profiles/r02_c3_plan_streams.jsonl).
   hipStream_t side = st;
   std::unique_lock<std::mutex> fork_lock;
-  const int side_last = getenv("BCE_PLAN_SIDE") ? atoi(getenv("BCE_PLAN_SIDE")) : 3;  // last side bin
-  const bool fork = side_last >= 0;
-  if (fork) {
-    rc = side_fork(st, &side, &fork_lock);
-    if (rc) return rc;
-  }
+  constexpr int side_last = kPlanSideLast;
+  rc = side_fork(st, &side, &fork_lock);
+  if (rc) return rc;
+  // EXACT: the non-power-of-two bins (1025..1536, 2049..3072) ride in the launch of the
+  // power-of-two bin above them (their markets sit right below it in `order`).  The exact
+  // kernel's LDS chain buffers allow two workgroups per CU at 3/6 waves as at 4/8, so the
+  // smaller workgroup only loses latency hiding, and a separate launch adds a tail.
+  const bool merge_np2 = mode == BCE_MODE_EXACT;
   for (int b = BCE_NBINS - 1; b >= 0; --b) {
+    if (merge_np2 && (b == kBinNp2Lo || b == kBinNp2Hi)) continue;
+    const int b0 = (merge_np2 && (b == kBinNp2Lo + 1 || b == kBinNp2Hi + 1)) ? b - 1 : b;
     ConsArgs a = base;
-    a.list = order + bin_start_host[b];
-    a.n_list = bin_start_host[b + 1] - bin_start_host[b];
+    a.list = order + bin_start_host[b0];
+    a.n_list = bin_start_host[b + 1] - bin_start_host[b0];
     if (a.n_list == 0) continue;
     hipStream_t sb = (b <= side_last) ? side : st;
     if (b <= 3 && seg_ok) {
@@ -1777,10 +1783,8 @@ extern "C" int bce_consensus_planned(const int64_t* offsets, int64_t n_markets, 
     }
     if (rc) break;
   }
-  if (fork) {
-    const int rj = side_join(st);  // join even after a failed launch: st must not run ahead
-    if (!rc) rc = rj;
-  }
+  const int rj = side_join(st);  // join even after a failed launch: st must not run ahead
+  if (!rc) rc = rj;
   return rc;
 }
 

@@ -61,9 +61,9 @@ struct WideCfg {
   static constexpr int HR = (R < kWideHR) ? R : kWideHR;
   // register budget: workgroups of >= 4 waves get 4 waves per SIMD (<= 128 VGPRs), so two
   // LDS-sized workgroups share a CU
-  // a 6-wave workgroup needs 5 waves per SIMD (<= 102 VGPRs) for three of them to share a CU
-  // (LDS allows three); at 4 only two fit and the bin runs on 12 waves per CU
-  static constexpr int WPE = (NW == 6) ? 5 : kWideWPE;
+  // (the 6-wave FAST kernel at 5 waves per SIMD, <= 102 VGPRs, so three workgroups share a
+  // CU: C3 fast 1.55 -> 1.72 ms from its spills, profiles/r03g/wide_ab.txt)
+  static constexpr int WPE = kWideWPE;
   static constexpr int A_DBL = P + 64;  // + the run sums' read-ahead
   // region B (u32): sort exchange rows, then leaders [P] (+ exact: chain buffers
   // [2][3][NT] doubles + the chain's read-ahead)

@@ -27,9 +27,9 @@ VARIANTS = {
     # round-2 thread-major exchange rows (2-way bank conflicts) instead of 4-key planes
     "wrows": [("consensus_wide.hip", "buf + (r >> 2) * PL + t * 4)", "buf + t * R + r)"),
               ("consensus_wide.hip", "buf + (r >> 2) * PL + (t ^ MT) * 4)", "buf + (t ^ MT) * R + r)")],
-    # the 6-wave kernel at 4 waves per SIMD (two workgroups per CU) instead of 5 (three)
-    "w6wpe4": [("consensus_wide.hip", "static constexpr int WPE = (NW == 6) ? 5 : kWideWPE;",
-                "static constexpr int WPE = kWideWPE;")],
+    # the 6-wave kernel at 5 waves per SIMD (three workgroups per CU, spills) instead of 4
+    "w6wpe5": [("consensus_wide.hip", "static constexpr int WPE = kWideWPE;",
+                "static constexpr int WPE = (NW == 6) ? 5 : kWideWPE;")],
     # tie-break lane-per-market kernel at the compiler's choice (1 wave per SIMD, no spills)
     "tbocc1": [("tiebreak.hip", "__attribute__((amdgpu_waves_per_eu(2, 2))) ", "")],
     # FAST nweight from the weight output read-back instead of the LDS park (round 2)
@@ -37,7 +37,14 @@ VARIANTS = {
     # power-of-two bins only: 1025..2048 on 4 waves, 2049..4096 on 8 (round 2)
     "wpow2": [("consensus_wide.hip", "  if (max_len <= 1536) return launch_wide<3, 8, FAST, 4>(a, st);\n", ""),
               ("consensus_wide.hip", "  if (max_len <= 3072) return launch_wide<6, 8, FAST, 8>(a, st);\n", "")],
+    # EXACT: the non-power-of-two bins in launches of their own (as FAST) instead of riding
+    # with the power-of-two bin above them
+    "wsplitx": [("consensus.hip", "const bool merge_np2 = mode == BCE_MODE_EXACT;", "const bool merge_np2 = false;")],
+    # FAST too: the non-power-of-two bins ride with the bin above them (power-of-two kernels)
+    "wmergef": [("consensus.hip", "const bool merge_np2 = mode == BCE_MODE_EXACT;", "const bool merge_np2 = true;")],
 }
+
+
 def build(names):
     tab_variants.build(names, VARIANTS)
 
