@@ -42,6 +42,20 @@ VARIANTS = {
     "wsplitx": [("consensus.hip", "const bool merge_np2 = mode == BCE_MODE_EXACT;", "const bool merge_np2 = false;")],
     # FAST too: the non-power-of-two bins ride with the bin above them (power-of-two kernels)
     "wmergef": [("consensus.hip", "const bool merge_np2 = mode == BCE_MODE_EXACT;", "const bool merge_np2 = true;")],
+    # ---- ablations (timing only; outputs are wrong by construction) ----
+    # the sort network run twice (the second pass on sorted keys costs the same)
+    "xsort2": [("consensus_wide.hip", "    wide_sort<NN, NW, R>(key, sX, t, lane);\n",
+                "    wide_sort<NN, NW, R>(key, sX, t, lane);\n    wide_sort<NN, NW, R>(key, sX, t, lane);\n")],
+    # no relconf / present-bit gathers (constant rows)
+    "xnogather": [("consensus_wide.hip", "rc[i] = a.relconf[sids[i]];", "rc[i] = make_double2(0.5 + 1e-9 * sids[i], 0.25);"),
+                  ("consensus_wide.hip", "pwd[i] = a.pbits[sids[i] >> 5];", "pwd[i] = 0xFFFFFFFFu;")],
+    # no normalizedWeight phase
+    "xnonw": [("consensus_wide.hip", "    if (a.nweight) {  // core.py:151", "    if (false) {  // core.py:151")],
+    # no sorted-probability gather from region A
+    "xnosp": [("consensus_wide.hip", "x[r] = (q < n) ? sA[key[r] & QMASK] : 0.0;", "x[r] = (q < n) ? 0.5 : 0.0;")],
+    # no run sums (constant averages)
+    "xnorun": [("consensus_wide.hip", "avg = (jj < u && len <= kWaveRun) ? run_sum(sA + q0s[i], len) : 0.0;",
+                "avg = (jj < u) ? 0.5 : 0.0;")],
 }
 
 
