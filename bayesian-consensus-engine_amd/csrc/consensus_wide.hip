@@ -126,6 +126,71 @@ constexpr int xw_index(int K, int J, int R) {
   return idx;
 }
 
+// One lane stage over 8 keys with the partner's key read through DPP inside the
+// instructions that use it: per key v_sub_co_u32_dpp (borrow = partner < key, into VCC),
+// s_xor_b64 with the stage's lower-lane mask, v_cndmask_b32_dpp (keep the key or take the
+// partner's) -- two VALU per key instead of a v_mov_b32_dpp, a v_cmp and a v_cndmask (the
+// compiler neither folds DPP into a compare nor into a select whose DPP operand is src1,
+// and gfx950 has no VOPC DPP).  FLIP: key r's partner is key R-1-r of the partner lane.
+// The outputs are early-clobber, so no instruction in the block reads a register written
+// in it; `s_nop 1` covers the VALU-write -> DPP-read hazard on the inputs.
+#define BCE_DPP_CAS(O, A, B, C)                                                  \
+  "v_sub_co_u32_dpp %[j], vcc, %[" B "], %[" A "] " C " row_mask:0xf bank_mask:0xf\n" \
+  "s_xor_b64 vcc, vcc, %[lm]\n"                                                  \
+  "v_cndmask_b32_dpp %[" O "], %[" B "], %[" A "], vcc " C " row_mask:0xf bank_mask:0xf\n"
+#define BCE_DPP_STAGE8(C, B0, B1, B2, B3, B4, B5, B6, B7)                                                       \
+  asm("s_nop 1\n" BCE_DPP_CAS("o0", "k0", B0, C) BCE_DPP_CAS("o1", "k1", B1, C) BCE_DPP_CAS("o2", "k2", B2, C)    \
+          BCE_DPP_CAS("o3", "k3", B3, C) BCE_DPP_CAS("o4", "k4", B4, C) BCE_DPP_CAS("o5", "k5", B5, C)           \
+              BCE_DPP_CAS("o6", "k6", B6, C) BCE_DPP_CAS("o7", "k7", B7, C)                                      \
+      : [o0] "=&v"(o[0]), [o1] "=&v"(o[1]), [o2] "=&v"(o[2]), [o3] "=&v"(o[3]), [o4] "=&v"(o[4]),              \
+        [o5] "=&v"(o[5]), [o6] "=&v"(o[6]), [o7] "=&v"(o[7]), [j] "=&v"(junk)                                  \
+      : [k0] "v"(s[0]), [k1] "v"(s[1]), [k2] "v"(s[2]), [k3] "v"(s[3]), [k4] "v"(s[4]), [k5] "v"(s[5]),        \
+        [k6] "v"(s[6]), [k7] "v"(s[7]), [lm] "s"(lower)                                                        \
+      : "vcc")
+#define BCE_DPP_STAGE8_ANY(C, FLIP)                                                   \
+  do {                                                                                \
+    if (FLIP)                                                                         \
+      BCE_DPP_STAGE8(C, "k7", "k6", "k5", "k4", "k3", "k2", "k1", "k0");              \
+    else                                                                              \
+      BCE_DPP_STAGE8(C, "k0", "k1", "k2", "k3", "k4", "k5", "k6", "k7");              \
+  } while (0)
+
+// Lane distances the fused stage serves: one DPP pattern (quad_perm, row_half_mirror,
+// row_mirror, row_ror:8), or l ^ 4 = quad_perm 3,2,1,0 of a row_half_mirror copy.
+constexpr bool dpp_fusable(int M) { return M == 1 || M == 2 || M == 3 || M == 4 || M == 7 || M == 8 || M == 15; }
+
+template <int M, bool FLIP>
+__device__ __forceinline__ void dpp_stage8(unsigned (&key)[8], uint64_t lower) {
+  unsigned o[8], junk;
+  if constexpr (M == 4) {
+    unsigned s[8];  // s[r] = key[r] of lane l ^ 7; quad_perm 3,2,1,0 of it is lane l ^ 4
+#pragma unroll
+    for (int r = 0; r < 8; ++r) s[r] = (unsigned)__builtin_amdgcn_mov_dpp((int)key[r], 0x141, 0xF, 0xF, false);
+    // here the DPP operand (B) is the half-mirrored copy, the kept operand (A) the key
+    asm("s_nop 1\n" BCE_DPP_CAS("o0", "q0", "k0", "quad_perm:[3,2,1,0]") BCE_DPP_CAS("o1", "q1", "k1", "quad_perm:[3,2,1,0]")
+            BCE_DPP_CAS("o2", "q2", "k2", "quad_perm:[3,2,1,0]") BCE_DPP_CAS("o3", "q3", "k3", "quad_perm:[3,2,1,0]")
+                BCE_DPP_CAS("o4", "q4", "k4", "quad_perm:[3,2,1,0]") BCE_DPP_CAS("o5", "q5", "k5", "quad_perm:[3,2,1,0]")
+                    BCE_DPP_CAS("o6", "q6", "k6", "quad_perm:[3,2,1,0]") BCE_DPP_CAS("o7", "q7", "k7", "quad_perm:[3,2,1,0]")
+        : [o0] "=&v"(o[0]), [o1] "=&v"(o[1]), [o2] "=&v"(o[2]), [o3] "=&v"(o[3]), [o4] "=&v"(o[4]), [o5] "=&v"(o[5]),
+          [o6] "=&v"(o[6]), [o7] "=&v"(o[7]), [j] "=&v"(junk)
+        : [k0] "v"(s[0]), [k1] "v"(s[1]), [k2] "v"(s[2]), [k3] "v"(s[3]), [k4] "v"(s[4]), [k5] "v"(s[5]),
+          [k6] "v"(s[6]), [k7] "v"(s[7]), [q0] "v"(key[0]), [q1] "v"(key[1]), [q2] "v"(key[2]), [q3] "v"(key[3]),
+          [q4] "v"(key[4]), [q5] "v"(key[5]), [q6] "v"(key[6]), [q7] "v"(key[7]), [lm] "s"(lower)
+        : "vcc");
+    static_assert(!FLIP, "l ^ 4 is a half-cleaner distance only");
+  } else {
+    const unsigned (&s)[8] = key;
+    if constexpr (M == 1) BCE_DPP_STAGE8_ANY("quad_perm:[1,0,3,2]", FLIP);
+    else if constexpr (M == 2) BCE_DPP_STAGE8_ANY("quad_perm:[2,3,0,1]", FLIP);
+    else if constexpr (M == 3) BCE_DPP_STAGE8_ANY("quad_perm:[3,2,1,0]", FLIP);
+    else if constexpr (M == 7) BCE_DPP_STAGE8_ANY("row_half_mirror", FLIP);
+    else if constexpr (M == 8) BCE_DPP_STAGE8_ANY("row_ror:8", FLIP);
+    else if constexpr (M == 15) BCE_DPP_STAGE8_ANY("row_mirror", FLIP);
+  }
+#pragma unroll
+  for (int r = 0; r < 8; ++r) key[r] = o[r];
+}
+
 // One stage of the flip-form bitonic network over PN = 64*NN*R keys, position q = t*R + r:
 // the first stage of merge K pairs q with q ^ (K-1), the others pair q with q ^ J, and the
 // lower position always keeps the minimum -- no direction bits anywhere.  Threads t >= 64*NW
@@ -146,6 +211,11 @@ __device__ __forceinline__ void wide_stage(unsigned (&key)[R], unsigned* sX, int
   } else if constexpr (flip ? (K <= 64 * R) : (J < 64 * R)) {  // across lanes (never crosses a wave)
     constexpr int MK = flip ? (K / R - 1) : (J / R);
     const bool lower = (lane & (flip ? (K / R / 2) : MK)) == 0;
+    if constexpr (R == 8 && dpp_fusable(MK)) {
+      dpp_stage8<MK, flip>(key, (uint64_t)ballot(lower));
+      if constexpr (J > 1) wide_stage<NN, NW, R, K, J / 2>(key, sX, t, lane);
+      return;
+    }
     unsigned y[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) y[r] = lane_xor<MK>(key[flip ? R - 1 - r : r]);

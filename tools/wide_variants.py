@@ -42,6 +42,8 @@ VARIANTS = {
     "wsplitx": [("consensus.hip", "const bool merge_np2 = mode == BCE_MODE_EXACT;", "const bool merge_np2 = false;")],
     # FAST too: the non-power-of-two bins ride with the bin above them (power-of-two kernels)
     "wmergef": [("consensus.hip", "const bool merge_np2 = mode == BCE_MODE_EXACT;", "const bool merge_np2 = true;")],
+    # round-2/3 lane stages: v_mov_b32_dpp + v_cmp + s_xor + v_cndmask per key (no DPP fusion)
+    "wnodpp": [("consensus_wide.hip", "if constexpr (R == 8 && dpp_fusable(MK)) {", "if constexpr (false) {")],
     # ---- ablations (timing only; outputs are wrong by construction) ----
     # the sort network run twice (the second pass on sorted keys costs the same)
     "xsort2": [("consensus_wide.hip", "    wide_sort<NN, NW, R>(key, sX, t, lane);\n",
