@@ -155,40 +155,81 @@ constexpr int xw_index(int K, int J, int R) {
       BCE_DPP_STAGE8(C, "k0", "k1", "k2", "k3", "k4", "k5", "k6", "k7");              \
   } while (0)
 
-// Lane distances the fused stage serves: one DPP pattern (quad_perm, row_half_mirror,
-// row_mirror, row_ror:8), or l ^ 4 = quad_perm 3,2,1,0 of a row_half_mirror copy.
+// Lane bits 2 and 3 separate the two lanes of a pair by DPP bank (bank = lane bits 3..2
+// of the row), so the stage needs no select at all: v_min_u32_dpp writes the lower lanes'
+// banks, v_max_u32_dpp the upper lanes' (bank_mask), each reading the partner through its
+// own row pattern -- two VALU per key, no compare in VCC.  CLO/BLO: the lower lanes' DPP
+// pattern and banks, CHI/BHI the upper lanes'.
+#define BCE_BANK_CAS(O, A, B, CLO, BLO, CHI, BHI)                                            \
+  "v_min_u32_dpp %[" O "], %[" B "], %[" A "] " CLO " row_mask:0xf bank_mask:" BLO "\n"     \
+  "v_max_u32_dpp %[" O "], %[" B "], %[" A "] " CHI " row_mask:0xf bank_mask:" BHI "\n"
+#define BCE_BANK_STAGE8(CLO, BLO, CHI, BHI, B0, B1, B2, B3, B4, B5, B6, B7)                                   \
+  asm("s_nop 1\n" BCE_BANK_CAS("o0", "k0", B0, CLO, BLO, CHI, BHI) BCE_BANK_CAS("o1", "k1", B1, CLO, BLO, CHI, BHI) \
+          BCE_BANK_CAS("o2", "k2", B2, CLO, BLO, CHI, BHI) BCE_BANK_CAS("o3", "k3", B3, CLO, BLO, CHI, BHI)          \
+              BCE_BANK_CAS("o4", "k4", B4, CLO, BLO, CHI, BHI) BCE_BANK_CAS("o5", "k5", B5, CLO, BLO, CHI, BHI)      \
+                  BCE_BANK_CAS("o6", "k6", B6, CLO, BLO, CHI, BHI) BCE_BANK_CAS("o7", "k7", B7, CLO, BLO, CHI, BHI)  \
+      : [o0] "=&v"(o[0]), [o1] "=&v"(o[1]), [o2] "=&v"(o[2]), [o3] "=&v"(o[3]), [o4] "=&v"(o[4]),               \
+        [o5] "=&v"(o[5]), [o6] "=&v"(o[6]), [o7] "=&v"(o[7])                                                    \
+      : [k0] "v"(s[0]), [k1] "v"(s[1]), [k2] "v"(s[2]), [k3] "v"(s[3]), [k4] "v"(s[4]), [k5] "v"(s[5]),         \
+        [k6] "v"(s[6]), [k7] "v"(s[7]))
+#define BCE_BANK_STAGE8_ANY(CLO, BLO, CHI, BHI, FLIP)                                          \
+  do {                                                                                         \
+    if (FLIP)                                                                                  \
+      BCE_BANK_STAGE8(CLO, BLO, CHI, BHI, "k7", "k6", "k5", "k4", "k3", "k2", "k1", "k0");     \
+    else                                                                                       \
+      BCE_BANK_STAGE8(CLO, BLO, CHI, BHI, "k0", "k1", "k2", "k3", "k4", "k5", "k6", "k7");     \
+  } while (0)
+
+// Lane distances the fused 8-key stage serves: lane bits 0..1 through one DPP pattern
+// (quad_perm) with the compare in VCC, lane bits 2..3 (row_ror:4/12, row_ror:8,
+// row_half_mirror, row_mirror) by bank.
 constexpr bool dpp_fusable(int M) { return M == 1 || M == 2 || M == 3 || M == 4 || M == 7 || M == 8 || M == 15; }
 
 template <int M, bool FLIP>
 __device__ __forceinline__ void dpp_stage8(unsigned (&key)[8], uint64_t lower) {
   unsigned o[8], junk;
-  if constexpr (M == 4) {
-    unsigned s[8];  // s[r] = key[r] of lane l ^ 7; quad_perm 3,2,1,0 of it is lane l ^ 4
-#pragma unroll
-    for (int r = 0; r < 8; ++r) s[r] = (unsigned)__builtin_amdgcn_mov_dpp((int)key[r], 0x141, 0xF, 0xF, false);
-    // here the DPP operand (B) is the half-mirrored copy, the kept operand (A) the key
-    asm("s_nop 1\n" BCE_DPP_CAS("o0", "q0", "k0", "quad_perm:[3,2,1,0]") BCE_DPP_CAS("o1", "q1", "k1", "quad_perm:[3,2,1,0]")
-            BCE_DPP_CAS("o2", "q2", "k2", "quad_perm:[3,2,1,0]") BCE_DPP_CAS("o3", "q3", "k3", "quad_perm:[3,2,1,0]")
-                BCE_DPP_CAS("o4", "q4", "k4", "quad_perm:[3,2,1,0]") BCE_DPP_CAS("o5", "q5", "k5", "quad_perm:[3,2,1,0]")
-                    BCE_DPP_CAS("o6", "q6", "k6", "quad_perm:[3,2,1,0]") BCE_DPP_CAS("o7", "q7", "k7", "quad_perm:[3,2,1,0]")
-        : [o0] "=&v"(o[0]), [o1] "=&v"(o[1]), [o2] "=&v"(o[2]), [o3] "=&v"(o[3]), [o4] "=&v"(o[4]), [o5] "=&v"(o[5]),
-          [o6] "=&v"(o[6]), [o7] "=&v"(o[7]), [j] "=&v"(junk)
-        : [k0] "v"(s[0]), [k1] "v"(s[1]), [k2] "v"(s[2]), [k3] "v"(s[3]), [k4] "v"(s[4]), [k5] "v"(s[5]),
-          [k6] "v"(s[6]), [k7] "v"(s[7]), [q0] "v"(key[0]), [q1] "v"(key[1]), [q2] "v"(key[2]), [q3] "v"(key[3]),
-          [q4] "v"(key[4]), [q5] "v"(key[5]), [q6] "v"(key[6]), [q7] "v"(key[7]), [lm] "s"(lower)
-        : "vcc");
-    static_assert(!FLIP, "l ^ 4 is a half-cleaner distance only");
-  } else {
-    const unsigned (&s)[8] = key;
-    if constexpr (M == 1) BCE_DPP_STAGE8_ANY("quad_perm:[1,0,3,2]", FLIP);
-    else if constexpr (M == 2) BCE_DPP_STAGE8_ANY("quad_perm:[2,3,0,1]", FLIP);
-    else if constexpr (M == 3) BCE_DPP_STAGE8_ANY("quad_perm:[3,2,1,0]", FLIP);
-    else if constexpr (M == 7) BCE_DPP_STAGE8_ANY("row_half_mirror", FLIP);
-    else if constexpr (M == 8) BCE_DPP_STAGE8_ANY("row_ror:8", FLIP);
-    else if constexpr (M == 15) BCE_DPP_STAGE8_ANY("row_mirror", FLIP);
-  }
+  const unsigned (&s)[8] = key;
+  // row_ror:N reads lane (l - N) mod 16: the l ^ 4 partner is ror 12 for bit 2 clear
+  // (banks 0, 2), ror 4 for bit 2 set (banks 1, 3)
+  if constexpr (M == 4) BCE_BANK_STAGE8_ANY("row_ror:12", "0x5", "row_ror:4", "0xa", FLIP);
+  else if constexpr (M == 8) BCE_BANK_STAGE8_ANY("row_ror:8", "0x3", "row_ror:8", "0xc", FLIP);
+  else if constexpr (M == 7) BCE_BANK_STAGE8_ANY("row_half_mirror", "0x5", "row_half_mirror", "0xa", FLIP);
+  else if constexpr (M == 15) BCE_BANK_STAGE8_ANY("row_mirror", "0x3", "row_mirror", "0xc", FLIP);
+  else if constexpr (M == 1) BCE_DPP_STAGE8_ANY("quad_perm:[1,0,3,2]", FLIP);
+  else if constexpr (M == 2) BCE_DPP_STAGE8_ANY("quad_perm:[2,3,0,1]", FLIP);
+  else if constexpr (M == 3) BCE_DPP_STAGE8_ANY("quad_perm:[3,2,1,0]", FLIP);
+  (void)junk;
+  (void)lower;
 #pragma unroll
   for (int r = 0; r < 8; ++r) key[r] = o[r];
+}
+
+// Half-cleaner across lane bit 4 or 5 (l ^ 16, l ^ 32) on pairs of keys: v_permlane16/32_swap
+// of keys (a, b) leaves each lane holding both members of one pair -- a[l] and a[l ^ M] in
+// the lanes with the bit clear, b[l ^ M] and b[l] in the others, the lower position always
+// in the first register -- so one min/max pair does the stage for both keys, and a second
+// swap puts them back.  Four VALU per two keys, no lane masks.
+template <int M, int R>
+__device__ __forceinline__ void swap_stage(unsigned (&key)[R]) {
+#pragma unroll
+  for (int r = 0; r < R; r += 2) {
+    unsigned lo, hi;
+    if constexpr (M == 32) {
+      const auto s1 = __builtin_amdgcn_permlane32_swap(key[r], key[r + 1], false, false);
+      lo = min(s1[0], s1[1]);
+      hi = max(s1[0], s1[1]);
+      const auto s2 = __builtin_amdgcn_permlane32_swap(lo, hi, false, false);
+      key[r] = s2[0];
+      key[r + 1] = s2[1];
+    } else {
+      const auto s1 = __builtin_amdgcn_permlane16_swap(key[r], key[r + 1], false, false);
+      lo = min(s1[0], s1[1]);
+      hi = max(s1[0], s1[1]);
+      const auto s2 = __builtin_amdgcn_permlane16_swap(lo, hi, false, false);
+      key[r] = s2[0];
+      key[r + 1] = s2[1];
+    }
+  }
 }
 
 // One stage of the flip-form bitonic network over PN = 64*NN*R keys, position q = t*R + r:
@@ -213,6 +254,11 @@ __device__ __forceinline__ void wide_stage(unsigned (&key)[R], unsigned* sX, int
     const bool lower = (lane & (flip ? (K / R / 2) : MK)) == 0;
     if constexpr (R == 8 && dpp_fusable(MK)) {
       dpp_stage8<MK, flip>(key, (uint64_t)ballot(lower));
+      if constexpr (J > 1) wide_stage<NN, NW, R, K, J / 2>(key, sX, t, lane);
+      return;
+    }
+    if constexpr (!flip && (MK == 16 || MK == 32)) {
+      swap_stage<MK, R>(key);
       if constexpr (J > 1) wide_stage<NN, NW, R, K, J / 2>(key, sX, t, lane);
       return;
     }

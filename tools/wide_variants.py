@@ -44,6 +44,59 @@ VARIANTS = {
     "wmergef": [("consensus.hip", "const bool merge_np2 = mode == BCE_MODE_EXACT;", "const bool merge_np2 = true;")],
     # round-2/3 lane stages: v_mov_b32_dpp + v_cmp + s_xor + v_cndmask per key (no DPP fusion)
     "wnodpp": [("consensus_wide.hip", "if constexpr (R == 8 && dpp_fusable(MK)) {", "if constexpr (false) {")],
+    # half-cleaners across lane bits 4/5 through permlane + compare in VCC instead of the swap trick
+    "wnoswap": [("consensus_wide.hip", "if constexpr (!flip && (MK == 16 || MK == 32)) {", "if constexpr (false) {")],
+    # ---- exact-preserving ablations: a compare-exchange stage applied twice is a no-op on
+    # the data, so these time one class of sort stages without changing the results
+    "xin2": [("consensus_wide.hip", """        key[r] = x < y ? x : y;
+        key[r2] = x < y ? y : x;""", """        unsigned a1 = x < y ? x : y, b1 = x < y ? y : x;
+        asm volatile("" : "+v"(a1), "+v"(b1));
+        key[r] = a1 < b1 ? a1 : b1;
+        key[r2] = a1 < b1 ? b1 : a1;""")],
+    "xlane2": [("consensus_wide.hip", "      dpp_stage8<MK, flip>(key, (uint64_t)ballot(lower));\n",
+                "      dpp_stage8<MK, flip>(key, (uint64_t)ballot(lower));\n      dpp_stage8<MK, flip>(key, (uint64_t)ballot(lower));\n"),
+               ("consensus_wide.hip", """    for (int r = 0; r < R; ++r) key[r] = ((key[r] < y[r]) == lower) ? key[r] : y[r];
+  } else {""", """    for (int r = 0; r < R; ++r) key[r] = ((key[r] < y[r]) == lower) ? key[r] : y[r];
+#pragma unroll
+    for (int r = 0; r < R; ++r) y[r] = lane_xor<MK>(key[flip ? R - 1 - r : r]);
+#pragma unroll
+    for (int r = 0; r < R; ++r) key[r] = ((key[r] < y[r]) == lower) ? key[r] : y[r];
+  } else {""")],
+    "xxw2": [("consensus_wide.hip", """      key[r] = ((key[r] < yr) == lower) ? key[r] : yr;
+    }
+  }
+  if constexpr (J > 1)""", """      key[r] = ((key[r] < yr) == lower) ? key[r] : yr;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R; r += 4)
+      *reinterpret_cast<uint4*>(buf + (r >> 2) * PL + t * 4) = make_uint4(key[r], key[r + 1], key[r + 2], key[r + 3]);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R; r += 4) {
+      const uint4 y4 = real ? *reinterpret_cast<const uint4*>(buf + (r >> 2) * PL + (t ^ MT) * 4)
+                            : make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+      y[r] = y4.x;
+      y[r + 1] = y4.y;
+      y[r + 2] = y4.z;
+      y[r + 3] = y4.w;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const unsigned yr = y[flip ? R - 1 - r : r];
+      key[r] = ((key[r] < yr) == lower) ? key[r] : yr;
+    }
+  }
+  if constexpr (J > 1)""")],
+    # one extra workgroup barrier per stage on the wave-crossing stages only (no LDS work)
+    "xxwbar": [("consensus_wide.hip", """      key[r] = ((key[r] < yr) == lower) ? key[r] : yr;
+    }
+  }
+  if constexpr (J > 1)""", """      key[r] = ((key[r] < yr) == lower) ? key[r] : yr;
+    }
+    __syncthreads();
+  }
+  if constexpr (J > 1)""")],
     # ---- ablations (timing only; outputs are wrong by construction) ----
     # the sort network run twice (the second pass on sorted keys costs the same)
     "xsort2": [("consensus_wide.hip", "    wide_sort<NN, NW, R>(key, sX, t, lane);\n",
