@@ -37,7 +37,7 @@
 
 #pragma clang fp contract(off)
 
-constexpr int kWideHR = 2;       // rounds of NT uniques whose gathers are in flight together
+constexpr int kWideHR = 1;       // rounds of NT uniques whose gathers are in flight together (2: C3 fast +6%)
 constexpr int kWideWPE = 4;      // min waves per SIMD (register budget; 4 vs 2: exact -1.3%, fast unchanged)
 constexpr int kWideNWBF = 4;     // FAST nweight read-backs per batch (1: 1.645, 2: 1.634, 4: 1.587 ms C3)
 

@@ -46,6 +46,48 @@ VARIANTS = {
     "wnodpp": [("consensus_wide.hip", "if constexpr (R == 8 && dpp_fusable(MK)) {", "if constexpr (false) {")],
     # half-cleaners across lane bits 4/5 through permlane + compare in VCC instead of the swap trick
     "wnoswap": [("consensus_wide.hip", "if constexpr (!flip && (MK == 16 || MK == 32)) {", "if constexpr (false) {")],
+    # gathers of 2 rounds of uniques in flight together (default 1; 3 and 4 were slower still)
+    "whr2": [("consensus_wide.hip", "constexpr int kWideHR = 1;", "constexpr int kWideHR = 2;")],
+    # phase timer (s_memtime stamps of wave 0 per market, summed per workgroup size): timing aid only
+    "wprof": [("consensus_wide.hip", "namespace bce {\nnamespace {\n\nconstexpr int ilog2c",
+               "__device__ unsigned long long g_wprof[16 * 8];\n#define WPS(p) { const unsigned long long _n = __builtin_amdgcn_s_memtime(); pacc[p] += _n - pt0; pt0 = _n; }\n"
+               "namespace bce {\nnamespace {\n\nconstexpr int ilog2c"),
+              ("consensus_wide.hip", "  for (int64_t li = blockIdx.x; li < a.n_list; li += G) {\n",
+               "  unsigned long long pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};\n  unsigned long long pt0 = 0;\n"
+               "  for (int64_t li = blockIdx.x; li < a.n_list; li += G) {\n    pt0 = __builtin_amdgcn_s_memtime();\n"),
+              ("consensus_wide.hip", "    // ---- 2. sort (core.py:103", "    WPS(0);\n    // ---- 2. sort (core.py:103"),
+              ("consensus_wide.hip", "    wide_sort<NN, NW, R>(key, sX, t, lane);\n", "    wide_sort<NN, NW, R>(key, sX, t, lane);\n    WPS(1);\n"),
+              ("consensus_wide.hip", "    __syncthreads();  // (a) input-order", "    __syncthreads(); WPS(2); // (a) input-order"),
+              ("consensus_wide.hip", "    __syncthreads();  // (b) every read", "    __syncthreads(); WPS(3); // (b) every read"),
+              ("consensus_wide.hip", "    __syncthreads();  // (c) sorted probs", "    __syncthreads(); WPS(4); // (c) sorted probs"),
+              ("consensus_wide.hip", "    // ---- 5. next market's probabilities", "    WPS(5);\n    // ---- 5. next market's probabilities"),
+              ("consensus_wide.hip", "    __syncthreads();  // totals + w[j] visible", "    __syncthreads(); WPS(6); // totals + w[j] visible"),
+              ("consensus_wide.hip", """          }
+        }
+      }
+    }
+  }
+}
+
+template <int NW, int R, bool FAST, int NN = NW>""", """          }
+        }
+      }
+    }
+    WPS(7);
+  }
+  if (t == 0)
+    for (int p = 0; p < 8; ++p) atomicAdd(&g_wprof[NW * 8 + p], pacc[p]);
+}
+
+template <int NW, int R, bool FAST, int NN = NW>"""),
+              ("consensus_wide.hip", "}  // namespace bce\n", """}  // namespace bce
+
+extern "C" int bce_debug_wprof(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wprof), sizeof(g_wprof)) != hipSuccess) return 1;
+  static unsigned long long zero[16 * 8] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_wprof), zero, sizeof(g_wprof)) != hipSuccess;
+}
+""")],
     # ---- exact-preserving ablations: a compare-exchange stage applied twice is a no-op on
     # the data, so these time one class of sort stages without changing the results
     "xin2": [("consensus_wide.hip", """        key[r] = x < y ? x : y;
@@ -147,6 +189,23 @@ def one(name, mode, reps):
     ms = sorted(a.elapsed_time(b) for a, b in ev)
     out = {"variant": name, "mode": mode, "median_ms": ms[len(ms) // 2], "min_ms": ms[0]}
     N.check_faults()
+    if name == "wprof":  # per workgroup size: share of wave 0's cycles per phase (timed reps only)
+        import ctypes
+        lib = N.lib()
+        buf = (ctypes.c_ulonglong * 128)()
+        lib.bce_debug_wprof(buf)  # clear what the ramp accumulated ...
+        for _ in range(reps):
+            batch.consensus(*d, table, plan=plan, mode=mode, out=res)
+        torch.cuda.synchronize()
+        lib.bce_debug_wprof(buf)  # ... and read the timed reps
+        names = ["keys", "sort", "bar_a", "x+leaders+bar_b", "stores+bar_c", "per_unique", "totals+bar", "nweight"]
+        prof = {}
+        for nw in range(1, 9):
+            v = [buf[nw * 8 + p] for p in range(8)]
+            if sum(v):
+                prof[f"nw{nw}"] = {k: round(x / sum(v), 4) for k, x in zip(names, v)}
+                prof[f"nw{nw}"]["cycles"] = sum(v)
+        out["phases"] = prof
     print(json.dumps(out), flush=True)
 
 
