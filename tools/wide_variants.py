@@ -46,8 +46,6 @@ VARIANTS = {
     "wnodpp": [("consensus_wide.hip", "if constexpr (R == 8 && dpp_fusable(MK)) {", "if constexpr (false) {")],
     # half-cleaners across lane bits 4/5 through permlane + compare in VCC instead of the swap trick
     "wnoswap": [("consensus_wide.hip", "if constexpr (!flip && (MK == 16 || MK == 32)) {", "if constexpr (false) {")],
-    # gathers of 2 rounds of uniques in flight together (default 1; 3 and 4 were slower still)
-    "whr2": [("consensus_wide.hip", "constexpr int kWideHR = 1;", "constexpr int kWideHR = 2;")],
     # phase timer (s_memtime stamps of wave 0 per market, summed per workgroup size): timing aid only
     "wprof": [("consensus_wide.hip", "namespace bce {\nnamespace {\n\nconstexpr int ilog2c",
                "__device__ unsigned long long g_wprof[16 * 8];\n#define WPS(p) { const unsigned long long _n = __builtin_amdgcn_s_memtime(); pacc[p] += _n - pt0; pt0 = _n; }\n"
@@ -88,6 +86,17 @@ extern "C" int bce_debug_wprof(unsigned long long* out) {
   return hipMemcpyToSymbol(HIP_SYMBOL(g_wprof), zero, sizeof(g_wprof)) != hipSuccess;
 }
 """)],
+    # more waves per SIMD for the 3-wave and 1-wave kernels (register budget 102 / 85)
+    "w3wpe5": [("consensus_wide.hip", "static constexpr int WPE = kWideWPE;",
+                "static constexpr int WPE = (NW == 3) ? 5 : kWideWPE;")],
+    "w1wpe5": [("consensus_wide.hip", "static constexpr int WPE = kWideWPE;",
+                "static constexpr int WPE = (NW == 1) ? 5 : kWideWPE;")],
+    "w1wpe6": [("consensus_wide.hip", "static constexpr int WPE = kWideWPE;",
+                "static constexpr int WPE = (NW == 1) ? 6 : kWideWPE;")],
+    "w36wpe5": [("consensus_wide.hip", "static constexpr int WPE = kWideWPE;",
+                "static constexpr int WPE = (NW == 3 || NW == 6) ? 5 : kWideWPE;")],
+    # each market's probabilities loaded one market ahead (round 2/3) instead of at its start
+    "wahead": [("consensus_wide.hip", "constexpr bool kWideProbsLate = true;", "constexpr bool kWideProbsLate = false;")],
     # ---- exact-preserving ablations: a compare-exchange stage applied twice is a no-op on
     # the data, so these time one class of sort stages without changing the results
     "xin2": [("consensus_wide.hip", """        key[r] = x < y ? x : y;
@@ -144,14 +153,14 @@ extern "C" int bce_debug_wprof(unsigned long long* out) {
     "xsort2": [("consensus_wide.hip", "    wide_sort<NN, NW, R>(key, sX, t, lane);\n",
                 "    wide_sort<NN, NW, R>(key, sX, t, lane);\n    wide_sort<NN, NW, R>(key, sX, t, lane);\n")],
     # no relconf / present-bit gathers (constant rows)
-    "xnogather": [("consensus_wide.hip", "rc[i] = a.relconf[sids[i]];", "rc[i] = make_double2(0.5 + 1e-9 * sids[i], 0.25);"),
-                  ("consensus_wide.hip", "pwd[i] = a.pbits[sids[i] >> 5];", "pwd[i] = 0xFFFFFFFFu;")],
+    "xnogather": [("consensus_wide.hip", "          rc = a.relconf[sid];\n          pwd = a.pbits[sid >> 5];",
+                   "          rc = make_double2(0.5 + 1e-9 * sid, 0.25);\n          pwd = 0xFFFFFFFFu;")],
     # no normalizedWeight phase
     "xnonw": [("consensus_wide.hip", "    if (a.nweight) {  // core.py:151", "    if (false) {  // core.py:151")],
     # no sorted-probability gather from region A
     "xnosp": [("consensus_wide.hip", "x[r] = (q < n) ? sA[key[r] & QMASK] : 0.0;", "x[r] = (q < n) ? 0.5 : 0.0;")],
     # no run sums (constant averages)
-    "xnorun": [("consensus_wide.hip", "avg = (jj < u && len <= kWaveRun) ? run_sum(sA + q0s[i], len) : 0.0;",
+    "xnorun": [("consensus_wide.hip", "avg = (jj < u && len <= kWaveRun) ? run_sum(sA + q0, len) : 0.0;",
                 "avg = (jj < u) ? 0.5 : 0.0;")],
 }
 
