@@ -37,8 +37,7 @@
 
 #pragma clang fp contract(off)
 
-constexpr bool kWideProbsLate = true;  // a market's probs loaded at its start, not one market ahead:
-                                       // 16 fewer VGPRs live through the per-unique phase (-4%)  // the next round's gathers issued before this round's arithmetic
+constexpr int kWideHR = 1;       // rounds of NT uniques whose gathers are in flight together (2: C3 fast +6%)
 constexpr int kWideWPE = 4;      // min waves per SIMD (register budget; 4 vs 2: exact -1.3%, fast unchanged)
 constexpr int kWideNWBF = 4;     // FAST nweight read-backs per batch (1: 1.645, 2: 1.634, 4: 1.587 ms C3)
 
@@ -59,7 +58,7 @@ struct WideCfg {
   static constexpr int PN = 64 * NN * R;
   static constexpr int IB = ilog2c(PN);
   static constexpr int XROW = R;      // exchange row (u32), two buffers
-  static constexpr int HR = 1;  // EXACT producer rounds with gathers in flight together (2 spilled: +4%)
+  static constexpr int HR = (R < kWideHR) ? R : kWideHR;
   // register budget: workgroups of >= 4 waves get 4 waves per SIMD (<= 128 VGPRs), so two
   // LDS-sized workgroups share a CU
   // (the 6-wave FAST kernel at 5 waves per SIMD, <= 102 VGPRs, so three workgroups share a
@@ -489,14 +488,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
   if (blockIdx.x < a.n_list) {
     meta(blockIdx.x);
     load_sids();
-    if (!kWideProbsLate) load_probs();
+    load_probs();
   }
 
   for (int64_t li = blockIdx.x; li < a.n_list; li += G) {
     const int32_t m = nm;
     const int64_t off = noff;
     const int n = nn;
-    if (kWideProbsLate) load_probs();  // this market's probabilities land during the sort
 
     // ---- 1. keys; next market's metadata + sids ------------------------------------
     unsigned key[R];
@@ -510,28 +508,22 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
     }
     if (ballot(badsid)) raise_fault(a.fault, kFaultSid);
     int myerr = kNoErr;
-    // input-order probs into region A (range-checked on the way, core.py:59-60); region A's
-    // last readers are the previous market's run sums (before its final barrier) unless
-    // normalizedWeight reads w[j] from it.  Late: after the sort, whose wave-crossing
-    // stages (NW > 1) put every wave past the previous market, so no barrier of its own.
-    auto stage_probs = [&]() {
+    // input-order probs into region A before the next loads; region A's last readers are
+    // the previous market's run sums (before its final barrier) unless normalizedWeight
+    // reads w[j] from it
+    if (NW > 1 && !wback) __syncthreads();
 #pragma unroll
-      for (int c = 0; c < R; ++c) {
-        const int i = c * NT + t;
-        const double p = pp[c];
-        sA[i] = p;
-        if ((i < n) && (p < 0.0 || p > 1.0) && myerr == kNoErr) myerr = i;
-      }
-    };
-    if (!kWideProbsLate) {
-      if (NW > 1 && !wback) __syncthreads();
-      stage_probs();
+    for (int c = 0; c < R; ++c) {
+      const int i = c * NT + t;
+      const double p = pp[c];
+      sA[i] = p;
+      if ((i < n) && (p < 0.0 || p > 1.0) && myerr == kNoErr) myerr = i;  // core.py:59-60
     }
     const bool has_next = li + G < a.n_list;
     if (has_next) {
       meta(li + G);
       load_sids();
-      if (!kWideProbsLate) load_probs();
+      load_probs();
     }
     if (n > P) {  // longer than this launch's max_len: left unprocessed, reported
       raise_fault(a.fault, kFaultTooLong);
@@ -541,7 +533,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
 
     // ---- 2. sort (core.py:103 order; ties in input order by the index bits) ----------
     wide_sort<NN, NW, R>(key, sX, t, lane);
-    if (kWideProbsLate) stage_probs();
 
     // ---- 3. input-order probs + range check, sorted probs in place, leaders ----------
     if (lane == 63) sLast[wv] = key[R - 1];
@@ -694,84 +685,104 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
     }
     const int nr = piped ? 0 : (u + NT - 1) / NT;
     const bool park = FAST && wback && u <= WFREE;
-    // one round of NT uniques at a time: two rounds' gathers in flight together spilled
-    // (+6%), and issuing the next round's leaders + gathers ahead of this round's arithmetic
-    // waits out their LDS reads first (+7%, profiles/r03k/wide_probs_late_ab.txt)
-    auto fetch = [&](int jj, double2& rc, int& q0, int& q1, unsigned& sid, unsigned& pwd) {
-      q0 = q1 = 0;
-      sid = pwd = 0;
-      rc = make_double2(0.5, 0.25);  // DEFAULT_RELIABILITY / _CONFIDENCE (empty table)
-      if (jj < u) {
-        const unsigned lv = sLead[jj];
-        q0 = (int)(lv & QMASK);
-        sid = min(lv >> IB, smax);  // <= smax by construction of the key; clamped anyway
-        q1 = (jj + 1 < u) ? (int)(sLead[jj + 1] & QMASK) : n;
-        if (a.n_sources > 0) {
-          rc = a.relconf[sid];
-          pwd = a.pbits[sid >> 5];
+    for (int h = 0; h < nr; h += HR) {
+      double2 rc[HR];
+      int q0s[HR], q1s[HR];
+      unsigned sids[HR], pwd[HR];
+#pragma unroll
+      for (int i = 0; i < HR; ++i) {  // every gather of the group in flight together
+        const int jj = (h + i) * NT + t;
+        q0s[i] = q1s[i] = 0;
+        sids[i] = pwd[i] = 0;
+        rc[i] = make_double2(0.5, 0.25);  // DEFAULT_RELIABILITY / _CONFIDENCE (empty table)
+        if (jj < u) {
+          const unsigned lv = sLead[jj];
+          q0s[i] = (int)(lv & QMASK);
+          sids[i] = min(lv >> IB, smax);  // <= smax by construction of the key; clamped anyway
+          q1s[i] = (jj + 1 < u) ? (int)(sLead[jj + 1] & QMASK) : n;
+          if (a.n_sources > 0) {
+            rc[i] = a.relconf[sids[i]];
+            pwd[i] = a.pbits[sids[i] >> 5];
+          }
         }
       }
-    };
-    for (int h = 0; h < nr; ++h) {
-      const int jj = h * NT + t;
-      double2 rc;
-      int q0, q1;
-      unsigned sid, pwd;
-      fetch(jj, rc, q0, q1, sid, pwd);
-      const int len = q1 - q0;
-      double avg = 0.0;
-      if constexpr (FAST) {
-        // runs longer than kWaveRun (hot sources) are summed by the whole wave in a fixed
-        // order instead of by their own lane, so one hot source does not hold the wave
-        avg = (jj < u && len <= kWaveRun) ? run_sum(sA + q0, len) : 0.0;
-        unsigned long long lm = ballot(jj < u && len > kWaveRun);
-        while (lm) {
-          const int L = __builtin_ctzll(lm);
-          lm &= lm - 1;
-          const int lq0 = __builtin_amdgcn_readlane(q0, L), llen = __builtin_amdgcn_readlane(len, L);
-          double part = 0.0;
-          for (int e = lane; e < llen; e += 64) part += sA[lq0 + e];
-          part = wave_sum_fixed(part);
-          if (lane == L) avg = part / (double)llen;
+      double vw[HR], va[HR], vc[HR];
+#pragma unroll
+      for (int i = 0; i < HR; ++i) {
+        const int jj = (h + i) * NT + t;
+        const int len = q1s[i] - q0s[i];
+        double avg = 0.0;
+        if constexpr (FAST) {
+          // runs longer than kWaveRun (hot sources) are summed by the whole wave in a fixed
+          // order instead of by their own lane, so one hot source does not hold the wave
+          avg = (jj < u && len <= kWaveRun) ? run_sum(sA + q0s[i], len) : 0.0;
+          unsigned long long lm = ballot(jj < u && len > kWaveRun);
+          while (lm) {
+            const int L = __builtin_ctzll(lm);
+            lm &= lm - 1;
+            const int lq0 = __builtin_amdgcn_readlane(q0s[i], L), llen = __builtin_amdgcn_readlane(len, L);
+            double part = 0.0;
+            for (int e = lane; e < llen; e += 64) part += sA[lq0 + e];
+            part = wave_sum_fixed(part);
+            if (lane == L) avg = part / (double)llen;
+          }
+        } else if (jj < u) {
+          avg = run_sum(sA + q0s[i], len);
         }
-      } else if (jj < u) {
-        avg = run_sum(sA + q0, len);
-      }
-      double vw = 0.0, va = 0.0, vc = 0.0;
-      if (jj < u) {
-        const double w = rc.x;  // core.py:111,119
-        vw = w;
-        va = avg * w;        // core.py:136
-        vc = rc.y * w;       // core.py:142
+        vw[i] = va[i] = vc[i] = 0.0;
+        if (jj < u) {
+          const double w = rc[i].x;  // core.py:111,119
+          vw[i] = w;
+          va[i] = avg * w;        // core.py:136
+          vc[i] = rc[i].y * w;    // core.py:142
+        }
       }
       if constexpr (FAST) {
-        pw += vw;  // round order: fixed per thread
-        pa += va;
-        pc += vc;
+#pragma unroll
+        for (int i = 0; i < HR; ++i) {  // round order: fixed per thread
+          pw += vw[i];
+          pa += va[i];
+          pc += vc[i];
+        }
         if (!wback) {
-          __syncthreads();  // every sorted-prob read of this round done
-          if (jj < u) sA[jj] = vw;  // later rounds read only slots > jj
+          __syncthreads();  // every sorted-prob read of this group done
+#pragma unroll
+          for (int i = 0; i < HR; ++i) {
+            const int jj = (h + i) * NT + t;
+            if (jj < u) sA[jj] = vw[i];  // later groups read only slots > jj
+          }
         }
       } else {
-        double* const buf = sWAC + (h & 1) * 3 * NT;
-        buf[t] = vw;
-        buf[NT + t] = va;
-        buf[2 * NT + t] = vc;
-        __syncthreads();  // round staged; every sorted-prob read of this round is done
-        if (jj < u && !wback) sA[jj] = vw;  // slot jj is only read by uniques <= jj
-        if (wv == 0) {
-          __builtin_amdgcn_s_setprio(2);  // the chain is the critical path
-          const int ce = (u - h * NT < NT) ? u - h * NT : NT;
-          chain_add(acc, buf + (lane % 3) * NT, ce);
-          __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+        for (int i = 0; i < HR; ++i) {
+          if (h + i < nr) {
+            double* const buf = sWAC + ((h + i) & 1) * 3 * NT;
+            buf[t] = vw[i];
+            buf[NT + t] = va[i];
+            buf[2 * NT + t] = vc[i];
+            __syncthreads();  // round staged; every sorted-prob read of this group is done
+            const int jj = (h + i) * NT + t;
+            if (jj < u && !wback) sA[jj] = vw[i];  // slot jj is only read by uniques <= jj
+            if (wv == 0) {
+              __builtin_amdgcn_s_setprio(2);  // the chain is the critical path
+              const int ce = (u - (h + i) * NT < NT) ? u - (h + i) * NT : NT;
+              chain_add(acc, buf + (lane % 3) * NT, ce);
+              __builtin_amdgcn_s_setprio(0);
+            }
+          }
         }
       }
-      // per-unique outputs after the round's LDS work, so no store is pending under it
-      if (jj < u) {
-        const int64_t p = off + jj;
-        if (a.usid) a.usid[p] = (int32_t)sid | (((pwd >> (sid & 31)) & 1u) ? 0 : (int32_t)0x80000000);
-        if (a.weight) a.weight[p] = vw;
-        if (park) sW[jj] = vw;
+      // per-unique outputs after the group's LDS work, so no store is pending under it
+#pragma unroll
+      for (int i = 0; i < HR; ++i) {
+        const int jj = (h + i) * NT + t;
+        if (jj < u) {
+          const int64_t p = off + jj;
+          if (a.usid)
+            a.usid[p] = (int32_t)sids[i] | (((pwd[i] >> (sids[i] & 31)) & 1u) ? 0 : (int32_t)0x80000000);
+          if (a.weight) a.weight[p] = vw[i];
+          if (park) sW[jj] = vw[i];
+        }
       }
     }
 

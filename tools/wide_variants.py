@@ -95,8 +95,10 @@ extern "C" int bce_debug_wprof(unsigned long long* out) {
                 "static constexpr int WPE = (NW == 1) ? 6 : kWideWPE;")],
     "w36wpe5": [("consensus_wide.hip", "static constexpr int WPE = kWideWPE;",
                 "static constexpr int WPE = (NW == 3 || NW == 6) ? 5 : kWideWPE;")],
-    # each market's probabilities loaded one market ahead (round 2/3) instead of at its start
-    "wahead": [("consensus_wide.hip", "constexpr bool kWideProbsLate = true;", "constexpr bool kWideProbsLate = false;")],
+    # two rounds of uniques with their gathers in flight together (round 2/3 default; +6%)
+    "whr2": [("consensus_wide.hip", "constexpr int kWideHR = 1;", "constexpr int kWideHR = 2;")],
+    # each market's probabilities loaded at its start and staged after the sort, instead of one
+    # market ahead: +2.6% fast, -0.6% exact (profiles/r03k/wide_probs_late_ab.txt)
     # ---- exact-preserving ablations: a compare-exchange stage applied twice is a no-op on
     # the data, so these time one class of sort stages without changing the results
     "xin2": [("consensus_wide.hip", """        key[r] = x < y ? x : y;
@@ -153,14 +155,14 @@ extern "C" int bce_debug_wprof(unsigned long long* out) {
     "xsort2": [("consensus_wide.hip", "    wide_sort<NN, NW, R>(key, sX, t, lane);\n",
                 "    wide_sort<NN, NW, R>(key, sX, t, lane);\n    wide_sort<NN, NW, R>(key, sX, t, lane);\n")],
     # no relconf / present-bit gathers (constant rows)
-    "xnogather": [("consensus_wide.hip", "          rc = a.relconf[sid];\n          pwd = a.pbits[sid >> 5];",
-                   "          rc = make_double2(0.5 + 1e-9 * sid, 0.25);\n          pwd = 0xFFFFFFFFu;")],
+    "xnogather": [("consensus_wide.hip", "rc[i] = a.relconf[sids[i]];", "rc[i] = make_double2(0.5 + 1e-9 * sids[i], 0.25);"),
+                  ("consensus_wide.hip", "pwd[i] = a.pbits[sids[i] >> 5];", "pwd[i] = 0xFFFFFFFFu;")],
     # no normalizedWeight phase
     "xnonw": [("consensus_wide.hip", "    if (a.nweight) {  // core.py:151", "    if (false) {  // core.py:151")],
     # no sorted-probability gather from region A
     "xnosp": [("consensus_wide.hip", "x[r] = (q < n) ? sA[key[r] & QMASK] : 0.0;", "x[r] = (q < n) ? 0.5 : 0.0;")],
     # no run sums (constant averages)
-    "xnorun": [("consensus_wide.hip", "avg = (jj < u && len <= kWaveRun) ? run_sum(sA + q0, len) : 0.0;",
+    "xnorun": [("consensus_wide.hip", "avg = (jj < u && len <= kWaveRun) ? run_sum(sA + q0s[i], len) : 0.0;",
                 "avg = (jj < u) ? 0.5 : 0.0;")],
 }
 
