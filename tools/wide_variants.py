@@ -97,8 +97,10 @@ extern "C" int bce_debug_wprof(unsigned long long* out) {
                 "static constexpr int WPE = (NW == 3 || NW == 6) ? 5 : kWideWPE;")],
     # two rounds of uniques with their gathers in flight together (round 2/3 default; +6%)
     "whr2": [("consensus_wide.hip", "constexpr int kWideHR = 1;", "constexpr int kWideHR = 2;")],
-    # each market's probabilities loaded at its start and staged after the sort, instead of one
-    # market ahead: +2.6% fast, -0.6% exact (profiles/r03k/wide_probs_late_ab.txt)
+    # (each market's probabilities loaded at its start and staged after the sort instead of one
+    # market ahead: +2.6% fast, -0.6% exact, profiles/r03k/wide_probs_late_ab.txt)
+    # every wide bin on st (no alternation of small bins with the side stream)
+    "wnoalt": [("consensus.hip", "constexpr int kSmallRounds = 4;", "constexpr int kSmallRounds = 0;")],
     # ---- exact-preserving ablations: a compare-exchange stage applied twice is a no-op on
     # the data, so these time one class of sort stages without changing the results
     "xin2": [("consensus_wide.hip", """        key[r] = x < y ? x : y;
