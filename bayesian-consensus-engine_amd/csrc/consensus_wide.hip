@@ -133,7 +133,8 @@ constexpr int xw_index(int K, int J, int R) {
 // compiler neither folds DPP into a compare nor into a select whose DPP operand is src1,
 // and gfx950 has no VOPC DPP).  FLIP: key r's partner is key R-1-r of the partner lane.
 // The outputs are early-clobber, so no instruction in the block reads a register written
-// in it; `s_nop 1` covers the VALU-write -> DPP-read hazard on the inputs.
+// in it; `s_nop 1` covers the VALU-write -> DPP-read hazard on the inputs; the s_xor writes
+// SCC, so the block clobbers it (a scalar branch condition computed before it is dead).
 #define BCE_DPP_CAS(O, A, B, C)                                                  \
   "v_sub_co_u32_dpp %[j], vcc, %[" B "], %[" A "] " C " row_mask:0xf bank_mask:0xf\n" \
   "s_xor_b64 vcc, vcc, %[lm]\n"                                                  \
@@ -146,7 +147,7 @@ constexpr int xw_index(int K, int J, int R) {
         [o5] "=&v"(o[5]), [o6] "=&v"(o[6]), [o7] "=&v"(o[7]), [j] "=&v"(junk)                                  \
       : [k0] "v"(s[0]), [k1] "v"(s[1]), [k2] "v"(s[2]), [k3] "v"(s[3]), [k4] "v"(s[4]), [k5] "v"(s[5]),        \
         [k6] "v"(s[6]), [k7] "v"(s[7]), [lm] "s"(lower)                                                        \
-      : "vcc")
+      : "vcc", "scc")
 #define BCE_DPP_STAGE8_ANY(C, FLIP)                                                   \
   do {                                                                                \
     if (FLIP)                                                                         \
@@ -262,6 +263,22 @@ __device__ __forceinline__ void wide_stage(unsigned (&key)[R], unsigned* sX, int
       if constexpr (J > 1) wide_stage<NN, NW, R, K, J / 2>(key, sX, t, lane);
       return;
     }
+    if constexpr (flip && MK == 31) {
+      // the flip of merge K = 32R as a reversal of each K-block's upper half (q ^ (K/2 - 1):
+      // row_mirror of key R-1-r, written in rows 1 and 3 only) and a half-cleaner on lane
+      // bit 4 -- the pairs are the same; the upper half then holds its bitonic sequence
+      // reversed, which the following half-cleaners sort as well (a reversed bitonic
+      // sequence is bitonic), so the merge's output is the same sorted sequence
+      unsigned nk[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        nk[r] = (unsigned)__builtin_amdgcn_update_dpp((int)key[r], (int)key[R - 1 - r], 0x140, 0xA, 0xF, false);
+#pragma unroll
+      for (int r = 0; r < R; ++r) key[r] = nk[r];
+      swap_stage<16, R>(key);
+      if constexpr (J > 1) wide_stage<NN, NW, R, K, J / 2>(key, sX, t, lane);
+      return;
+    }
     unsigned y[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) y[r] = lane_xor<MK>(key[flip ? R - 1 - r : r]);
@@ -291,10 +308,14 @@ __device__ __forceinline__ void wide_stage(unsigned (&key)[R], unsigned* sX, int
       y[r + 2] = y4.z;
       y[r + 3] = y4.w;
     }
+    // `lower` is uniform over the wave here (the partner is a whole wave away): one min or
+    // one max per key under a scalar branch, no compare in VCC
+    if (__builtin_amdgcn_readfirstlane((int)lower)) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const unsigned yr = y[flip ? R - 1 - r : r];
-      key[r] = ((key[r] < yr) == lower) ? key[r] : yr;
+      for (int r = 0; r < R; ++r) key[r] = min(key[r], y[flip ? R - 1 - r : r]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) key[r] = max(key[r], y[flip ? R - 1 - r : r]);
     }
   }
   if constexpr (J > 1) wide_stage<NN, NW, R, K, J / 2>(key, sX, t, lane);
@@ -772,15 +793,16 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
           }
         }
       }
-      // per-unique outputs after the group's LDS work, so no store is pending under it
+      // per-unique outputs after the group's LDS work, so no store is pending under it;
+      // nontemporal (FAST -0.5..1%, profiles/r03k/wide_r03u_ab.txt)
 #pragma unroll
       for (int i = 0; i < HR; ++i) {
         const int jj = (h + i) * NT + t;
         if (jj < u) {
           const int64_t p = off + jj;
           if (a.usid)
-            a.usid[p] = (int32_t)sids[i] | (((pwd[i] >> (sids[i] & 31)) & 1u) ? 0 : (int32_t)0x80000000);
-          if (a.weight) a.weight[p] = vw[i];
+            __builtin_nontemporal_store((int32_t)sids[i] | (((pwd[i] >> (sids[i] & 31)) & 1u) ? 0 : (int32_t)0x80000000), &a.usid[p]);
+          if (a.weight) __builtin_nontemporal_store(vw[i], &a.weight[p]);
           if (park) sW[jj] = vw[i];
         }
       }
@@ -845,7 +867,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
 #pragma unroll
           for (int k = 0; k < NB; ++k) {
             const int jj = j0 + NT * k;
-            if (jj < u) a.nweight[off + jj] = (tw > 0.0) ? wj[k] / tw : 0.0;
+            if (jj < u) __builtin_nontemporal_store((tw > 0.0) ? wj[k] / tw : 0.0, &a.nweight[off + jj]);
           }
         }
       }

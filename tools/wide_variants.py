@@ -99,8 +99,32 @@ extern "C" int bce_debug_wprof(unsigned long long* out) {
     "whr2": [("consensus_wide.hip", "constexpr int kWideHR = 1;", "constexpr int kWideHR = 2;")],
     # (each market's probabilities loaded at its start and staged after the sort instead of one
     # market ahead: +2.6% fast, -0.6% exact, profiles/r03k/wide_probs_late_ab.txt)
-    # every wide bin on st (no alternation of small bins with the side stream)
-    "wnoalt": [("consensus.hip", "constexpr int kSmallRounds = 4;", "constexpr int kSmallRounds = 0;")],
+    # (alternating the wide bins of a market shard between st and the side stream -- bins under
+    # 4 rounds of resident workgroups -- made the 1/8 shard step slower, 0.241 -> 0.277 ms,
+    # profiles/r03k/c3_shards_alt.json; not kept)
+    # two rounds of gathers in flight for the 1-wave kernels only (lower register pressure): no gain
+    "whr2nw1": [("consensus_wide.hip", "static constexpr int HR = (R < kWideHR) ? R : kWideHR;",
+                 "static constexpr int HR = (NW == 1) ? ((R < 2) ? R : 2) : kWideHR;")],
+    # the K = 32R flip stage through the generic lane exchange (compare in VCC)
+    "wnoflip31": [("consensus_wide.hip", "if constexpr (flip && MK == 31) {", "if constexpr (false) {")],
+    # wave-crossing stages with the per-key compare/select of round 2 instead of a uniform min/max
+    "wxwsel": [("consensus_wide.hip", """    if (__builtin_amdgcn_readfirstlane((int)lower)) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) key[r] = min(key[r], y[flip ? R - 1 - r : r]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) key[r] = max(key[r], y[flip ? R - 1 - r : r]);
+    }""", """#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const unsigned yr = y[flip ? R - 1 - r : r];
+      key[r] = ((key[r] < yr) == lower) ? key[r] : yr;
+    }""")],
+    # per-unique stores without the nontemporal hint (FAST +0.5..1%)
+    "wtst": [("consensus_wide.hip", """            __builtin_nontemporal_store((int32_t)sids[i] | (((pwd[i] >> (sids[i] & 31)) & 1u) ? 0 : (int32_t)0x80000000), &a.usid[p]);
+          if (a.weight) __builtin_nontemporal_store(vw[i], &a.weight[p]);""", """            a.usid[p] = (int32_t)sids[i] | (((pwd[i] >> (sids[i] & 31)) & 1u) ? 0 : (int32_t)0x80000000);
+          if (a.weight) a.weight[p] = vw[i];"""),
+             ("consensus_wide.hip", "            if (jj < u) __builtin_nontemporal_store((tw > 0.0) ? wj[k] / tw : 0.0, &a.nweight[off + jj]);",
+              "            if (jj < u) a.nweight[off + jj] = (tw > 0.0) ? wj[k] / tw : 0.0;")],
     # ---- exact-preserving ablations: a compare-exchange stage applied twice is a no-op on
     # the data, so these time one class of sort stages without changing the results
     "xin2": [("consensus_wide.hip", """        key[r] = x < y ? x : y;
@@ -117,10 +141,10 @@ extern "C" int bce_debug_wprof(unsigned long long* out) {
 #pragma unroll
     for (int r = 0; r < R; ++r) key[r] = ((key[r] < y[r]) == lower) ? key[r] : y[r];
   } else {""")],
-    "xxw2": [("consensus_wide.hip", """      key[r] = ((key[r] < yr) == lower) ? key[r] : yr;
+    "xxw2": [("consensus_wide.hip", """      for (int r = 0; r < R; ++r) key[r] = max(key[r], y[flip ? R - 1 - r : r]);
     }
   }
-  if constexpr (J > 1)""", """      key[r] = ((key[r] < yr) == lower) ? key[r] : yr;
+  if constexpr (J > 1)""", """      for (int r = 0; r < R; ++r) key[r] = max(key[r], y[flip ? R - 1 - r : r]);
     }
     __syncthreads();
 #pragma unroll
@@ -144,10 +168,10 @@ extern "C" int bce_debug_wprof(unsigned long long* out) {
   }
   if constexpr (J > 1)""")],
     # one extra workgroup barrier per stage on the wave-crossing stages only (no LDS work)
-    "xxwbar": [("consensus_wide.hip", """      key[r] = ((key[r] < yr) == lower) ? key[r] : yr;
+    "xxwbar": [("consensus_wide.hip", """      for (int r = 0; r < R; ++r) key[r] = max(key[r], y[flip ? R - 1 - r : r]);
     }
   }
-  if constexpr (J > 1)""", """      key[r] = ((key[r] < yr) == lower) ? key[r] : yr;
+  if constexpr (J > 1)""", """      for (int r = 0; r < R; ++r) key[r] = max(key[r], y[flip ? R - 1 - r : r]);
     }
     __syncthreads();
   }
