@@ -403,7 +403,8 @@ def bench_c2(args, world, rank):
     return out
 
 
-SECONDARY = (("c3", 20, 3), ("c4", 100, 10), ("tb", 10, 2), ("c5", 4, 1))  # (config, steps, warmup)
+# (config, steps, warmup, clock ramp s): the clock ramp as in each config's own line
+SECONDARY = (("c3", 20, 3, 1.0), ("c4", 100, 10, 1.0), ("tb", 10, 2, 1.0), ("c5", 4, 1, 0.5))
 
 
 def run_secondary(args, world, rank) -> dict:
@@ -417,9 +418,9 @@ def run_secondary(args, world, rank) -> dict:
     from bench_extra import run_extra
 
     out = {}
-    for cfg, steps, warmup in SECONDARY:
+    for cfg, steps, warmup, ramp in SECONDARY:
         a2 = copy.copy(args)
-        a2.config, a2.steps, a2.warmup, a2.prewarm_s, a2.mode = cfg, steps, warmup, 0.3, None
+        a2.config, a2.steps, a2.warmup, a2.prewarm_s, a2.mode = cfg, steps, warmup, ramp, None
         t0 = time.perf_counter()
         try:
             j = run_extra(a2, world, rank)

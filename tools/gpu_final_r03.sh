@@ -12,5 +12,5 @@ timeout -k 10 500 python3 bench.py > $o/default.json 2> $o/default.err && \
 timeout -k 10 240 python3 bench.py --config ns --steps 100 --warmup 10 > $o/ns.json 2> $o/ns.err && \
 timeout -k 10 240 python3 bench.py --config agg --steps 100 --warmup 10 > $o/agg.json 2> $o/agg.err && \
 timeout -k 10 300 python3 bench.py --config c3 --shard all/8 > $o/c3_shards.json 2> $o/c3_shards.err && \
-bash tools/gpu_profile.sh c2 consensus_tab32_kernel markets=1000000 signals_per_market=32 kernel=consensus_tab32_kernel -- && \
+bash tools/gpu_profile.sh c2 consensus_tab32_kernel markets=1000000 signals_per_market=32 kernel=consensus_tab32_kernel -- --no-secondary && \
 bash tools/gpu_profile.sh c3 consensus signals_this_rank=100000000 steps_total=15 -- --config c3
