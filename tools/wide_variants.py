@@ -125,6 +125,22 @@ extern "C" int bce_debug_wprof(unsigned long long* out) {
           if (a.weight) a.weight[p] = vw[i];"""),
              ("consensus_wide.hip", "            if (jj < u) __builtin_nontemporal_store((tw > 0.0) ? wj[k] / tw : 0.0, &a.nweight[off + jj]);",
               "            if (jj < u) a.nweight[off + jj] = (tw > 0.0) ? wj[k] / tw : 0.0;")],
+    # (a window of 1-3 rounds of gathers issued ahead of the round that uses them measured
+    # slower than one round at a time: 1.373-1.493 vs 1.346 ms, profiles/r03w/ab.txt)
+    # lane bits 0..1 as DPP-folded min and max (bound_ctrl) + a select on the lane mask: 3 VALU,
+    # no compare in VCC, instead of v_sub_co_u32_dpp / s_xor / v_cndmask_b32_dpp
+    "wqpmm": [("consensus_wide.hip", """  else if constexpr (M == 1) BCE_DPP_STAGE8_ANY("quad_perm:[1,0,3,2]", FLIP);
+  else if constexpr (M == 2) BCE_DPP_STAGE8_ANY("quad_perm:[2,3,0,1]", FLIP);
+  else if constexpr (M == 3) BCE_DPP_STAGE8_ANY("quad_perm:[3,2,1,0]", FLIP);""", """  else {
+    constexpr int CT = (M == 1) ? 0xB1 : (M == 2) ? 0x4E : 0x1B;
+    const bool lo_lane = (lower >> lane_id()) & 1;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const unsigned y = (unsigned)__builtin_amdgcn_update_dpp(0, (int)key[FLIP ? 7 - r : r], CT, 0xF, 0xF, true);
+      const unsigned mn = min(key[r], y), mx = max(key[r], y);
+      o[r] = lo_lane ? mn : mx;
+    }
+  }""")],
     # ---- exact-preserving ablations: a compare-exchange stage applied twice is a no-op on
     # the data, so these time one class of sort stages without changing the results
     "xin2": [("consensus_wide.hip", """        key[r] = x < y ? x : y;
