@@ -128,7 +128,7 @@ extern "C" int bce_debug_wprof(unsigned long long* out) {
     # (a window of 1-3 rounds of gathers issued ahead of the round that uses them measured
     # slower than one round at a time: 1.373-1.493 vs 1.346 ms, profiles/r03w/ab.txt)
     # lane bits 0..1 as DPP-folded min and max (bound_ctrl) + a select on the lane mask: 3 VALU,
-    # no compare in VCC, instead of v_sub_co_u32_dpp / s_xor / v_cndmask_b32_dpp
+    # no compare in VCC, instead of v_sub_co_u32_dpp / s_xor / v_cndmask_b32_dpp (+1%)
     "wqpmm": [("consensus_wide.hip", """  else if constexpr (M == 1) BCE_DPP_STAGE8_ANY("quad_perm:[1,0,3,2]", FLIP);
   else if constexpr (M == 2) BCE_DPP_STAGE8_ANY("quad_perm:[2,3,0,1]", FLIP);
   else if constexpr (M == 3) BCE_DPP_STAGE8_ANY("quad_perm:[3,2,1,0]", FLIP);""", """  else {
@@ -141,6 +141,10 @@ extern "C" int bce_debug_wprof(unsigned long long* out) {
       o[r] = lo_lane ? mn : mx;
     }
   }""")],
+    # (the 6-wave bin -- two workgroups per CU at 4 waves/SIMD -- with its probabilities loaded
+    # late to free 16 VGPRs, alone or at 5 waves/SIMD for three workgroups per CU (13 dwords
+    # still spilled), also with the 3-wave bin: 1.352 / 1.471 / 1.476 vs 1.345 ms,
+    # profiles/r03x/ab.txt; not kept)
     # ---- exact-preserving ablations: a compare-exchange stage applied twice is a no-op on
     # the data, so these time one class of sort stages without changing the results
     "xin2": [("consensus_wide.hip", """        key[r] = x < y ? x : y;
