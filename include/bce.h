@@ -126,7 +126,10 @@ int bce_validate_csr(const int64_t* offsets, int64_t n_markets, const double* pr
 
 /* Host-planned variant for ragged batches: the caller bins markets by length once
  * (bce_plan_bins on HOST offsets) and passes the device copy of the ordered market
- * list plus the bin boundaries.  bin_start has BCE_NBINS+1 entries (host array). */
+ * list plus the bin boundaries.  bin_start has BCE_NBINS+1 entries (host array).
+ * bce_consensus_planned runs the n <= 64 bins on a library-owned side stream (one per
+ * device) forked from `stream` by an event and joined back into it before it returns, so
+ * the caller sees ordinary stream order; concurrent callers are serialised over the fork. */
 #define BCE_NBINS 13 /* n<=8, <=16, <=32, <=64, <=128, <=256, <=512, <=1024, <=1536, <=2048, <=3072, <=4096, >4096 */
 int bce_plan_bins(const int64_t* offsets_host, int64_t n_markets, int32_t* order_host,
                   int64_t* bin_start_host, int32_t* max_len_host);
