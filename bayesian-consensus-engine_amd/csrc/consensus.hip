@@ -1754,7 +1754,13 @@ extern "C" int bce_consensus_planned(const int64_t* offsets, int64_t n_markets, 
   // kernel's LDS chain buffers allow two workgroups per CU at 3/6 waves as at 4/8, so the
   // smaller workgroup only loses latency hiding, and a separate launch adds a tail.
   const bool merge_np2 = mode == BCE_MODE_EXACT;
-  for (int b = BCE_NBINS - 1; b >= 0; --b) {
+  // Longest bins first, except that the 2049..3072 bin precedes the 3073..4096 one: its
+  // 6-wave workgroups leave 4 of a CU's 16 wave slots free (two per CU at 128 VGPRs), which
+  // the side stream's short-market kernels then fill (C3 fast -1.3%,
+  // profiles/r03x/order_ab.txt).
+  static const int kOrder[BCE_NBINS] = {12, 10, 11, 9, 8, 7, 6, 5, 4, 3, 2, 1, 0};
+  for (int oi = 0; oi < BCE_NBINS; ++oi) {
+    const int b = kOrder[oi];
     if (merge_np2 && (b == kBinNp2Lo || b == kBinNp2Hi)) continue;
     const int b0 = (merge_np2 && (b == kBinNp2Lo + 1 || b == kBinNp2Hi + 1)) ? b - 1 : b;
     ConsArgs a = base;

@@ -145,6 +145,16 @@ extern "C" int bce_debug_wprof(unsigned long long* out) {
     # late to free 16 VGPRs, alone or at 5 waves/SIMD for three workgroups per CU (13 dwords
     # still spilled), also with the 3-wave bin: 1.352 / 1.471 / 1.476 vs 1.345 ms,
     # profiles/r03x/ab.txt; not kept)
+    # longest bins strictly first (round 2/3 order; the 6-wave-first order is -1.3%)
+    "wordlong": [("consensus.hip", "static const int kOrder[BCE_NBINS] = {12, 10, 11, 9, 8, 7, 6, 5, 4, 3, 2, 1, 0};",
+                  "static const int kOrder[BCE_NBINS] = {12, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2, 1, 0};")],
+    # (also moving the 3-wave bin before the 4-wave bin: no further change)
+    # the 1537..2048 bin (4-wave workgroups) on the side stream, launched with the 6-wave bin
+    # first on st: 2 x 6 + 1 x 4 waves fill a CU's 16 wave slots (+8.5%: 1.443 vs 1.329 ms)
+    "wside4": [("consensus.hip", "static const int kOrder[BCE_NBINS] = {12, 10, 11, 9, 8, 7, 6, 5, 4, 3, 2, 1, 0};",
+                "static const int kOrder[BCE_NBINS] = {12, 10, 9, 11, 8, 7, 6, 5, 4, 3, 2, 1, 0};"),
+               ("consensus.hip", "hipStream_t sb = (b <= side_last) ? side : st;",
+                "hipStream_t sb = (b <= side_last || (b == 9 && !merge_np2)) ? side : st;")],
     # ---- exact-preserving ablations: a compare-exchange stage applied twice is a no-op on
     # the data, so these time one class of sort stages without changing the results
     "xin2": [("consensus_wide.hip", """        key[r] = x < y ? x : y;
