@@ -155,6 +155,9 @@ extern "C" int bce_debug_wprof(unsigned long long* out) {
                 "static const int kOrder[BCE_NBINS] = {12, 10, 9, 11, 8, 7, 6, 5, 4, 3, 2, 1, 0};"),
                ("consensus.hip", "hipStream_t sb = (b <= side_last) ? side : st;",
                 "hipStream_t sb = (b <= side_last || (b == 9 && !merge_np2)) ? side : st;")],
+    # (FAST runs inside one thread's R sorted positions averaged in phase 3 -- their sum from
+    # the registers, the average over the leader's sorted slot -- so the per-unique phase reads
+    # one slot: +6%, 1.41 vs 1.33 ms, parity green, profiles/r03aa/ab.txt; not kept)
     # ---- exact-preserving ablations: a compare-exchange stage applied twice is a no-op on
     # the data, so these time one class of sort stages without changing the results
     "xin2": [("consensus_wide.hip", """        key[r] = x < y ? x : y;
