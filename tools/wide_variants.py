@@ -158,6 +158,10 @@ extern "C" int bce_debug_wprof(unsigned long long* out) {
     # (FAST runs inside one thread's R sorted positions averaged in phase 3 -- their sum from
     # the registers, the average over the leader's sorted slot -- so the per-unique phase reads
     # one slot: +6%, 1.41 vs 1.33 ms, parity green, profiles/r03aa/ab.txt; not kept)
+    # (the 2049..3072 bin split at 2560 -- markets <= 2560 on 5-wave workgroups, three per CU
+    # -- measured 1.379 vs 1.329 ms, parity green, profiles/r03ac/ab.txt; not kept.  Neither
+    # were the non-power-of-two bins split out of EXACT's power-of-two launches again:
+    # 2.149 vs 2.024 ms, profiles/r03ab/ab.txt)
     # ---- exact-preserving ablations: a compare-exchange stage applied twice is a no-op on
     # the data, so these time one class of sort stages without changing the results
     "xin2": [("consensus_wide.hip", """        key[r] = x < y ? x : y;
