@@ -162,6 +162,11 @@ extern "C" int bce_debug_wprof(unsigned long long* out) {
     # -- measured 1.379 vs 1.329 ms, parity green, profiles/r03ac/ab.txt; not kept.  Neither
     # were the non-power-of-two bins split out of EXACT's power-of-two launches again:
     # 2.149 vs 2.024 ms, profiles/r03ab/ab.txt)
+    # (a FAST dedup-before-sort path -- LDS hash of sids with CAS inserts, a prefix count for
+    # the unique index, 64-bit fixed-point atomic sums, then only the u distinct keys sorted,
+    # on half the network when u <= P/2 -- was correct (wide/consensus parity green) but
+    # 2.27 vs 1.32 ms: contended LDS atomics on hot sources, ten barriers per market and
+    # 10-34 spilled VGPRs; profiles/r03ad/ab.txt, not kept)
     # ---- exact-preserving ablations: a compare-exchange stage applied twice is a no-op on
     # the data, so these time one class of sort stages without changing the results
     "xin2": [("consensus_wide.hip", """        key[r] = x < y ? x : y;
