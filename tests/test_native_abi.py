@@ -59,8 +59,12 @@ def test_plan_bins_host():
     assert N.NBINS == 13
     for b in range(N.NBINS):
         ms = order[bins[b]:bins[b + 1]]
-        assert np.all(np.diff(ms) > 0)  # ascending inside a bin
         ln = lens[ms]
+        if 4 <= b <= 11:  # wide bins: longest first, ties in market order (LPT)
+            assert np.all(np.diff(ln) <= 0)
+            assert np.all(np.diff(ms)[np.diff(ln) == 0] > 0)
+        else:
+            assert np.all(np.diff(ms) > 0)  # ascending inside a bin
         assert np.all((ln <= edges[b + 1]) & ((ln > edges[b]) if b else True))
     assert sorted(order.tolist()) == list(range(len(lens)))
     assert mx[0] == lens.max()
