@@ -126,7 +126,9 @@ int bce_validate_csr(const int64_t* offsets, int64_t n_markets, const double* pr
 
 /* Host-planned variant for ragged batches: the caller bins markets by length once
  * (bce_plan_bins on HOST offsets) and passes the device copy of the ordered market
- * list plus the bin boundaries.  bin_start has BCE_NBINS+1 entries (host array).
+ * list plus the bin boundaries.  bin_start has BCE_NBINS+1 entries (host array).  Inside
+ * a bin markets keep their index order, except the wide bins (65..4096 signals), which
+ * are ordered longest first (ties by index) so each launch ends on its short markets.
  * bce_consensus_planned runs the n <= 64 bins on a library-owned side stream (one per
  * device) forked from `stream` by an event and joined back into it before it returns, so
  * the caller sees ordinary stream order; concurrent callers are serialised over the fork. */
