@@ -167,6 +167,10 @@ extern "C" int bce_debug_wprof(unsigned long long* out) {
     # on half the network when u <= P/2 -- was correct (wide/consensus parity green) but
     # 2.27 vs 1.32 ms: contended LDS atomics on hot sources, ten barriers per market and
     # 10-34 spilled VGPRs; profiles/r03ad/ab.txt, not kept)
+    # FAST duplicate runs summed by the whole wave from 24 / 96 signals instead of 48
+    # (24: same, 96: +1%, profiles/r03af/ab.txt)
+    "wrun24": [("consensus_wide.hip", "constexpr int kWaveRun = 48;", "constexpr int kWaveRun = 24;")],
+    "wrun96": [("consensus_wide.hip", "constexpr int kWaveRun = 48;", "constexpr int kWaveRun = 96;")],
     # ---- exact-preserving ablations: a compare-exchange stage applied twice is a no-op on
     # the data, so these time one class of sort stages without changing the results
     "xin2": [("consensus_wide.hip", """        key[r] = x < y ? x : y;
