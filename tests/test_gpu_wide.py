@@ -171,3 +171,36 @@ def test_wide_direct_csr_unplanned():
     out = {k: getattr(res, k).cpu().numpy() for k in ("consensus", "confidence", "total_weight", "n_unique",
                                                       "err_idx", "usid", "weight", "nweight")}
     _compare_vec(out, exp, g["offsets"])
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("pattern", ["descending", "ascending", "sawtooth", "max_sid"])
+def test_wide_ordered_inputs(pattern, mode):
+    """Market inputs already ordered (or reversed, or a sawtooth with every other sid
+    repeated), and sids at the top of the key range, at every bin edge: the register
+    network's lane stages (DPP-fused compares, bank-masked min/max, permlane swap pairs, the
+    flip-31 reversal) and the uniform wave-crossing min/max see every compare go the same
+    way, and +inf padding ties real keys when sid = 2^(32 - IB) - 1."""
+    lens = np.array(EDGES * 2, np.int64)
+    off = np.zeros(len(lens) + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    n = int(off[-1])
+    S = 1 << 20  # the largest table a 4096-key bin packs into 32-bit keys
+    sid = np.zeros(n, np.int32)
+    for m, L in enumerate(lens):
+        i = np.arange(L)
+        if pattern == "descending":
+            v = S - 1 - 3 * i
+        elif pattern == "ascending":
+            v = 5 + 7 * i
+        elif pattern == "sawtooth":
+            v = (i // 2) * 11 + (i % 2) * 5 * (L - i)
+        else:  # the largest sids, with duplicates
+            v = S - 1 - (i % 97)
+        sid[off[m]:off[m + 1]] = np.clip(v, 0, S - 1)
+    rng = np.random.default_rng(7)
+    prob = rng.random(n)
+    rel = rng.uniform(0.1, 1.0, S)
+    conf = rng.random(S)
+    present = (rng.random(S) < 0.8).astype(np.uint8)
+    _check(dict(offsets=off, sid=sid, prob=prob, rel=rel, conf=conf, present=present), mode)
