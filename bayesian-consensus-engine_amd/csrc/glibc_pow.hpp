@@ -83,7 +83,7 @@ BCE_POW_FN double specialcase(double tmp, uint64_t sbits, uint64_t ki) {
 }
 
 // exp(x + xtail), e_pow.c exp_inline with sign_bias 0 (the square is never negative)
-BCE_POW_FN double exp_inline(double x, double xtail) {
+BCE_POW_FN double exp_inline(double x, double xtail, const unsigned long long* tab = kExpTab) {
   uint32_t abstop = top12(x) & 0x7ff;
   if (abstop - top12(0x1p-54) >= top12(512.0) - top12(0x1p-54)) {
     if (abstop - top12(0x1p-54) >= 0x80000000u) return 1.0 + x;
@@ -97,8 +97,8 @@ BCE_POW_FN double exp_inline(double x, double xtail) {
   r += xtail;
   const uint64_t idx = 2 * (ki & 127);
   const uint64_t top = ki << (52 - 7);
-  const double tail = asd(kExpTab[idx]);
-  const uint64_t sbits = kExpTab[idx + 1] + top;
+  const double tail = asd(tab[idx]);
+  const uint64_t sbits = tab[idx + 1] + top;
   const double r2 = r * r;
   const double tmp = __builtin_fma(r2 * r2, __builtin_fma(r, BCE_EXP_C5, BCE_EXP_C4),
                                    __builtin_fma(r2, __builtin_fma(r, BCE_EXP_C3, BCE_EXP_C2), tail + r));
@@ -159,7 +159,9 @@ BCE_POW_FN double pow2_full(double x) {
 // a constant pair (glibc_pow_tables.inc), so only the exp half runs.  CPython's float_pow
 // answers y == 0 (1.0) and NaN y (NaN) itself; the rest follows e_pow.c's special cases for
 // x = 2 (|y| < 2^-65: 1 + y; |y| >= 2^63: inf / 0; y = +-inf: inf / 0).
-BCE_POW_FN double pow_base2(double y) {
+// tab: kExpTab or a copy of it (a kernel may stage the 2 KB in LDS: one ds_read per lookup
+// instead of a per-lane gather from the constant table)
+BCE_POW_FN double pow_base2(double y, const unsigned long long* tab = kExpTab) {
   const uint64_t iy = asu(y);
   const uint32_t topy = top12(y) & 0x7ff;
   if (topy - 0x3be >= 0x43e - 0x3be) {
@@ -173,7 +175,7 @@ BCE_POW_FN double pow_base2(double y) {
   }
   const double ehi = y * BCE_POW_LOG2_HI;
   const double elo = __builtin_fma(y, BCE_POW_LOG2_LO, __builtin_fma(y, BCE_POW_LOG2_HI, -ehi));
-  return exp_inline(ehi, elo);
+  return exp_inline(ehi, elo, tab);
 }
 
 }  // namespace bce_pow
