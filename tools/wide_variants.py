@@ -171,6 +171,14 @@ extern "C" int bce_debug_wprof(unsigned long long* out) {
     # (24: same, 96: +1%, profiles/r03af/ab.txt)
     "wrun24": [("consensus_wide.hip", "constexpr int kWaveRun = 48;", "constexpr int kWaveRun = 24;")],
     "wrun96": [("consensus_wide.hip", "constexpr int kWaveRun = 48;", "constexpr int kWaveRun = 96;")],
+    # LDS-DMA helpers that save and restore M0 around the DMA (the compiler ignores an M0
+    # clobber: M0 is reserved); written in round 3, not yet run on a GPU (tools/gpu_r03aj.sh)
+    "wm0save": [("consensus_common.hpp",
+                 'asm volatile("s_mov_b32 m0, %0\\n\\ts_nop 0\\n\\tglobal_load_lds_dwordx4 %1, off" ::"s"(l), "v"(g) : "memory", "m0");',
+                 'uint32_t keep;\n  asm volatile("s_mov_b32 %0, m0\\n\\ts_mov_b32 m0, %1\\n\\ts_nop 0\\n\\tglobal_load_lds_dwordx4 %2, off\\n\\ts_mov_b32 m0, %0" : "=&s"(keep) : "s"(l), "v"(g) : "memory");'),
+                ("consensus_common.hpp",
+                 'asm volatile("s_mov_b32 m0, %0\\n\\ts_nop 0\\n\\tglobal_load_lds_dword %1, off" ::"s"(l), "v"(g) : "memory", "m0");',
+                 'uint32_t keep;\n  asm volatile("s_mov_b32 %0, m0\\n\\ts_mov_b32 m0, %1\\n\\ts_nop 0\\n\\tglobal_load_lds_dword %2, off\\n\\ts_mov_b32 m0, %0" : "=&s"(keep) : "s"(l), "v"(g) : "memory");')],
     # ---- exact-preserving ablations: a compare-exchange stage applied twice is a no-op on
     # the data, so these time one class of sort stages without changing the results
     "xin2": [("consensus_wide.hip", """        key[r] = x < y ? x : y;
