@@ -464,7 +464,9 @@ def reestimate(P: torch.Tensor, iters: int, w0: float = 0.5, w: Optional[torch.T
     agreement pass counts from those bits (bce_reestimate_consensus_votes /
     bce_reestimate_agreement_votes; A*ceil(M/64)*8 bytes of scratch).  ``mode="fast"``
     runs the consensus pass on the matrix cores (bce_reestimate_consensus_votes_mfma:
-    consensus within 4*A*2^-53, votes and agreement counts identical to exact; weights >= 0)."""
+    consensus within 4*A*2^-53, votes and agreement counts identical to exact).  Its
+    summation order needs every weight finite and >= 0; the library checks that on the
+    device and runs the exact kernel for an iteration whose weights break it."""
     L = N.require_gpu()
     A, M = P.shape
     dev = P.device

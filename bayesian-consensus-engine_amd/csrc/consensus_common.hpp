@@ -129,14 +129,23 @@ __device__ __forceinline__ void raise_fault(int* fault, int code) {
 
 // LDS-DMA issued from inline asm.  The compiler's wait-count pass treats every LDS
 // access after a *builtin* LDS-DMA as a possible alias and drains vmcnt(0) in front of
-// it; the kernels that use these order their images themselves.
+// it; the kernels that use these order their images themselves.  M0 is reserved to the
+// compiler (an "m0" clobber is ignored), so the helpers save it into an SGPR, point it at
+// the LDS destination for the DMA and restore it before returning: whatever M0 value the
+// compiler keeps live across the call survives.
 __device__ __forceinline__ void dma_b128(const void* g, const void* lds) {
   const uint32_t l = (uint32_t)(uintptr_t)lds;
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(l), "v"(g) : "memory", "m0");
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, off\n\t"
+               "s_mov_b32 m0, %0\n\ts_nop 0"
+               : "=&s"(keep) : "s"(l), "v"(g) : "memory");
 }
 __device__ __forceinline__ void dma_b32(const void* g, const void* lds) {
   const uint32_t l = (uint32_t)(uintptr_t)lds;
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off" ::"s"(l), "v"(g) : "memory", "m0");
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %2, off\n\t"
+               "s_mov_b32 m0, %0\n\ts_nop 0"
+               : "=&s"(keep) : "s"(l), "v"(g) : "memory");
 }
 
 // ---- host side -------------------------------------------------------------------------

@@ -151,7 +151,11 @@ constexpr int kVoteRows = 16;
 __global__ __launch_bounds__(256) void reestimate_consensus_votes_kernel(
     const double* __restrict__ P, int64_t A, int64_t M, int64_t ld, const double* __restrict__ w,
     double* __restrict__ cons, uint8_t* __restrict__ null_out, unsigned long long* __restrict__ vote_bits,
-    unsigned long long* __restrict__ cvote_words, unsigned long long* __restrict__ ok_words) {
+    unsigned long long* __restrict__ cvote_words, unsigned long long* __restrict__ ok_words,
+    const int32_t* __restrict__ only_if) {
+  // only_if (nullable): run only when *only_if != 0 -- the MFMA entry point launches this
+  // kernel behind its own and lets the weight check pick one of the two on the device
+  if (only_if && *only_if == 0) return;
   const int lane = lane_id();
   const int64_t m = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int64_t k = m >> 6;
@@ -239,8 +243,14 @@ __global__ __launch_bounds__(256) void reestimate_agreement_votes_kernel(
 // 0.5), regrouped per agent into the vote_bits word layout of the exact kernel.
 // The sums are in MFMA order, not agent order (within 4*A*2^-53 of the exact consensus);
 // markets whose consensus lies within 8*A*2^-53 of 0.5 -- where the vote could differ --
-// (or whose column holds a cell outside [0, 1] or NaN) are listed for reestimate_fixup_kernel, which redoes them in exact agent order, so the
-// votes and therefore the agreement counts are identical to the exact path.
+// (or whose column holds a finite cell outside [0, 1], where that bound does not hold) are
+// listed for reestimate_fixup_kernel, which redoes them in exact agent order, so the votes
+// and therefore the agreement counts are identical to the exact path.  A column holding a
+// NaN cell sums to NaN in every order (NaN * w is NaN for any w), so it needs no redo.
+// Precondition of the error bound and the null test: every weight finite and >= 0.
+// reestimate_total_kernel checks it on the device; if any weight breaks it, the MFMA and
+// fixup kernels exit at once and the exact kernel (launched behind them, gated on the same
+// word) computes the iteration instead -- same results, exact-mode speed.
 typedef double mfma_d4 __attribute__((ext_vector_type(4)));
 constexpr int kMfmaSteps = 4;  // 4-agent MFMA steps per loop iteration (16 agents)
 
@@ -248,8 +258,17 @@ __global__ __launch_bounds__(256) void reestimate_total_kernel(const double* __r
                                                                double* __restrict__ total_fast,
                                                                int32_t* __restrict__ nflag) {
   __shared__ double part[256];
+  __shared__ int badS;
+  if (threadIdx.x == 0) badS = 0;
+  __syncthreads();
   double s = 0.0;
-  for (int64_t a = threadIdx.x; a < A; a += 256) s += w[a];  // fixed order: deterministic
+  bool bad = false;
+  for (int64_t a = threadIdx.x; a < A; a += 256) {
+    const double x = w[a];
+    s += x;  // fixed order: deterministic
+    bad = bad || !(x >= 0.0 && x <= __builtin_huge_val());  // negative, NaN or +inf
+  }
+  if (bad) badS = 1;
   part[threadIdx.x] = s;
   __syncthreads();
   for (int h = 128; h > 0; h >>= 1) {
@@ -258,7 +277,8 @@ __global__ __launch_bounds__(256) void reestimate_total_kernel(const double* __r
   }
   if (threadIdx.x == 0) {
     *total_fast = part[0];
-    *nflag = 0;
+    nflag[0] = 0;     // flagged-market count
+    nflag[1] = badS;  // 1: a weight breaks the precondition -> the exact kernel runs instead
   }
 }
 
@@ -267,6 +287,7 @@ __global__ __launch_bounds__(256) void reestimate_votes_mfma_kernel(
     const double* __restrict__ total_fast, double* __restrict__ cons, uint8_t* __restrict__ null_out,
     unsigned long long* __restrict__ vote_bits, unsigned long long* __restrict__ cvote_words,
     unsigned long long* __restrict__ ok_words, int32_t* __restrict__ nflag, int32_t* __restrict__ flags) {
+  if (nflag[1]) return;  // weights outside [0, inf): the gated exact kernel does this iteration
   const int lane = lane_id();
   const int64_t k = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;  // vote word = 64 markets
   const int64_t m0 = k << 6;
@@ -280,6 +301,7 @@ __global__ __launch_bounds__(256) void reestimate_votes_mfma_kernel(
   for (int j = 0; j < 4; ++j) inm[j] = m0 + 16 * j + n < M;
   unsigned long long* vb = vote_bits + k * A;
   bool odd[4] = {false, false, false, false};  // a cell outside [0, 1] (or NaN) in this lane's column
+  bool hnan[4] = {false, false, false, false};  // a NaN cell in this lane's column
   for (int64_t a = 0; a < A; a += 4 * kMfmaSteps) {
     double v[kMfmaSteps][4], wa[kMfmaSteps];
 #pragma unroll
@@ -297,6 +319,7 @@ __global__ __launch_bounds__(256) void reestimate_votes_mfma_kernel(
       for (int j = 0; j < 4; ++j) {
         acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(wa[q], v[q][j], acc[j], 0, 0, 0);
         odd[j] = odd[j] || !(v[q][j] >= 0.0 && v[q][j] <= 1.0);
+        hnan[j] = hnan[j] || (v[q][j] != v[q][j]);
         bal[j] = ballot(a + 4 * q + ka < A && inm[j] && v[q][j] >= 0.5);  // market.py:298-299
       }
       // agent a + 4q + lane's vote word (lanes 0..3): its 16-bit slice of every ballot
@@ -315,17 +338,21 @@ __global__ __launch_bounds__(256) void reestimate_votes_mfma_kernel(
   const bool isnull = (total == 0.0);  // w >= 0: zero in every order iff every weight is zero
   const double c = isnull ? 0.0 : ws / total;
   // |fast - exact| <= ~4*A*2^-53 for cells in [0, 1] (both sums of non-negative terms within
-  // A*2^-53 relative of the true one, c <= 1); a column holding anything else (or NaN) is
-  // always redone
-  unsigned long long oddm = 0;
+  // A*2^-53 relative of the true one, c <= 1); a column holding another finite value is
+  // always redone, a column holding a NaN never (NaN in every order)
+  unsigned long long oddm = 0, nanm = 0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     unsigned long long b = ballot(odd[j]);
     b |= (b >> 16) | (b >> 32) | (b >> 48);
     oddm |= (b & 0xFFFFull) << (16 * j);
+    unsigned long long q = ballot(hnan[j]);
+    q |= (q >> 16) | (q >> 32) | (q >> 48);
+    nanm |= (q & 0xFFFFull) << (16 * j);
   }
   const double bound = 8.0 * (double)(A + 2) * 0x1p-53;
-  const bool near = in && !isnull && (fabs(c - 0.5) <= bound || ((oddm >> lane) & 1ull));
+  const bool colnan = (nanm >> lane) & 1ull;
+  const bool near = in && !isnull && !colnan && (fabs(c - 0.5) <= bound || ((oddm >> lane) & 1ull));
   if (in) {
     cons[m] = c;
     null_out[m] = isnull ? 1 : 0;
@@ -340,28 +367,44 @@ __global__ __launch_bounds__(256) void reestimate_votes_mfma_kernel(
 }
 
 // Exact redo of the flagged markets (agent-order sums, as reestimate_consensus_votes_kernel):
-// one wave per flagged market, lanes load 64 agents at a time, lane 0 adds in agent order.
-__global__ __launch_bounds__(64) void reestimate_fixup_kernel(const double* __restrict__ P, int64_t A, int64_t ld,
-                                                              const double* __restrict__ w,
-                                                              const int32_t* __restrict__ nflag,
-                                                              const int32_t* __restrict__ flags,
-                                                              double* __restrict__ cons,
-                                                              unsigned long long* __restrict__ cvote_words) {
-  const int lane = lane_id();
-  for (int f = blockIdx.x; f < *nflag; f += gridDim.x) {
-    const int64_t m = flags[f];
+// lane per flagged market, 64 flags per wave (grid-stride over the flag list, whose length
+// only the device knows), agents streamed kVoteRows rows at a time.  Each lane runs its own
+// two ordered chains (core.py:116,120,136), so 64 markets advance per instruction; the flag
+// list is filled a wave's ballot at a time in column order, so neighbouring lanes mostly
+// read neighbouring columns.
+__global__ __launch_bounds__(256) void reestimate_fixup_kernel(const double* __restrict__ P, int64_t A, int64_t ld,
+                                                               const double* __restrict__ w,
+                                                               const int32_t* __restrict__ nflag,
+                                                               const int32_t* __restrict__ flags,
+                                                               double* __restrict__ cons,
+                                                               unsigned long long* __restrict__ cvote_words) {
+  const int nf = nflag[0];
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t f0 = wave * 64; f0 < nf; f0 += nwaves * 64) {
+    const int64_t f = f0 + lane_id();
+    const bool in = f < nf;
+    const int64_t m = in ? flags[f] : 0;
+    const double* col = P + m;
     double ws = 0.0, total = 0.0;
-    for (int64_t a0 = 0; a0 < A; a0 += 64) {
-      const int64_t a = a0 + lane;
-      const double v = a < A ? P[a * ld + m] : 0.0, wq = a < A ? w[a] : 0.0;
-      const int cnt = (A - a0 < 64) ? (int)(A - a0) : 64;
-      for (int q = 0; q < cnt; ++q) {
-        const double vq = __shfl(v, q), wqq = __shfl(wq, q);
-        ws += (0.0 + vq) * wqq;  // core.py:116,136
-        total += wqq;
+    int64_t a = 0;
+    for (; a + kVoteRows <= A; a += kVoteRows) {
+      double v[kVoteRows];
+#pragma unroll
+      for (int q = 0; q < kVoteRows; ++q) v[q] = in ? col[(a + q) * ld] : 0.0;
+#pragma unroll
+      for (int q = 0; q < kVoteRows; ++q) {
+        const double wq = w[a + q];
+        ws += (0.0 + v[q]) * wq;
+        total += wq;
       }
     }
-    if (lane == 0) {
+    for (; a < A; ++a) {
+      const double wq = w[a];
+      ws += (0.0 + (in ? col[a * ld] : 0.0)) * wq;
+      total += wq;
+    }
+    if (in) {
       const double c = ws / total;  // total > 0: flagged markets are not null
       cons[m] = c;
       const unsigned long long bit = 1ull << (m & 63);
@@ -450,7 +493,7 @@ extern "C" int bce_reestimate_consensus_votes(const double* P, int64_t A, int64_
   hipLaunchKernelGGL(reestimate_consensus_votes_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0,
                      as_stream(stream), P, A, M, ld, w, consensus, null_out,
                      reinterpret_cast<unsigned long long*>(vote_bits), reinterpret_cast<unsigned long long*>(cvote_words),
-                     reinterpret_cast<unsigned long long*>(ok_words));
+                     reinterpret_cast<unsigned long long*>(ok_words), (const int32_t*)nullptr);
   return check_launch("reestimate_consensus_votes_kernel");
 }
 
@@ -501,9 +544,16 @@ extern "C" int bce_reestimate_consensus_votes_mfma(const double* P, int64_t A, i
                      nflag, flags);
   rc = check_launch("reestimate_votes_mfma_kernel");
   if (rc) return rc;
-  hipLaunchKernelGGL(reestimate_fixup_kernel, dim3(64), dim3(64), 0, st, P, A, ld, w, nflag, flags, consensus,
-                     reinterpret_cast<unsigned long long*>(cvote_words));
-  return check_launch("reestimate_fixup_kernel");
+  hipLaunchKernelGGL(reestimate_fixup_kernel, dim3((unsigned)cu_count() * 4), dim3(256), 0, st, P, A, ld, w, nflag,
+                     flags, consensus, reinterpret_cast<unsigned long long*>(cvote_words));
+  rc = check_launch("reestimate_fixup_kernel");
+  if (rc) return rc;
+  // precondition fallback (weights negative / NaN / inf): exits at once unless nflag[1] != 0
+  hipLaunchKernelGGL(reestimate_consensus_votes_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, P, A, M,
+                     ld, w, consensus, null_out, reinterpret_cast<unsigned long long*>(vote_bits),
+                     reinterpret_cast<unsigned long long*>(cvote_words),
+                     reinterpret_cast<unsigned long long*>(ok_words), (const int32_t*)(nflag + 1));
+  return check_launch("reestimate_consensus_votes_kernel (fallback)");
 }
 
 extern "C" int64_t bce_reestimate_mfma_scratch_bytes(int64_t M) { return 16 + 4 * (M > 0 ? M : 1); }

@@ -239,7 +239,17 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     const int64_t endl = off + n;
     const int64_t E = ((int64_t)__builtin_amdgcn_readlane((int)(endl >> 32), last_lane) << 32) |
                       (uint32_t)__builtin_amdgcn_readlane((int)endl, last_lane);
-    const int cnt_tile = (int)(E - B);  // <= 64 * 32
+    const int cnt_tile = (int)(E - B);  // <= 64 * 32 unless a market inside [B, E) was too long
+    if (STAGED && (E - B > 64 * kTbLpmMax || E < B)) {
+      // a market longer than kTbLpmMax (already faulted and zeroed above) still lies inside
+      // [B, E): staging the range would run past this wave's buffer, so the tile is skipped
+      // (every market gets the empty marker; the fault word reports the call as failed)
+      raise_fault(fault, kFaultTooLong);
+      if (has) {
+        a.winner[m] = 0.0; a.label[m] = -1; a.n_groups[m] = -1; a.variance[m] = 0.0;
+      }
+      continue;
+    }
     const int lrow = (int)(off - B);    // this lane's row in the staged buffer
     // every lane reads inside its own row (positions past n re-read the last agent); a lane
     // with an empty market reads the tile's first agent (masked later)
@@ -274,6 +284,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
           if (e + 1 < cnt_tile) dst[B + e + 1] = buf[tb_pad(e + 1)];
         }
       }
+      wave_sync_lds();  // the buffer's next writers (this wave) come after these reads
     };
     auto flush_i32 = [&](int32_t* dst) {
       wave_sync_lds();
@@ -286,6 +297,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
           for (int q = 0; q < 4 && e + q < cnt_tile; ++q) dst[B + e + q] = ibuf[tb_pad(e + q)];
         }
       }
+      wave_sync_lds();  // (as flush: the int32 reads are fenced before the next double writes)
     };
     // agent t of this lane's market
     auto at = [&](const double* src, int t) -> double {

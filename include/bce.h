@@ -280,9 +280,13 @@ int bce_reestimate_agreement_votes(const uint64_t* vote_bits, int64_t A, int64_t
 /* BCE_MODE_FAST pass 1 of the single-read iteration on the matrix cores: w^T P with
  * v_mfma_f64_16x16x4_f64 (the north star's "MFMA contraction"), same outputs as
  * bce_reestimate_consensus_votes.  consensus within 4*A*2^-53 of the agent-order value;
- * markets within 8*A*2^-53 of 0.5 (or with a cell outside [0, 1]) are redone in agent order, so vote_bits / cvote_words /
- * ok_words -- and the agreement counts -- are identical to the exact pass.  scratch: device
- * buffer of bce_reestimate_mfma_scratch_bytes(M) bytes (8-byte aligned). */
+ * markets within 8*A*2^-53 of 0.5 (or with a finite cell outside [0, 1]) are redone in agent
+ * order, so vote_bits / cvote_words / ok_words -- and the agreement counts -- are identical
+ * to the exact pass (a column with a NaN cell is NaN in every order and is not redone).
+ * PRECONDITION of the MFMA order: every w[a] finite and >= 0.  It is checked on the device;
+ * when any weight breaks it, this call computes the iteration with the exact kernel instead
+ * (results identical to bce_reestimate_consensus_votes, at exact-mode speed).  scratch:
+ * device buffer of bce_reestimate_mfma_scratch_bytes(M) bytes (8-byte aligned). */
 int bce_reestimate_consensus_votes_mfma(const double* P, int64_t A, int64_t M, int64_t ld, const double* w,
                                         double* consensus, uint8_t* null_out, uint64_t* vote_bits,
                                         uint64_t* cvote_words, uint64_t* ok_words, void* scratch,

@@ -628,3 +628,104 @@ def test_reestimate_mfma_fast_mode_matches_exact_votes(A, M):
         near = fin & (np.abs(ce - 0.5) <= 4 * (A + 2) * 2.0 ** -53)
         assert np.array_equal(cf[near], ce[near])  # the redone markets are exact
         assert np.array_equal(np.isnan(cf), np.isnan(ce))  # NaN columns redone too
+
+
+def _votes_both_modes(P, w):
+    """(exact, mfma) outputs of one single-read iteration on the same P and weights."""
+    import torch
+    from bayesian_engine import _native as N
+    A, M = P.shape
+    Pt = P if isinstance(P, torch.Tensor) else torch.from_numpy(P).cuda()
+    wt = w if isinstance(w, torch.Tensor) else torch.from_numpy(w).cuda()
+    L = N.lib()
+    st = N.stream(Pt.device)
+    K = (M + 63) // 64
+    nb = int(L.bce_reestimate_mfma_scratch_bytes(M))
+    scratch = torch.empty((nb + 7) // 8, dtype=torch.int64, device="cuda")
+    out = []
+    for fn in ("bce_reestimate_consensus_votes", "bce_reestimate_consensus_votes_mfma"):
+        c = torch.empty(M, dtype=torch.float64, device="cuda")
+        nu = torch.empty(M, dtype=torch.uint8, device="cuda")
+        votes = torch.empty((K, A), dtype=torch.int64, device="cuda")
+        words = torch.empty((2, K), dtype=torch.int64, device="cuda")
+        g = torch.zeros(A + 1, dtype=torch.int64, device="cuda")
+        extra = (N.ptr(scratch), scratch.numel() * 8) if fn.endswith("mfma") else ()
+        N.check(getattr(L, fn)(N.ptr(Pt), A, M, M, N.ptr(wt), N.ptr(c), N.ptr(nu), N.ptr(votes), N.ptr(words[0]),
+                               N.ptr(words[1]), *extra, st), fn)
+        N.check(L.bce_reestimate_agreement_votes(N.ptr(votes), A, M, N.ptr(words[0]), N.ptr(words[1]),
+                                                 N.ptr(g[:A]), N.ptr(g[A:]), st))
+        torch.cuda.synchronize()
+        out.append((c.cpu().numpy(), nu.cpu().numpy(), votes.cpu().numpy(), words.cpu().numpy(), g.cpu().numpy()))
+    return out
+
+
+@pytest.mark.parametrize("wkind", ["negative", "nan", "inf", "neg_zero"])
+def test_reestimate_mfma_weights_outside_precondition_fall_back_to_exact(wkind):
+    """The MFMA order's error bound and null test assume finite w >= 0 (stats.hip).  Weights
+    that break it make bce_reestimate_consensus_votes_mfma run the exact kernel (device-side
+    check): every output identical to the exact pass, bit for bit.  -0.0 is >= 0 and stays
+    on the MFMA path (consensus within the bound, votes identical)."""
+    rng = np.random.default_rng(7)
+    A, M = 300, 5000
+    P = rng.beta(2, 2, size=(A, M))
+    w = rng.random(A)
+    if wkind == "negative":
+        w[rng.random(A) < 0.3] *= -1.0  # mixed signs: totals can cancel
+    elif wkind == "nan":
+        w[17] = np.nan
+    elif wkind == "inf":
+        w[3] = np.inf
+    else:
+        w[::2] = -0.0
+    (ce, ne, ve, we, ge), (cf, nf, vf, wf, gf) = _votes_both_modes(P, w)
+    assert np.array_equal(ne, nf) and np.array_equal(ve, vf) and np.array_equal(we, wf)
+    assert np.array_equal(ge, gf)
+    if wkind == "neg_zero":
+        assert np.abs(cf - ce).max() <= 4 * (A + 2) * 2.0 ** -53
+    else:
+        assert np.array_equal(cf, ce, equal_nan=True)
+
+
+def test_reestimate_mfma_nan_cells_match_exact_without_redo_cliff():
+    """10% NaN cells: every column holds a NaN, so every consensus is NaN in any order -- the
+    MFMA pass must match exact (votes, words, counts) without redoing the columns one by one
+    (it stays within 2x of the exact pass's time)."""
+    import time
+    import torch
+    rng = np.random.default_rng(11)
+    A, M = 2048, 65536
+    P = rng.beta(2, 2, size=(A, M))
+    P[rng.random((A, M)) < 0.1] = np.nan
+    Pt = torch.from_numpy(P).cuda()
+    w = torch.from_numpy(rng.random(A)).cuda()
+    (ce, ne, ve, we, ge), (cf, nf, vf, wf, gf) = _votes_both_modes(Pt, w)
+    assert np.array_equal(ne, nf) and np.array_equal(ve, vf) and np.array_equal(we, wf)
+    assert np.array_equal(ge, gf)
+    assert np.array_equal(np.isnan(cf), np.isnan(ce)) and np.isnan(ce).all()
+    from bayesian_engine import batch
+    times = {}
+    for mode in ("exact", "fast"):
+        batch.reestimate(Pt, 1, mode=mode)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        batch.reestimate(Pt, 3, mode=mode)
+        torch.cuda.synchronize()
+        times[mode] = time.perf_counter() - t0
+    assert times["fast"] <= 2.0 * times["exact"], times
+
+
+def test_reestimate_mfma_out_of_range_cells_redone_exactly():
+    """Finite cells outside [0, 1] void the MFMA error bound: those columns are redone in agent
+    order by the lane-per-market fixup kernel -- consensus bit-exact there, votes identical."""
+    rng = np.random.default_rng(12)
+    A, M = 1000, 20000
+    P = rng.beta(2, 2, size=(A, M))
+    odd = rng.random(M) < 0.3
+    P[rng.integers(0, A, odd.sum()), np.nonzero(odd)[0]] = rng.uniform(-5, 5, odd.sum())
+    w = rng.random(A)
+    (ce, ne, ve, we, ge), (cf, nf, vf, wf, gf) = _votes_both_modes(P, w)
+    assert np.array_equal(ne, nf) and np.array_equal(ve, vf) and np.array_equal(we, wf)
+    assert np.array_equal(ge, gf)
+    hit = odd & ((P < 0) | (P > 1)).any(axis=0)
+    assert hit.sum() > 1000
+    assert np.array_equal(cf[hit], ce[hit])

@@ -35,16 +35,23 @@ def _rows(d, pattern):
 
 
 def stats(d, kern):
-    for r in _rows(d, "*kernel_stats.csv"):
-        if kern in r["Name"]:
-            return float(r["AverageNs"]) / 1e6, int(r["Calls"]), r["Name"]
-    raise SystemExit(f"kernel {kern} not in stats")
+    """(avg ms, calls, full name) of the kernel matching `kern` with the most total time, and
+    every matching kernel's row (a substring can match several instantiations)."""
+    rows = [r for r in _rows(d, "*kernel_stats.csv") if kern in r["Name"]]
+    if not rows:
+        raise SystemExit(f"kernel {kern} not in stats")
+    rows.sort(key=lambda r: -float(r["TotalDurationNs"]))
+    every = [{"kernel": r["Name"], "avg_ms": float(r["AverageNs"]) / 1e6, "min_ms": float(r["MinNs"]) / 1e6,
+              "max_ms": float(r["MaxNs"]) / 1e6, "calls": int(r["Calls"])} for r in rows]
+    r = rows[0]
+    return float(r["AverageNs"]) / 1e6, int(r["Calls"]), r["Name"], every
 
 
-def steady(d, kern, last):
-    """Average duration (ms) of the last `last` dispatches of the kernel in the trace: the
-    timed steps, without the clock ramp and warmup dispatches the --stats average includes."""
-    rows = [r for r in _rows(d, "*kernel_trace.csv") if kern in r["Kernel_Name"]]
+def steady(d, name, last):
+    """Average duration (ms) of the last `last` dispatches of the kernel named exactly `name`
+    in the trace: the timed steps, without the clock ramp and warmup dispatches the --stats
+    average includes."""
+    rows = [r for r in _rows(d, "*kernel_trace.csv") if r["Kernel_Name"] == name]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows[-last:]]
     return sum(durs) / len(durs) if durs else None
@@ -63,10 +70,12 @@ def counter(d, kern, name, per_step=None):
 
 def main():
     if sys.argv[1] == "stats":
-        ms, calls, name = stats(sys.argv[2], sys.argv[3])
+        ms, calls, name, every = stats(sys.argv[2], sys.argv[3])
         out = {"kernel": name, "avg_ms": ms, "calls": calls}
-        if len(sys.argv) > 4:  # the timed steps alone
-            out[f"avg_ms_last_{sys.argv[4]}"] = steady(sys.argv[2], sys.argv[3], int(sys.argv[4]))
+        if len(sys.argv) > 4:  # the timed steps alone (of that same kernel)
+            out[f"avg_ms_last_{sys.argv[4]}"] = steady(sys.argv[2], name, int(sys.argv[4]))
+        if len(every) > 1:
+            out["matching_kernels"] = every
         print(json.dumps(out))
         return
     fdir, wdir, kern, out = sys.argv[2:6]
