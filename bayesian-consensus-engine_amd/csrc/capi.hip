@@ -147,6 +147,7 @@ static const char* fault_text(int code) {
     case kFaultSid: return "consensus: a sid is >= n_sources (its row read was clamped)";
     case kFaultTooLong: return "consensus: a market is longer than the launch's max_len (left unprocessed)";
     case kFaultSpinChain: return "consensus_wide_kernel: exact-mode chain hand-off timed out";
+    case 6: return "tiebreak round(): rounded value too large to represent";
     default: return "unknown device fault";
   }
 }

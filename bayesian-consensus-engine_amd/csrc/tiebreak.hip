@@ -13,6 +13,7 @@
 #include "bce_internal.hpp"
 #include "consensus_common.hpp"
 #include "glibc_pow.hpp"
+#include "py_round_big.hpp"
 
 #pragma clang fp contract(off)
 
@@ -37,17 +38,32 @@ struct TbArgs {
   int32_t* g_of;   // nullable: per agent, the ordinal of its group (dict insertion order)
   double rscale;   // 10^ndigits (ndigits >= 0) or 10^-ndigits (ndigits < 0)
   double rthresh;  // see py_round_nd
-  int rmode;       // 0: py_round_nd, 1: py_round_neg, 2: identity (nd > 323), 3: signed zero (nd < -308)
+  int rmode;       // 0: py_round_nd, 1: py_round_neg, 2: identity (nd > 323), 3: signed zero (nd < -308),
+                   // 4: big-integer path 23 <= nd <= 323, 5: big-integer path -308 <= nd <= -16
+  int rnd;         // ndigits (modes 4, 5)
+  int* fault;      // device fault word: kFaultRoundOverflow (CPython's OverflowError)
 };
 
-// round(prediction, precision) of tiebreak.py:54 for every precision CPython accepts that
-// this build restates exactly (see tb_round_mode on the host)
+constexpr int kFaultRoundOverflow = 6;  // round(x, nd) too large to represent (mode 5)
+
+// round(prediction, precision) of tiebreak.py:54 for every precision CPython accepts (see
+// tb_round_mode on the host).  EXOTIC kernels (modes 4, 5: 10^|nd| not an exact double) run
+// the exact big-integer restatement of py_round_big.hpp; the others never contain it.
+template <bool EXOTIC>
 __device__ __forceinline__ double tb_round(double x, const TbArgs& a) {
-  switch (a.rmode) {
-    case 0: return py_round_nd(x, a.rscale, a.rthresh);
-    case 1: return py_round_neg(x, a.rscale);
-    case 2: return x;
-    default: return (x != x || fabs(x) == __builtin_inf()) ? x : copysign(0.0, x);
+  if constexpr (EXOTIC) {
+    if (a.rmode == 4) return bce_round::round_pos(x, a.rnd);
+    bool ovf = false;
+    const double r = bce_round::round_neg(x, -a.rnd, &ovf);
+    if (ovf && a.fault) atomicCAS(a.fault, 0, kFaultRoundOverflow);
+    return r;
+  } else {
+    switch (a.rmode) {
+      case 0: return py_round_nd(x, a.rscale, a.rthresh);
+      case 1: return py_round_neg(x, a.rscale);
+      case 2: return x;
+      default: return (x != x || fabs(x) == __builtin_inf()) ? x : copysign(0.0, x);
+    }
   }
 }
 
@@ -70,6 +86,7 @@ __device__ __forceinline__ double rl_f64(double v, int l) {
   return *reinterpret_cast<double*>(&y);
 }
 
+template <bool EXOTIC>
 __global__ __launch_bounds__(256) void tiebreak_wave_kernel(TbArgs a, const int32_t* list,
                                                             int64_t n_list) {
   const int lane = lane_id();
@@ -106,7 +123,7 @@ __global__ __launch_bounds__(256) void tiebreak_wave_kernel(TbArgs a, const int3
       }
       continue;
     }
-    const double key = tb_round(p, a);
+    const double key = tb_round<EXOTIC>(p, a);
     // leader = first index with an equal key (dict insertion order)
     int leader = lane;
     for (int j = 0; j < n; ++j) {
@@ -205,7 +222,7 @@ constexpr int kTbStage = 64 * kTbLpmMax + 64;  // doubles per wave buffer: a til
 
 __device__ __forceinline__ int tb_pad(int i) { return i + (i >> 5); }
 
-template <bool STAGED>
+template <bool STAGED, bool EXOTIC>
 __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_eu(2, 2))) void tiebreak_lpm_kernel(TbArgs a, const int32_t* list,
                                                                          int64_t n_list, int* fault) {
   // one buffer per wave (16.9 KB): two workgroups of four waves per CU
@@ -329,7 +346,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     const double praw0 = at(a.pred, 0);  // a single agent keeps its raw prediction (tiebreak.py:89-96)
     {
 #pragma unroll
-      for (int t = 0; t < kTbLpmMax; ++t) kp[t] = tb_round(at(a.pred, min(t, last)), a);
+      for (int t = 0; t < kTbLpmMax; ++t) kp[t] = tb_round<EXOTIC>(at(a.pred, min(t, last)), a);
       int go[kTbLpmMax];
 #pragma unroll
       for (int t = 0; t < kTbLpmMax; ++t) {
@@ -502,7 +519,7 @@ constexpr int kTbThreads = 256;
 constexpr int kTbMax = 4096;
 constexpr unsigned long long kNanKey = 0xFFFFFFFFFFFFF000ull;
 
-template <bool IN_LDS>
+template <bool IN_LDS, bool EXOTIC>
 __global__ __launch_bounds__(kTbThreads) void tiebreak_block_kernel(TbArgs a, const int32_t* list,
                                                                     int64_t n_list, void* scratch,
                                                                     int64_t stride) {
@@ -532,7 +549,7 @@ __global__ __launch_bounds__(kTbThreads) void tiebreak_block_kernel(TbArgs a, co
     for (int i = tid; i < P; i += kTbThreads) {
       unsigned long long kk = ~0ull;
       if (i < n) {
-        double k = tb_round(a.pred[off + i], a);
+        double k = tb_round<EXOTIC>(a.pred[off + i], a);
         if (k == 0.0) k = 0.0;  // -0.0 and 0.0 share one dict slot
         unsigned long long b = (unsigned long long)__double_as_longlong(k);
         kk = (b >> 63) ? ~b : (b | 0x8000000000000000ull);  // total order on doubles
@@ -606,7 +623,7 @@ __global__ __launch_bounds__(kTbThreads) void tiebreak_block_kernel(TbArgs a, co
         if (sk[t] == kNanKey) break;
       }
       const double dens = tot / (double)cnt;
-      const double key = tb_round(a.pred[off + i0], a);
+      const double key = tb_round<EXOTIC>(a.pred[off + i0], a);
       const int64_t g = off + sRank[i0];
       if (a.g_key) a.g_key[g] = key;
       if (a.g_count) a.g_count[g] = cnt;
@@ -695,7 +712,8 @@ static double round_thresh(int nd) {
 }
 // CPython float.__round__(x, nd): nd > 323 returns x, nd < -308 returns 0.0 * x
 // (NDIGITS_MAX / NDIGITS_MIN of floatobject.c); in between the correctly rounded decimal.
-// Restated exactly here for -15 <= nd <= 22 (10^|nd| exact, remainders exact).
+// Restated with doubles for -15 <= nd <= 22 (10^|nd| exact, remainders exact) and with
+// exact big integers (py_round_big.hpp, EXOTIC kernels) for the rest.
 static int tb_round_mode(int nd, double* scale, double* thresh) {
   *scale = 1.0;
   *thresh = 0.0;
@@ -710,7 +728,34 @@ static int tb_round_mode(int nd, double* scale, double* thresh) {
     *scale = pow10_exact(-nd);
     return 1;
   }
-  return -1;
+  return nd > 0 ? 4 : 5;
+}
+
+template <bool EXOTIC>
+static int launch_tb_short(const TbArgs& a, const int32_t* market_list, int64_t nl, int32_t max_len, void* stream) {
+  if (max_len <= kTbLpmMax) {  // lane per market: 64 markets per wave, kTbLpmWaves per workgroup
+    const int64_t tiles = (nl + 63) / 64;
+    int64_t blocks = (tiles + kTbLpmWaves - 1) / kTbLpmWaves;
+    // contiguous markets stage each wave's agent range in LDS; a market list gathers rows
+    const void* fn = market_list ? reinterpret_cast<const void*>(&tiebreak_lpm_kernel<false, EXOTIC>)
+                                 : reinterpret_cast<const void*>(&tiebreak_lpm_kernel<true, EXOTIC>);
+    const int per_cu = blocks_per_cu(fn, 64 * kTbLpmWaves, 0, 1, "tiebreak_lpm_kernel");
+    const int64_t cap = (int64_t)cu_count() * per_cu;
+    if (blocks > cap) blocks = cap;
+    if (market_list)
+      hipLaunchKernelGGL((tiebreak_lpm_kernel<false, EXOTIC>), dim3((int)blocks), dim3(64 * kTbLpmWaves), 0,
+                         as_stream(stream), a, market_list, nl, fault_word());
+    else
+      hipLaunchKernelGGL((tiebreak_lpm_kernel<true, EXOTIC>), dim3((int)blocks), dim3(64 * kTbLpmWaves), 0,
+                         as_stream(stream), a, market_list, nl, fault_word());
+    return check_launch("tiebreak_lpm_kernel");
+  }
+  int64_t blocks = (nl + 3) / 4;
+  const int64_t cap = (int64_t)cu_count() * 16;
+  if (blocks > cap) blocks = cap;
+  hipLaunchKernelGGL(tiebreak_wave_kernel<EXOTIC>, dim3((int)blocks), dim3(256), 0, as_stream(stream), a,
+                     market_list, nl);
+  return check_launch("tiebreak_wave_kernel");
 }
 
 extern "C" int bce_tiebreak_csr(const int64_t* offsets, int64_t n_markets, const int32_t* market_list,
@@ -728,65 +773,20 @@ extern "C" int bce_tiebreak_csr(const int64_t* offsets, int64_t n_markets, const
               "tiebreak: max_len must be in 1..64 (longer markets: bce_tiebreak_csr_long)");
   double rs = 1.0, rt = 0.0;
   const int rmode = tb_round_mode(ndigits, &rs, &rt);
-  if (rmode < 0) {
-    set_error("tiebreak: precision %d is outside what this build restates exactly "
-              "(-15..22, below -308, above 323)", ndigits);
-    return BCE_EUNSUPPORTED;
-  }
   TbArgs a{offsets, n_markets, pred, conf, weight, rel, winner, label, n_groups, variance,
-           g_key, g_count, g_density, g_avgconf, g_maxrel, g_of, rs, rt, rmode};
-  if (max_len <= kTbLpmMax) {  // lane per market: 64 markets per wave, kTbLpmWaves per workgroup
-    const int64_t tiles = (nl + 63) / 64;
-    int64_t blocks = (tiles + kTbLpmWaves - 1) / kTbLpmWaves;
-    // contiguous markets stage each wave's agent range in LDS; a market list gathers rows
-    const void* fn = market_list ? reinterpret_cast<const void*>(&tiebreak_lpm_kernel<false>)
-                                 : reinterpret_cast<const void*>(&tiebreak_lpm_kernel<true>);
-    const int per_cu = blocks_per_cu(fn, 64 * kTbLpmWaves, 0, 1, "tiebreak_lpm_kernel");
-    const int64_t cap = (int64_t)cu_count() * per_cu;
-    if (blocks > cap) blocks = cap;
-    if (market_list)
-      hipLaunchKernelGGL((tiebreak_lpm_kernel<false>), dim3((int)blocks), dim3(64 * kTbLpmWaves), 0,
-                         as_stream(stream), a, market_list, nl, fault_word());
-    else
-      hipLaunchKernelGGL((tiebreak_lpm_kernel<true>), dim3((int)blocks), dim3(64 * kTbLpmWaves), 0,
-                         as_stream(stream), a, market_list, nl, fault_word());
-    return check_launch("tiebreak_lpm_kernel");
-  }
-  int64_t blocks = (nl + 3) / 4;
-  const int64_t cap = (int64_t)cu_count() * 16;
-  if (blocks > cap) blocks = cap;
-  hipLaunchKernelGGL(tiebreak_wave_kernel, dim3((int)blocks), dim3(256), 0, as_stream(stream), a,
-                     market_list, nl);
-  return check_launch("tiebreak_wave_kernel");
+           g_key, g_count, g_density, g_avgconf, g_maxrel, g_of, rs, rt, rmode, ndigits, fault_word()};
+  return rmode >= 4 ? launch_tb_short<true>(a, market_list, nl, max_len, stream)
+                    : launch_tb_short<false>(a, market_list, nl, max_len, stream);
 }
 
-extern "C" int bce_tiebreak_csr_long(const int64_t* offsets, int64_t n_markets, const int32_t* list,
-                                     int64_t n_list, int32_t ndigits, const double* pred,
-                                     const double* conf, const double* weight, const double* rel,
-                                     int64_t max_len, double* winner, int32_t* label,
-                                     int32_t* n_groups, double* variance, double* g_key,
-                                     int32_t* g_count, double* g_density, double* g_avgconf,
-                                     double* g_maxrel, int32_t* g_of, void* stream) {
-  BCE_REQUIRE(n_list >= 0 && (n_list == 0 || list), "tiebreak_long: bad list");
-  if (n_list == 0) return BCE_OK;
-  BCE_REQUIRE(offsets && pred && conf && weight && rel && winner && label && n_groups && variance,
-              "tiebreak_long: NULL argument");
-  BCE_REQUIRE(max_len > 0 && max_len < (1ll << 31), "tiebreak_long: max_len out of range");
-  double rs = 1.0, rt = 0.0;
-  const int rmode = tb_round_mode(ndigits, &rs, &rt);
-  if (rmode < 0) {
-    set_error("tiebreak: precision %d is outside what this build restates exactly "
-              "(-15..22, below -308, above 323)", ndigits);
-    return BCE_EUNSUPPORTED;
-  }
-  TbArgs a{offsets, n_markets, pred, conf, weight, rel, winner, label, n_groups, variance,
-           g_key, g_count, g_density, g_avgconf, g_maxrel, g_of, rs, rt, rmode};
+template <bool EXOTIC>
+static int launch_tb_long(const TbArgs& a, const int32_t* list, int64_t n_list, int64_t max_len, void* stream) {
   hipStream_t st = as_stream(stream);
   if (max_len <= kTbMax) {
     int64_t blocks = n_list;
     const int64_t cap = (int64_t)cu_count() * 2;
     if (blocks > cap) blocks = cap;
-    hipLaunchKernelGGL(tiebreak_block_kernel<true>, dim3((int)blocks), dim3(kTbThreads), 0, st, a, list,
+    hipLaunchKernelGGL((tiebreak_block_kernel<true, EXOTIC>), dim3((int)blocks), dim3(kTbThreads), 0, st, a, list,
                        n_list, nullptr, (int64_t)0);
     return check_launch("tiebreak_block_kernel<lds>");
   }
@@ -803,9 +803,42 @@ extern "C" int bce_tiebreak_csr_long(const int64_t* offsets, int64_t n_markets, 
   if (blocks > cap) blocks = cap;
   void* scratch = nullptr;
   BCE_HIP(hipMallocAsync(&scratch, (size_t)(blocks * 16 * P), st));
-  hipLaunchKernelGGL(tiebreak_block_kernel<false>, dim3((int)blocks), dim3(kTbThreads), 0, st, a, list, n_list,
+  hipLaunchKernelGGL((tiebreak_block_kernel<false, EXOTIC>), dim3((int)blocks), dim3(kTbThreads), 0, st, a, list, n_list,
                      scratch, P);
   const int rc = check_launch("tiebreak_block_kernel<global>");
   BCE_HIP(hipFreeAsync(scratch, st));
   return rc;
+}
+
+extern "C" int bce_tiebreak_csr_long(const int64_t* offsets, int64_t n_markets, const int32_t* list,
+                                     int64_t n_list, int32_t ndigits, const double* pred,
+                                     const double* conf, const double* weight, const double* rel,
+                                     int64_t max_len, double* winner, int32_t* label,
+                                     int32_t* n_groups, double* variance, double* g_key,
+                                     int32_t* g_count, double* g_density, double* g_avgconf,
+                                     double* g_maxrel, int32_t* g_of, void* stream) {
+  BCE_REQUIRE(n_list >= 0 && (n_list == 0 || list), "tiebreak_long: bad list");
+  if (n_list == 0) return BCE_OK;
+  BCE_REQUIRE(offsets && pred && conf && weight && rel && winner && label && n_groups && variance,
+              "tiebreak_long: NULL argument");
+  BCE_REQUIRE(max_len > 0 && max_len < (1ll << 31), "tiebreak_long: max_len out of range");
+  double rs = 1.0, rt = 0.0;
+  const int rmode = tb_round_mode(ndigits, &rs, &rt);
+  TbArgs a{offsets, n_markets, pred, conf, weight, rel, winner, label, n_groups, variance,
+           g_key, g_count, g_density, g_avgconf, g_maxrel, g_of, rs, rt, rmode, ndigits, fault_word()};
+  return rmode >= 4 ? launch_tb_long<true>(a, list, n_list, max_len, stream)
+                    : launch_tb_long<false>(a, list, n_list, max_len, stream);
+}
+
+// Host-side run of the exotic-precision rounding (the same header code the EXOTIC kernels
+// run), for the CPU tests against Python round(): nd in 1..323 via round_pos, -308..-1 via
+// round_neg (both also valid where the double paths are used); *overflow = 1 when CPython
+// would raise OverflowError.
+extern "C" double bce_debug_py_round(double x, int32_t ndigits, int32_t* overflow) {
+  bool ovf = false;
+  double r = x;
+  if (ndigits > 0 && ndigits <= 323) r = bce_round::round_pos(x, ndigits);
+  else if (ndigits < 0 && ndigits >= -308) r = bce_round::round_neg(x, -ndigits, &ovf);
+  if (overflow) *overflow = ovf ? 1 : 0;
+  return r;
 }

@@ -495,7 +495,9 @@ def _c5(args, world, rank, barrier, max_over, sum_over):
     ev_k.clear()
     wall2, _ = _timed(step, a2, world, torch.cuda.current_stream(dev), barrier, max_over)
     kern2 = float(np.mean([a.elapsed_time(b) for a, b in ev_k[-a2.steps:]])) / 1e3
-    other = {"mode": mode["m"], "ms_per_step": wall2 / a2.steps * 1e3, "avg_launch_ms": kern2 * 1e3}
+    other = {"mode": mode["m"], "ms_per_step": wall2 / a2.steps * 1e3, "avg_launch_ms": kern2 * 1e3,
+             "frac": (8 * A * Mloc + 16 * A + 9 * Mloc) / kern2 / 1e9 / HBM_PEAK_GBS,
+             "traffic": _pmc("pmc_c5_fast.json" if mode["m"] == "fast" else "pmc_c5.json", markets_this_rank=Mloc)}
     mode["m"] = main_mode
     t_fast = kern if main_mode == "fast" else kern2
     parity = None
@@ -518,7 +520,8 @@ def _c5(args, world, rank, barrier, max_over, sum_over):
                    "markets_this_rank": Mloc,
                    "parallelism": f"markets sharded by column over {world} rank(s); per-agent counts all-reduced"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc("pmc_c5.json", markets_this_rank=Mloc),
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc("pmc_c5_fast.json" if main_mode == "fast" else "pmc_c5.json",
+                                                  markets_this_rank=Mloc),
                      "kernel": "reestimate_consensus_votes + reestimate_agreement_votes (one iteration)",
                      "bytes_per_launch": bytes_iter, "avg_launch_ms": kern * 1e3,
                      f"{other['mode']}_mode": other,

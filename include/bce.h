@@ -86,6 +86,11 @@ int bce_debug_set_spin_cap(int cap);
 /* Self-test of the wide kernel's VALU lane exchanges (DPP / permlane swaps) and wave scan:
  * one wave writes 13*64 words to `out` (see consensus_wide.hip); tests run it first. */
 int bce_debug_lane_selftest(unsigned* out, void* stream);
+/* Host run of the exact big-integer round(x, ndigits) the tie-break kernels use for
+ * 23 <= ndigits <= 323 and -308 <= ndigits <= -16 (valid for any 1 <= |ndigits| in range):
+ * for the CPU tests against Python round().  *overflow = 1 where CPython raises
+ * OverflowError.  No GPU needed. */
+double bce_debug_py_round(double x, int32_t ndigits, int32_t* overflow);
 
 /* ---- consensus: core.compute_consensus (core.py:63-179) + validation -------------
  *
@@ -210,9 +215,11 @@ int bce_namespace_resolve(int64_t n, const double* rel0, const double* conf0, co
  * max reliability (tiebreak.py:58-71); per signal (nullable g_of) the ordinal of its group,
  * which lets a caller rebuild the reference's dict keys with their Python types (an int
  * prediction keys its group with an int).  Group pointers may be NULL.  ndigits is the
- * DeterministicTieBreaker precision: CPython round(x, ndigits) restated exactly for
- * -15 <= ndigits <= 22, ndigits < -308 (signed zero) and ndigits > 323 (x itself); other
- * values return BCE_EUNSUPPORTED.
+ * DeterministicTieBreaker precision: CPython round(x, ndigits) restated exactly for every
+ * int (tiebreak.py:46-47,54): -15 <= ndigits <= 22 with doubles, ndigits < -308 (signed
+ * zero), ndigits > 323 (x itself), the rest with exact big integers (py_round_big.hpp).  A
+ * rounded key too large for a double (ndigits <= -16, |x| near DBL_MAX: CPython raises
+ * OverflowError) sets device fault 6, which bce_fault_check reports.
  * Slots n_groups <= j < n of a market's per-group outputs are scratch (unspecified values).
  * bce_tiebreak_csr: markets market_list[0..n_list) (NULL = all), every length <= max_len
  * <= 64 (one lane per market up to 32 agents, one wave per market beyond).  bce_tiebreak_csr_long: markets of any length >= 1, max_len

@@ -203,3 +203,56 @@ def test_glibc_pow2_restatement_matches_libm(tmp_path):
     # pow(2.0, y) of the decay factor (decay.py:58) too: bit-exact where exp2 is not
     assert f["pow2_tested"] > 3_900_000 and f["pow2_mismatches"] == 0
     assert f["exp2_differs"] > 100
+
+
+def _py_round_host(x, nd):
+    import ctypes as C
+    from bayesian_engine import _native as N
+    o = C.c_int32(0)
+    r = N.lib().bce_debug_py_round(float(x), int(nd), C.byref(o))
+    return r, bool(o.value)
+
+
+def _ref_round(x, nd):
+    try:
+        return round(x, nd), False
+    except OverflowError:
+        return None, True
+
+
+@pytest.mark.parametrize("nd", [23, 24, 30, 53, 100, 200, 300, 322, 323, -16, -17, -22, -23, -100, -200, -300, -307,
+                                -308, 1, 6, 17, 22, -1, -5, -15])
+def test_big_integer_round_matches_cpython(nd):
+    """tiebreak.py:54 round(prediction, precision) for the precisions whose 10^|nd| is not an
+    exact double: the exact big-integer restatement (py_round_big.hpp, the code the EXOTIC
+    tie-break kernels run) against CPython's round() on random, subnormal, tie and huge
+    values, bit for bit (including -0.0 and OverflowError)."""
+    import math
+    import struct
+    rng = np.random.default_rng(1000 + nd)
+    xs = list(rng.random(300))
+    xs += list(rng.random(200) * 10.0 ** rng.integers(-320, 300, 200))
+    bits = rng.integers(1, 1 << 52, 200, dtype=np.int64)
+    xs += [struct.unpack("<d", struct.pack("<q", int(b)))[0] for b in bits]  # subnormals
+    xs += [5e-324, 2.5e-323, 1e-300, 1e-200, 1e-30, 1e-24, 1.5e-23, 0.5, 0.125, 1.0, 2.5, 1e22, 1e23,
+           5e15, 4e15, 1.5e16, 2.5e16, 1e300, 1.7976931348623157e308, 8.98846567431158e307, 0.0, -0.0,
+           3.5e307, 4.5e307, 5e307, 1.0000000000000002, 0.1, 0.3]
+    # exact decimal ties at this precision: k + 1/2 units of 10^-nd where representable
+    if 0 < nd <= 330:
+        xs += [float(f"{k}.5e-{nd}") for k in range(0, 40)]
+    if nd < 0:
+        xs += [float(f"{k}.5e{-nd}") for k in range(0, 40)]
+    xs = [float(x) for x in xs]  # Python floats: numpy's own round() is not CPython's
+    xs += [-x for x in xs]
+    bad = []
+    for x in xs:
+        got, govf = _py_round_host(x, nd)
+        exp, eovf = _ref_round(x, nd)
+        if eovf or govf:
+            if eovf != govf:
+                bad.append((x, got, exp, govf, eovf))
+            continue
+        same = (struct.pack("<d", got) == struct.pack("<d", exp)) or (math.isnan(got) and math.isnan(exp))
+        if not same:
+            bad.append((x, got, exp))
+    assert not bad, bad[:5]
