@@ -322,7 +322,9 @@ def tiebreak(offsets: torch.Tensor, pred: torch.Tensor, conf: torch.Tensor, weig
     """DeterministicTieBreaker(precision).resolve for every CSR market (tiebreak.py:73-152).
 
     Any market length (> 4096 agents sort in a global scratch slice).  ``precision`` as
-    CPython round(): exact for -15..22, below -308 and above 323 (BCEError otherwise)."""
+    CPython round() for every int, bit for bit (exact big integers where 10^|precision| is
+    not a double); a rounded key too large for a double raises OverflowError, as CPython's
+    round() does (precision <= -16 only, checked with one stream synchronisation)."""
     L = N.require_gpu()
     M = offsets.numel() - 1
     Nsig = pred.numel()
@@ -344,7 +346,7 @@ def tiebreak(offsets: torch.Tensor, pred: torch.Tensor, conf: torch.Tensor, weig
     if len(long_) == 0:
         N.check(L.bce_tiebreak_csr(N.ptr(offsets), M, N.ptr(None), 0, *ins, int(max(int(lens.max(initial=1)), 1)),
                                    int(precision), *outs, st), "bce_tiebreak_csr")
-        return r
+        return _round_overflow_check(r, precision, dev)
     # n <= 32: the lane-per-market kernel; 33..64: wave per market; longer: workgroup per market
     for lo, hi in ((0, 32), (33, 64)):
         short = np.nonzero((lens >= lo) & (lens <= hi))[0].astype(np.int32)
@@ -355,6 +357,19 @@ def tiebreak(offsets: torch.Tensor, pred: torch.Tensor, conf: torch.Tensor, weig
     ll = torch.from_numpy(long_.astype(np.int32)).to(dev)
     N.check(L.bce_tiebreak_csr_long(N.ptr(offsets), M, N.ptr(ll), len(long_), int(precision), *ins,
                                     int(lens[long_].max()), *outs, st), "bce_tiebreak_csr_long")
+    return _round_overflow_check(r, precision, dev)
+
+
+def _round_overflow_check(r, precision: int, dev):
+    """round(x, n) with -308 <= n <= -16 can exceed DBL_MAX (CPython: OverflowError,
+    "rounded value too large to represent"); the kernels record that as device fault 6."""
+    if -308 <= int(precision) <= -16:
+        try:
+            N.check_faults(dev, "tiebreak round()")
+        except N.BCEError as exc:
+            if "too large to represent" in str(exc):
+                raise OverflowError("rounded value too large to represent") from None
+            raise
     return r
 
 

@@ -3,6 +3,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <set>
@@ -46,7 +47,10 @@ struct DevCtx {
   std::mutex side_mu;  // held from the plan's fork to its join (bce_consensus_planned)
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  int* queue = nullptr;               // kQueueSlots pairs of team-kernel queue words
+  std::atomic<unsigned> queue_next{0};
 };
+constexpr int kQueueSlots = 64;
 DevCtx g_dev[kMaxDev];
 
 DevCtx* dev_ctx() {
@@ -62,6 +66,10 @@ DevCtx* dev_ctx() {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
+    int* qw = nullptr;
+    if (e == hipSuccess) e = hipMalloc((void**)&qw, 2 * kQueueSlots * sizeof(int));
+    if (e == hipSuccess) e = hipMemset(qw, 0, 2 * kQueueSlots * sizeof(int));
+    if (e == hipSuccess) c->queue = qw;
     c->init_err = e;
     if (e == hipSuccess) c->fault = p;
   });
@@ -85,6 +93,13 @@ std::set<std::pair<int, const void*>> g_attr;
 int cu_count() {
   DevCtx* c = dev_ctx();
   return c ? c->cus : 256;
+}
+
+int* team_queue_slot() {
+  DevCtx* c = dev_ctx();
+  if (!c || !c->queue) return nullptr;
+  // a slot is reused after kQueueSlots launches; each launch zeroes its pair when it ends
+  return c->queue + 2 * (c->queue_next.fetch_add(1) % kQueueSlots);
 }
 
 int* fault_word() {

@@ -430,20 +430,81 @@ __device__ __forceinline__ void chain_add(double& acc, const double* src, int ce
   }
 }
 
-template <int NW, int R, bool FAST, int NN = NW>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg<NW, R, FAST, NN>::WPE, 8))) void consensus_wide_kernel(ConsArgs a) {
+// LDS of one market's team of NW waves, carved from a byte buffer: the per-bin kernel gives
+// each workgroup one team, the all-bins team kernel (below) lays 8/NW teams -- and over time
+// several configurations -- over one allocation.
+//   region A  P doubles (+ read-ahead pad): input-order probs, then sorted probs in place
+//   region B  sort exchange rows, then leaders [P] (+ exact: chain buffers [2][3][NT])
+//   small     per-wave last keys / counts, totals, error index, exact hand-off counters
+template <int NW, int R, bool FAST, int NN>
+struct WideLds {
+  using Cfg = WideCfg<NW, R, FAST, NN>;
+  static constexpr int A_BYTES = Cfg::A_DBL * 8;
+  static constexpr int B_BYTES = ((Cfg::B_U32 * 4 + 15) / 16) * 16;
+  static constexpr int TOT_OFF = A_BYTES + B_BYTES;          // sTot [3*NW] doubles
+  static constexpr int LAST_OFF = TOT_OFF + 24 * NW;          // sLast [NW]
+  static constexpr int CNT_OFF = LAST_OFF + 4 * NW;           // sCnt [NW]
+  static constexpr int MISC_OFF = CNT_OFF + 4 * NW;           // sErr, sRdy[2], sDone
+  static constexpr int BYTES = ((MISC_OFF + 16 + 15) / 16) * 16;
+  double* sA;
+  unsigned* sB;
+  double* sTot;
+  unsigned* sLast;
+  int* sCnt;
+  int* sErr;
+  int* sRdy;
+  int* sDone;
+  __device__ __forceinline__ explicit WideLds(unsigned char* base)
+      : sA(reinterpret_cast<double*>(base)),
+        sB(reinterpret_cast<unsigned*>(base + A_BYTES)),
+        sTot(reinterpret_cast<double*>(base + TOT_OFF)),
+        sLast(reinterpret_cast<unsigned*>(base + LAST_OFF)),
+        sCnt(reinterpret_cast<int*>(base + CNT_OFF)),
+        sErr(reinterpret_cast<int*>(base + MISC_OFF)),
+        sRdy(reinterpret_cast<int*>(base + MISC_OFF + 4)),
+        sDone(reinterpret_cast<int*>(base + MISC_OFF + 12)) {}
+};
+
+// The barrier a market's phases need: the whole workgroup, except for a one-wave team inside
+// the team kernel, whose LDS hand-offs stay inside its wave (in-order LDS + lgkmcnt drain).
+// Teams of >= 2 waves in the team kernel run in lockstep: every team executes the same
+// barrier sequence per market (the bin fixes it), dummy teams included.
+template <int NW, bool TEAM>
+__device__ __forceinline__ void team_sync() {
+  if constexpr (TEAM && NW == 1) wave_sync_lds();
+  else __syncthreads();
+}
+
+// Market metadata (m = order entry; n = 0 for a dummy team) and the buffer loads of its sids
+// and probabilities into registers (records = n signals, so i >= n reads 0).
+template <int NW, int R>
+__device__ __forceinline__ void wide_load(const ConsArgs& a, int64_t off, int n, int t, unsigned (&ps)[R],
+                                          double (&pp)[R]) {
+  constexpr int NT = 64 * NW, P = NT * R;
+  const int cnt = n < P ? n : P;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(a.sid + off), 0, cnt * 4, 0x00020000);
+#pragma unroll
+  for (int c = 0; c < R; ++c) ps[c] = __builtin_amdgcn_raw_buffer_load_b32(rs, t * 4, c * NT * 4, 0);
+  const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc((void*)(a.prob + off), 0, cnt * 8, 0x00020000);
+#pragma unroll
+  for (int c = 0; c < R; ++c)
+    pp[c] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rp, t * 8, c * NT * 8, 0));
+}
+
+// One market (m, off, n) on a team of NW waves; t = thread within the team.  ps / pp hold
+// its sids and probabilities (loaded by the caller); issue_next() is called once the keys are
+// built, to start the team's next market's loads into ps / pp.  m < 0: a dummy market (team
+// kernel, an item with fewer markets than teams) -- every barrier, no output.
+template <int NW, int R, bool FAST, int NN, bool TEAM, class NextFn>
+__device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW, R, FAST, NN>& L, const int t,
+                                            const int32_t m, const int64_t off, int n, unsigned (&ps)[R],
+                                            double (&pp)[R], NextFn&& issue_next) {
   using Cfg = WideCfg<NW, R, FAST, NN>;
   constexpr int NT = Cfg::NT, P = Cfg::P, IB = Cfg::IB, HR = Cfg::HR;
   constexpr unsigned QMASK = (unsigned)Cfg::PN - 1u;  // the input-index bits of a key
   constexpr int kNoErr = 0x7fffffff;
-  __shared__ __attribute__((aligned(16))) double sA[Cfg::A_DBL];
-  __shared__ __attribute__((aligned(16))) unsigned sB[Cfg::B_U32];
-  __shared__ unsigned sLast[NW];
-  __shared__ int sCnt[NW];
-  __shared__ int sErr;
-  __shared__ double sTot[3 * NW];
-  __shared__ int sRdy[2];  // exact, pipelined: producer-wave arrivals per ring slot
-  __shared__ int sDone;    // exact, pipelined: rounds the chain wave has consumed
+  double* const sA = L.sA;
+  unsigned* const sB = L.sB;
   unsigned* const sX = sB;                                            // sort exchange rows
   unsigned* const sLead = sB;                                         // [u] sid<<IB | q0
   double* const sWAC = reinterpret_cast<double*>(sB + P);             // exact: [2][3][NT]
@@ -457,14 +518,376 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
   constexpr int WFREE = FAST ? (Cfg::B_U32 - P) / 2 : 0;
   double* const sW = reinterpret_cast<double*>(sB + P);
 
-  const int t = threadIdx.x;
   const int lane = lane_id();
-  const int wv = t >> 6;
+  const int wv = __builtin_amdgcn_readfirstlane(t >> 6);  // wave within the team (uniform)
   const unsigned smax = (unsigned)(a.n_sources > 0 ? a.n_sources - 1 : 0);
   // normalizedWeight reads w[j] back from the weight output (this thread's own stores)
   // in workgroups of several waves (it saves their barriers); a single wave parks w[j] in
   // region A (dead sorted-prob slot j), which is faster than the global round trip.
   const bool wback = (NW > 1) && a.weight != nullptr;
+
+  // ---- 1. keys; next market's metadata + sids --------------------------------------
+  unsigned key[R];
+  bool badsid = false;
+#pragma unroll
+  for (int c = 0; c < R; ++c) {
+    const int i = c * NT + t;
+    const unsigned s = ps[c];
+    badsid |= (i < n) && (s > smax);
+    key[c] = (i < n) ? ((s < smax ? s : smax) << IB) | (unsigned)i : 0xFFFFFFFFu;
+  }
+  if (ballot(badsid)) raise_fault(a.fault, kFaultSid);
+  int myerr = kNoErr;
+  // input-order probs into region A before the next loads; region A's last readers are
+  // the previous market's run sums (before its final barrier) unless normalizedWeight
+  // reads w[j] from it
+  if (NW > 1 && !wback) team_sync<NW, TEAM>();
+#pragma unroll
+  for (int c = 0; c < R; ++c) {
+    const int i = c * NT + t;
+    const double p = pp[c];
+    sA[i] = p;
+    if ((i < n) && (p < 0.0 || p > 1.0) && myerr == kNoErr) myerr = i;  // core.py:59-60
+  }
+  issue_next();
+  if (n > P) {  // longer than this launch's max_len: left unprocessed, reported
+    raise_fault(a.fault, kFaultTooLong);
+    if constexpr (!TEAM) return;  // uniform over the workgroup
+    n = 0;                        // lockstep teams: a dummy market (every barrier, no output)
+  }
+  if (t == 0) *L.sErr = kNoErr;
+
+  // ---- 2. sort (core.py:103 order; ties in input order by the index bits) ----------
+  wide_sort<NN, NW, R>(key, sX, t, lane);
+
+  // ---- 3. input-order probs + range check, sorted probs in place, leaders ----------
+  if (lane == 63) L.sLast[wv] = key[R - 1];
+  team_sync<NW, TEAM>();  // (a) input-order probs + sLast visible; exchange rows dead
+  if (myerr != kNoErr) atomicMin(L.sErr, myerr);
+  double x[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int q = t * R + r;
+    x[r] = (q < n) ? sA[key[r] & QMASK] : 0.0;
+  }
+  const unsigned prev_in_wave = (unsigned)__builtin_amdgcn_update_dpp(0, (int)key[R - 1], 0x138, 0xF, 0xF, false);  // wave_shr:1
+  const unsigned prev_key = (lane > 0) ? prev_in_wave : (wv > 0 ? L.sLast[wv - 1] : 0u);
+  unsigned lead = 0;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int q = t * R + r;
+    const unsigned ps0 = ((r == 0) ? prev_key : key[r - 1]) >> IB;
+    const bool is = (q < n) && (q == 0 || (key[r] >> IB) != ps0);
+    lead |= is ? (1u << r) : 0u;
+  }
+  const int cnt = __popc(lead);
+  const int incl = wave_incl_scan(cnt);
+  if (lane == 63) L.sCnt[wv] = incl;
+  team_sync<NW, TEAM>();  // (b) every read of the input-order probs done; counts visible
+#pragma unroll
+  for (int r = 0; r < R; r += 2)
+    *reinterpret_cast<double2*>(sA + t * R + r) = make_double2(x[r], x[r + 1]);
+  int base = incl - cnt, u = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    const int cw = L.sCnt[w];
+    if (w < wv) base += cw;
+    u += cw;
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (lead & (1u << r)) {
+      const int jj = base + __popc(lead & ((1u << r) - 1u));
+      sLead[jj] = (key[r] & ~QMASK) | (unsigned)(t * R + r);
+    }
+  }
+  if (t == 0) {
+    L.sRdy[0] = L.sRdy[1] = 0;
+    *L.sDone = 0;
+  }
+  team_sync<NW, TEAM>();  // (c) sorted probs + leaders visible
+
+  // ---- 4. per-unique products --------------------------------------------------------
+  double acc = 0.0;                     // exact: wave 0 lanes 0..2 carry the chains
+  double pw = 0.0, pa = 0.0, pc = 0.0;  // fast: this thread's partial sums
+  // EXACT with several waves (and the weight output, so region A is not needed for w):
+  // wave 0 only carries the chains while waves 1.. produce rounds of NP = NT - 64
+  // uniques into a two-slot LDS ring, handed over with LDS counters instead of barriers,
+  // so the serial chains overlap the gathers and run sums of the next rounds.
+  const bool piped = !FAST && NW > 1 && wback;
+  if (piped) {
+    constexpr int NP = (NW > 1) ? NT - 64 : NT;
+    const int nrp = (u + NP - 1) / NP;
+    if (wv == 0) {
+      __builtin_amdgcn_s_setprio(2);  // the chain is the critical path
+      for (int r = 0; r < nrp; ++r) {
+        const int slot = r & 1;
+        const int need = (NW - 1) * ((r >> 1) + 1);
+        int spins = 0;
+        while (ldsflag(&L.sRdy[slot]) < need) {
+          if (++spins > a.spin_cap) {
+            raise_fault(a.fault, kFaultSpinChain);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        const int ce = (u - r * NP < NP) ? u - r * NP : NP;
+        chain_add(acc, sWAC + slot * 3 * NP + (lane % 3) * NP, ce);
+        if (lane == 0) __hip_atomic_store(L.sDone, r + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      __builtin_amdgcn_s_setprio(0);
+    } else {
+      const int pt = t - 64;
+      for (int h = 0; h < nrp; h += HR) {
+        double2 rc[HR];
+        int q0s[HR], q1s[HR];
+        unsigned sids[HR], pwd[HR];
+#pragma unroll
+        for (int i = 0; i < HR; ++i) {  // every gather of the group in flight together
+          const int jj = (h + i) * NP + pt;
+          q0s[i] = q1s[i] = 0;
+          sids[i] = pwd[i] = 0;
+          rc[i] = make_double2(0.5, 0.25);  // DEFAULT_RELIABILITY / _CONFIDENCE (empty table)
+          if (jj < u) {
+            const unsigned lv = sLead[jj];
+            q0s[i] = (int)(lv & QMASK);
+            sids[i] = min(lv >> IB, smax);
+            q1s[i] = (jj + 1 < u) ? (int)(sLead[jj + 1] & QMASK) : n;
+            if (a.n_sources > 0) {
+              rc[i] = a.relconf[sids[i]];
+              pwd[i] = a.pbits[sids[i] >> 5];
+            }
+          }
+        }
+        double vw[HR], va[HR], vc[HR];
+#pragma unroll
+        for (int i = 0; i < HR; ++i) {
+          const int jj = (h + i) * NP + pt;
+          vw[i] = va[i] = vc[i] = 0.0;
+          if (jj < u) {
+            const double avg = run_sum(sA + q0s[i], q1s[i] - q0s[i]);  // core.py:116
+            const double w = rc[i].x;  // core.py:111,119
+            vw[i] = w;
+            va[i] = avg * w;        // core.py:136
+            vc[i] = rc[i].y * w;    // core.py:142
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < HR; ++i) {
+          const int r = h + i;
+          if (r < nrp) {
+            const int slot = r & 1;
+            if (r >= 2) {  // the slot's previous round is consumed
+              int spins = 0;
+              while (ldsflag(L.sDone) < r - 1) {
+                if (++spins > a.spin_cap) {
+                  raise_fault(a.fault, kFaultSpinChain);
+                  break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+              }
+            }
+            double* const buf = sWAC + slot * 3 * NP;
+            buf[pt] = vw[i];
+            buf[NP + pt] = va[i];
+            buf[2 * NP + pt] = vc[i];
+            wave_sync_lds();  // this wave's part of the round is in LDS
+            if (lane == 0)
+              __hip_atomic_fetch_add(&L.sRdy[slot], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < HR; ++i) {
+          const int jj = (h + i) * NP + pt;
+          if (jj < u) {
+            const int64_t p = off + jj;
+            if (a.usid)
+              a.usid[p] = (int32_t)sids[i] | (((pwd[i] >> (sids[i] & 31)) & 1u) ? 0 : (int32_t)0x80000000);
+            a.weight[p] = vw[i];
+          }
+        }
+      }
+    }
+  }
+  const int nr = piped ? 0 : (u + NT - 1) / NT;
+  const bool park = FAST && wback && u <= WFREE;
+  for (int h = 0; h < nr; h += HR) {
+    double2 rc[HR];
+    int q0s[HR], q1s[HR];
+    unsigned sids[HR], pwd[HR];
+#pragma unroll
+    for (int i = 0; i < HR; ++i) {  // every gather of the group in flight together
+      const int jj = (h + i) * NT + t;
+      q0s[i] = q1s[i] = 0;
+      sids[i] = pwd[i] = 0;
+      rc[i] = make_double2(0.5, 0.25);  // DEFAULT_RELIABILITY / _CONFIDENCE (empty table)
+      if (jj < u) {
+        const unsigned lv = sLead[jj];
+        q0s[i] = (int)(lv & QMASK);
+        sids[i] = min(lv >> IB, smax);  // <= smax by construction of the key; clamped anyway
+        q1s[i] = (jj + 1 < u) ? (int)(sLead[jj + 1] & QMASK) : n;
+        if (a.n_sources > 0) {
+          rc[i] = a.relconf[sids[i]];
+          pwd[i] = a.pbits[sids[i] >> 5];
+        }
+      }
+    }
+    double vw[HR], va[HR], vc[HR];
+#pragma unroll
+    for (int i = 0; i < HR; ++i) {
+      const int jj = (h + i) * NT + t;
+      const int len = q1s[i] - q0s[i];
+      double avg = 0.0;
+      if constexpr (FAST) {
+        // runs longer than kWaveRun (hot sources) are summed by the whole wave in a fixed
+        // order instead of by their own lane, so one hot source does not hold the wave
+        avg = (jj < u && len <= kWaveRun) ? run_sum(sA + q0s[i], len) : 0.0;
+        unsigned long long lm = ballot(jj < u && len > kWaveRun);
+        while (lm) {
+          const int LL = __builtin_ctzll(lm);
+          lm &= lm - 1;
+          const int lq0 = __builtin_amdgcn_readlane(q0s[i], LL), llen = __builtin_amdgcn_readlane(len, LL);
+          double part = 0.0;
+          for (int e = lane; e < llen; e += 64) part += sA[lq0 + e];
+          part = wave_sum_fixed(part);
+          if (lane == LL) avg = part / (double)llen;
+        }
+      } else if (jj < u) {
+        avg = run_sum(sA + q0s[i], len);
+      }
+      vw[i] = va[i] = vc[i] = 0.0;
+      if (jj < u) {
+        const double w = rc[i].x;  // core.py:111,119
+        vw[i] = w;
+        va[i] = avg * w;        // core.py:136
+        vc[i] = rc[i].y * w;    // core.py:142
+      }
+    }
+    if constexpr (FAST) {
+#pragma unroll
+      for (int i = 0; i < HR; ++i) {  // round order: fixed per thread
+        pw += vw[i];
+        pa += va[i];
+        pc += vc[i];
+      }
+      if (!wback) {
+        team_sync<NW, TEAM>();  // every sorted-prob read of this group done
+#pragma unroll
+        for (int i = 0; i < HR; ++i) {
+          const int jj = (h + i) * NT + t;
+          if (jj < u) sA[jj] = vw[i];  // later groups read only slots > jj
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < HR; ++i) {
+        if (h + i < nr) {
+          double* const buf = sWAC + ((h + i) & 1) * 3 * NT;
+          buf[t] = vw[i];
+          buf[NT + t] = va[i];
+          buf[2 * NT + t] = vc[i];
+          team_sync<NW, TEAM>();  // round staged; every sorted-prob read of this group is done
+          const int jj = (h + i) * NT + t;
+          if (jj < u && !wback) sA[jj] = vw[i];  // slot jj is only read by uniques <= jj
+          if (wv == 0) {
+            __builtin_amdgcn_s_setprio(2);  // the chain is the critical path
+            const int ce = (u - (h + i) * NT < NT) ? u - (h + i) * NT : NT;
+            chain_add(acc, buf + (lane % 3) * NT, ce);
+            __builtin_amdgcn_s_setprio(0);
+          }
+        }
+      }
+    }
+    // per-unique outputs after the group's LDS work, so no store is pending under it;
+    // nontemporal (FAST -0.5..1%, profiles/r03k/wide_r03u_ab.txt)
+#pragma unroll
+    for (int i = 0; i < HR; ++i) {
+      const int jj = (h + i) * NT + t;
+      if (jj < u) {
+        const int64_t p = off + jj;
+        if (a.usid)
+          __builtin_nontemporal_store((int32_t)sids[i] | (((pwd[i] >> (sids[i] & 31)) & 1u) ? 0 : (int32_t)0x80000000), &a.usid[p]);
+        if (a.weight) __builtin_nontemporal_store(vw[i], &a.weight[p]);
+        if (park) sW[jj] = vw[i];
+      }
+    }
+  }
+
+  // ---- 5. totals, per-market outputs, nweight ------------------------------------------
+  if constexpr (FAST) {
+    pw = wave_sum_fixed(pw);
+    pa = wave_sum_fixed(pa);
+    pc = wave_sum_fixed(pc);
+    if (lane == 0) {
+      L.sTot[3 * wv] = pw;
+      L.sTot[3 * wv + 1] = pa;
+      L.sTot[3 * wv + 2] = pc;
+    }
+  } else {
+    if (wv == 0 && lane < 3) L.sTot[lane] = acc;
+  }
+  team_sync<NW, TEAM>();  // totals + w[j] visible
+  double tw = L.sTot[0], ta = L.sTot[1], tc = L.sTot[2];
+  if constexpr (FAST) {
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+      tw += L.sTot[3 * w];
+      ta += L.sTot[3 * w + 1];
+      tc += L.sTot[3 * w + 2];
+    }
+  }
+  if (t == 0 && m >= 0) {
+    const bool null_ = (n == 0) || (tw == 0.0);
+    a.consensus[m] = null_ ? 0.0 : ta / tw;
+    a.confidence[m] = null_ ? 0.0 : tc / tw;
+    a.total_weight[m] = tw;
+    a.n_unique[m] = u;
+    if (a.err_idx) a.err_idx[m] = (*L.sErr == kNoErr) ? -1 : *L.sErr;
+  }
+  if (a.nweight) {  // core.py:151
+    if constexpr (!FAST) {
+      // every read-back issued before any nweight store: loads retire behind earlier
+      // stores (vmcnt is in order), so a load/store per iteration waits out each store
+      // (C3 exact -2.6%; FAST: batches of kWideNWBF, a full batch costs it spills)
+      double wj[R];
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        const int jj = t + NT * k;
+        wj[k] = (jj < u) ? (wback ? a.weight[off + jj] : sA[jj]) : 0.0;
+      }
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        const int jj = t + NT * k;
+        if (jj < u) a.nweight[off + jj] = (tw > 0.0) ? wj[k] / tw : 0.0;
+      }
+    } else {
+      constexpr int NB = (kWideNWBF < R) ? kWideNWBF : R;  // read-backs per batch
+      for (int j0 = t; j0 < u; j0 += NB * NT) {
+        double wj[NB];
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+          const int jj = j0 + NT * k;
+          wj[k] = (jj < u) ? (park ? sW[jj] : wback ? a.weight[off + jj] : sA[jj]) : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+          const int jj = j0 + NT * k;
+          if (jj < u) __builtin_nontemporal_store((tw > 0.0) ? wj[k] / tw : 0.0, &a.nweight[off + jj]);
+        }
+      }
+    }
+  }
+}
+
+// One bin per launch: a persistent grid of NW-wave workgroups strides over the bin's market
+// list (one market per workgroup at a time, the next one's loads issued during this one).
+template <int NW, int R, bool FAST, int NN = NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg<NW, R, FAST, NN>::WPE, 8))) void consensus_wide_kernel(ConsArgs a) {
+  using LD = WideLds<NW, R, FAST, NN>;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LD::BYTES];
+  const LD L(smem);
+  const int t = threadIdx.x;
+  const int lane = lane_id();
 
   // Market metadata for this workgroup's next 64 markets (li = base + G*k on lane k) is
   // loaded in one vector batch, so picking a market is a readlane, never a scalar-load
@@ -493,384 +916,165 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
   };
   unsigned ps[R];
   double pp[R];
-  auto load_sids = [&]() {
-    const int cnt = nn < P ? nn : P;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(a.sid + noff), 0, cnt * 4, 0x00020000);
-#pragma unroll
-    for (int c = 0; c < R; ++c) ps[c] = __builtin_amdgcn_raw_buffer_load_b32(rs, t * 4, c * NT * 4, 0);
-  };
-  auto load_probs = [&]() {
-    const int cnt = nn < P ? nn : P;
-    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc((void*)(a.prob + noff), 0, cnt * 8, 0x00020000);
-#pragma unroll
-    for (int c = 0; c < R; ++c)
-      pp[c] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rp, t * 8, c * NT * 8, 0));
-  };
   if (blockIdx.x < a.n_list) {
     meta(blockIdx.x);
-    load_sids();
-    load_probs();
+    wide_load<NW, R>(a, noff, nn, t, ps, pp);
   }
-
   for (int64_t li = blockIdx.x; li < a.n_list; li += G) {
     const int32_t m = nm;
     const int64_t off = noff;
     const int n = nn;
+    wide_market<NW, R, FAST, NN, false>(a, L, t, m, off, n, ps, pp, [&]() {
+      if (li + G < a.n_list) {
+        meta(li + G);
+        wide_load<NW, R>(a, noff, nn, t, ps, pp);
+      }
+    });
+  }
+}
 
-    // ---- 1. keys; next market's metadata + sids ------------------------------------
-    unsigned key[R];
-    bool badsid = false;
-#pragma unroll
-    for (int c = 0; c < R; ++c) {
-      const int i = c * NT + t;
-      const unsigned s = ps[c];
-      badsid |= (i < n) && (s > smax);
-      key[c] = (i < n) ? ((s < smax ? s : smax) << IB) | (unsigned)i : 0xFFFFFFFFu;
-    }
-    if (ballot(badsid)) raise_fault(a.fault, kFaultSid);
-    int myerr = kNoErr;
-    // input-order probs into region A before the next loads; region A's last readers are
-    // the previous market's run sums (before its final barrier) unless normalizedWeight
-    // reads w[j] from it
-    if (NW > 1 && !wback) __syncthreads();
-#pragma unroll
-    for (int c = 0; c < R; ++c) {
-      const int i = c * NT + t;
-      const double p = pp[c];
-      sA[i] = p;
-      if ((i < n) && (p < 0.0 || p > 1.0) && myerr == kNoErr) myerr = i;  // core.py:59-60
-    }
-    const bool has_next = li + G < a.n_list;
-    if (has_next) {
-      meta(li + G);
-      load_sids();
-      load_probs();
-    }
-    if (n > P) {  // longer than this launch's max_len: left unprocessed, reported
-      raise_fault(a.fault, kFaultTooLong);
-      continue;
-    }
-    if (t == 0) sErr = kNoErr;
+// ---- all wide bins in one persistent launch (planned calls) ---------------------------
+// Workgroups of 8 waves pull items from a device queue: an item is up to 8/NW consecutive
+// markets of one length bin (the plan lists each bin's markets longest first and the bins
+// longest first), one market per team of NW waves.  One launch per step instead of one per
+// bin: a single ramp and a single tail, and a workgroup that finishes its long markets moves
+// on to shorter ones instead of idling at a bin boundary -- what a 1/8 market shard of C3
+// needs.  The queue word pair (next item, finished workgroups) is reset by the
+// last workgroup out, ready for the next launch.
+constexpr int kTeamWaves = 8;
+constexpr int kTeamBins = 8;  // 65..128, ..256, ..512, ..1024, ..1536, ..2048, ..3072, ..4096
 
-    // ---- 2. sort (core.py:103 order; ties in input order by the index bits) ----------
-    wide_sort<NN, NW, R>(key, sX, t, lane);
+struct WideItems {
+  int* queue;                    // [2]: next item, finished workgroups (zero between launches)
+  int32_t n_items;
+  int32_t item_start[kTeamBins + 1];  // items of team bin k: [item_start[k], item_start[k+1])
+  int32_t first[kTeamBins];      // bin k's first position in a.list
+  int32_t end[kTeamBins];        // one past its last
+};
 
-    // ---- 3. input-order probs + range check, sorted probs in place, leaders ----------
-    if (lane == 63) sLast[wv] = key[R - 1];
-    __syncthreads();  // (a) input-order probs + sLast visible; exchange rows dead
-    if (myerr != kNoErr) atomicMin(&sErr, myerr);
-    double x[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int q = t * R + r;
-      x[r] = (q < n) ? sA[key[r] & QMASK] : 0.0;
-    }
-    const unsigned prev_in_wave = (unsigned)__builtin_amdgcn_update_dpp(0, (int)key[R - 1], 0x138, 0xF, 0xF, false);  // wave_shr:1
-    const unsigned prev_key = (lane > 0) ? prev_in_wave : (wv > 0 ? sLast[wv - 1] : 0u);
-    unsigned lead = 0;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int q = t * R + r;
-      const unsigned ps0 = ((r == 0) ? prev_key : key[r - 1]) >> IB;
-      const bool is = (q < n) && (q == 0 || (key[r] >> IB) != ps0);
-      lead |= is ? (1u << r) : 0u;
-    }
-    const int cnt = __popc(lead);
-    const int incl = wave_incl_scan(cnt);
-    if (lane == 63) sCnt[wv] = incl;
-    __syncthreads();  // (b) every read of the input-order probs done; counts visible
-#pragma unroll
-    for (int r = 0; r < R; r += 2)
-      *reinterpret_cast<double2*>(sA + t * R + r) = make_double2(x[r], x[r + 1]);
-    int base = incl - cnt, u = 0;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) {
-      const int cw = sCnt[w];
-      if (w < wv) base += cw;
-      u += cw;
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      if (lead & (1u << r)) {
-        const int jj = base + __popc(lead & ((1u << r) - 1u));
-        sLead[jj] = (key[r] & ~QMASK) | (unsigned)(t * R + r);
-      }
-    }
-    if (t == 0) {
-      sRdy[0] = sRdy[1] = 0;
-      sDone = 0;
-    }
-    __syncthreads();  // (c) sorted probs + leaders visible
+// team bin k in processing order (longest markets first): 0 = 3073..4096, 7 = 65..128
+template <int K> struct TeamBin;
+template <> struct TeamBin<0> { static constexpr int NW = 8, R = 8; };  // 3073..4096
+template <> struct TeamBin<1> { static constexpr int NW = 8, R = 8; };  // 2049..3072
+template <> struct TeamBin<2> { static constexpr int NW = 4, R = 8; };  // 1537..2048
+template <> struct TeamBin<3> { static constexpr int NW = 4, R = 8; };  // 1025..1536
+template <> struct TeamBin<4> { static constexpr int NW = 2, R = 8; };  // 513..1024
+template <> struct TeamBin<5> { static constexpr int NW = 1, R = 8; };  // 257..512
+template <> struct TeamBin<6> { static constexpr int NW = 1, R = 4; };  // 129..256
+template <> struct TeamBin<7> { static constexpr int NW = 1, R = 2; };  // 65..128
 
-    // ---- 4. per-unique products --------------------------------------------------------
-    double acc = 0.0;                     // exact: wave 0 lanes 0..2 carry the chains
-    double pw = 0.0, pa = 0.0, pc = 0.0;  // fast: this thread's partial sums
-    // EXACT with several waves (and the weight output, so region A is not needed for w):
-    // wave 0 only carries the chains while waves 1.. produce rounds of NP = NT - 64
-    // uniques into a two-slot LDS ring, handed over with LDS counters instead of barriers,
-    // so the serial chains overlap the gathers and run sums of the next rounds.
-    const bool piped = !FAST && NW > 1 && wback;
-    if (piped) {
-      constexpr int NP = (NW > 1) ? NT - 64 : NT;
-      const int nrp = (u + NP - 1) / NP;
-      if (wv == 0) {
-        __builtin_amdgcn_s_setprio(2);  // the chain is the critical path
-        for (int r = 0; r < nrp; ++r) {
-          const int slot = r & 1;
-          const int need = (NW - 1) * ((r >> 1) + 1);
-          int spins = 0;
-          while (ldsflag(&sRdy[slot]) < need) {
-            if (++spins > a.spin_cap) {
-              raise_fault(a.fault, kFaultSpinChain);
-              break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-          }
-          const int ce = (u - r * NP < NP) ? u - r * NP : NP;
-          chain_add(acc, sWAC + slot * 3 * NP + (lane % 3) * NP, ce);
-          if (lane == 0) __hip_atomic_store(&sDone, r + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        __builtin_amdgcn_s_setprio(0);
-      } else {
-        const int pt = t - 64;
-        for (int h = 0; h < nrp; h += HR) {
-          double2 rc[HR];
-          int q0s[HR], q1s[HR];
-          unsigned sids[HR], pwd[HR];
-#pragma unroll
-          for (int i = 0; i < HR; ++i) {  // every gather of the group in flight together
-            const int jj = (h + i) * NP + pt;
-            q0s[i] = q1s[i] = 0;
-            sids[i] = pwd[i] = 0;
-            rc[i] = make_double2(0.5, 0.25);  // DEFAULT_RELIABILITY / _CONFIDENCE (empty table)
-            if (jj < u) {
-              const unsigned lv = sLead[jj];
-              q0s[i] = (int)(lv & QMASK);
-              sids[i] = min(lv >> IB, smax);
-              q1s[i] = (jj + 1 < u) ? (int)(sLead[jj + 1] & QMASK) : n;
-              if (a.n_sources > 0) {
-                rc[i] = a.relconf[sids[i]];
-                pwd[i] = a.pbits[sids[i] >> 5];
-              }
-            }
-          }
-          double vw[HR], va[HR], vc[HR];
-#pragma unroll
-          for (int i = 0; i < HR; ++i) {
-            const int jj = (h + i) * NP + pt;
-            vw[i] = va[i] = vc[i] = 0.0;
-            if (jj < u) {
-              const double avg = run_sum(sA + q0s[i], q1s[i] - q0s[i]);  // core.py:116
-              const double w = rc[i].x;  // core.py:111,119
-              vw[i] = w;
-              va[i] = avg * w;        // core.py:136
-              vc[i] = rc[i].y * w;    // core.py:142
-            }
-          }
-#pragma unroll
-          for (int i = 0; i < HR; ++i) {
-            const int r = h + i;
-            if (r < nrp) {
-              const int slot = r & 1;
-              if (r >= 2) {  // the slot's previous round is consumed
-                int spins = 0;
-                while (ldsflag(&sDone) < r - 1) {
-                  if (++spins > a.spin_cap) {
-                    raise_fault(a.fault, kFaultSpinChain);
-                    break;
-                  }
-                  __builtin_amdgcn_s_sleep(1);
-                }
-              }
-              double* const buf = sWAC + slot * 3 * NP;
-              buf[pt] = vw[i];
-              buf[NP + pt] = va[i];
-              buf[2 * NP + pt] = vc[i];
-              wave_sync_lds();  // this wave's part of the round is in LDS
-              if (lane == 0)
-                __hip_atomic_fetch_add(&sRdy[slot], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-          }
-#pragma unroll
-          for (int i = 0; i < HR; ++i) {
-            const int jj = (h + i) * NP + pt;
-            if (jj < u) {
-              const int64_t p = off + jj;
-              if (a.usid)
-                a.usid[p] = (int32_t)sids[i] | (((pwd[i] >> (sids[i] & 31)) & 1u) ? 0 : (int32_t)0x80000000);
-              a.weight[p] = vw[i];
-            }
-          }
-        }
-      }
-    }
-    const int nr = piped ? 0 : (u + NT - 1) / NT;
-    const bool park = FAST && wback && u <= WFREE;
-    for (int h = 0; h < nr; h += HR) {
-      double2 rc[HR];
-      int q0s[HR], q1s[HR];
-      unsigned sids[HR], pwd[HR];
-#pragma unroll
-      for (int i = 0; i < HR; ++i) {  // every gather of the group in flight together
-        const int jj = (h + i) * NT + t;
-        q0s[i] = q1s[i] = 0;
-        sids[i] = pwd[i] = 0;
-        rc[i] = make_double2(0.5, 0.25);  // DEFAULT_RELIABILITY / _CONFIDENCE (empty table)
-        if (jj < u) {
-          const unsigned lv = sLead[jj];
-          q0s[i] = (int)(lv & QMASK);
-          sids[i] = min(lv >> IB, smax);  // <= smax by construction of the key; clamped anyway
-          q1s[i] = (jj + 1 < u) ? (int)(sLead[jj + 1] & QMASK) : n;
-          if (a.n_sources > 0) {
-            rc[i] = a.relconf[sids[i]];
-            pwd[i] = a.pbits[sids[i] >> 5];
-          }
-        }
-      }
-      double vw[HR], va[HR], vc[HR];
-#pragma unroll
-      for (int i = 0; i < HR; ++i) {
-        const int jj = (h + i) * NT + t;
-        const int len = q1s[i] - q0s[i];
-        double avg = 0.0;
-        if constexpr (FAST) {
-          // runs longer than kWaveRun (hot sources) are summed by the whole wave in a fixed
-          // order instead of by their own lane, so one hot source does not hold the wave
-          avg = (jj < u && len <= kWaveRun) ? run_sum(sA + q0s[i], len) : 0.0;
-          unsigned long long lm = ballot(jj < u && len > kWaveRun);
-          while (lm) {
-            const int L = __builtin_ctzll(lm);
-            lm &= lm - 1;
-            const int lq0 = __builtin_amdgcn_readlane(q0s[i], L), llen = __builtin_amdgcn_readlane(len, L);
-            double part = 0.0;
-            for (int e = lane; e < llen; e += 64) part += sA[lq0 + e];
-            part = wave_sum_fixed(part);
-            if (lane == L) avg = part / (double)llen;
-          }
-        } else if (jj < u) {
-          avg = run_sum(sA + q0s[i], len);
-        }
-        vw[i] = va[i] = vc[i] = 0.0;
-        if (jj < u) {
-          const double w = rc[i].x;  // core.py:111,119
-          vw[i] = w;
-          va[i] = avg * w;        // core.py:136
-          vc[i] = rc[i].y * w;    // core.py:142
-        }
-      }
-      if constexpr (FAST) {
-#pragma unroll
-        for (int i = 0; i < HR; ++i) {  // round order: fixed per thread
-          pw += vw[i];
-          pa += va[i];
-          pc += vc[i];
-        }
-        if (!wback) {
-          __syncthreads();  // every sorted-prob read of this group done
-#pragma unroll
-          for (int i = 0; i < HR; ++i) {
-            const int jj = (h + i) * NT + t;
-            if (jj < u) sA[jj] = vw[i];  // later groups read only slots > jj
-          }
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < HR; ++i) {
-          if (h + i < nr) {
-            double* const buf = sWAC + ((h + i) & 1) * 3 * NT;
-            buf[t] = vw[i];
-            buf[NT + t] = va[i];
-            buf[2 * NT + t] = vc[i];
-            __syncthreads();  // round staged; every sorted-prob read of this group is done
-            const int jj = (h + i) * NT + t;
-            if (jj < u && !wback) sA[jj] = vw[i];  // slot jj is only read by uniques <= jj
-            if (wv == 0) {
-              __builtin_amdgcn_s_setprio(2);  // the chain is the critical path
-              const int ce = (u - (h + i) * NT < NT) ? u - (h + i) * NT : NT;
-              chain_add(acc, buf + (lane % 3) * NT, ce);
-              __builtin_amdgcn_s_setprio(0);
-            }
-          }
-        }
-      }
-      // per-unique outputs after the group's LDS work, so no store is pending under it;
-      // nontemporal (FAST -0.5..1%, profiles/r03k/wide_r03u_ab.txt)
-#pragma unroll
-      for (int i = 0; i < HR; ++i) {
-        const int jj = (h + i) * NT + t;
-        if (jj < u) {
-          const int64_t p = off + jj;
-          if (a.usid)
-            __builtin_nontemporal_store((int32_t)sids[i] | (((pwd[i] >> (sids[i] & 31)) & 1u) ? 0 : (int32_t)0x80000000), &a.usid[p]);
-          if (a.weight) __builtin_nontemporal_store(vw[i], &a.weight[p]);
-          if (park) sW[jj] = vw[i];
-        }
-      }
-    }
+template <bool FAST>
+constexpr int team_lds_bytes() {
+  int mx = 0;
+  const int b[5] = {kTeamWaves * WideLds<1, 2, FAST, 1>::BYTES, kTeamWaves * WideLds<1, 4, FAST, 1>::BYTES,
+                    kTeamWaves * WideLds<1, 8, FAST, 1>::BYTES, (kTeamWaves / 2) * WideLds<2, 8, FAST, 2>::BYTES,
+                    (kTeamWaves / 4) * WideLds<4, 8, FAST, 4>::BYTES};
+  for (int i = 0; i < 5; ++i) mx = b[i] > mx ? b[i] : mx;
+  const int b8 = WideLds<8, 8, FAST, 8>::BYTES;
+  return b8 > mx ? b8 : mx;
+}
 
-    // ---- 5. next market's probabilities; totals, per-market outputs, nweight ---------
-    if constexpr (FAST) {
-      pw = wave_sum_fixed(pw);
-      pa = wave_sum_fixed(pa);
-      pc = wave_sum_fixed(pc);
-      if (lane == 0) {
-        sTot[3 * wv] = pw;
-        sTot[3 * wv + 1] = pa;
-        sTot[3 * wv + 2] = pc;
-      }
-    } else {
-      if (wv == 0 && lane < 3) sTot[lane] = acc;
+__device__ __forceinline__ int team_bin_of(const WideItems& q, int item) {
+  int k = 0;
+#pragma unroll
+  for (int i = 1; i < kTeamBins; ++i) k += (item >= q.item_start[i]) ? 1 : 0;
+  return k;
+}
+
+// Items of team bin K while the queue keeps handing this workgroup items of that bin.
+// cur / nxt: the item being started and the one already claimed after it (known to every
+// thread); the claim after that is made by thread 0 during the current item and published at
+// the item's closing barrier (two LDS slots, alternating).
+template <int K, bool FAST>
+__device__ __forceinline__ void team_run(const ConsArgs& a, const WideItems& q, unsigned char* smem, int* sItem,
+                                         int& cur, int& nxt, int& slot, bool& claiming) {
+  constexpr int NW = TeamBin<K>::NW, R = TeamBin<K>::R;
+  constexpr int TEAMS = kTeamWaves / NW;
+  using LD = WideLds<NW, R, FAST, NW>;
+  const int t0 = threadIdx.x;
+  const int team = __builtin_amdgcn_readfirstlane((int)(t0 >> 6)) / NW;  // uniform: LDS bases stay scalar
+  const int t = t0 - team * 64 * NW;
+  const LD L(smem + team * LD::BYTES);
+  unsigned ps[R];
+  double pp[R];
+  // this team's market of item `it` (m < 0: none -- the bin's last item can be short)
+  auto market_of = [&](int it, int32_t& m, int64_t& off, int& n) {
+    const int64_t pos = (int64_t)q.first[K] + (int64_t)(it - q.item_start[K]) * TEAMS + team;
+    m = -1;
+    off = 0;
+    n = 0;
+    if (pos < q.end[K]) {
+      m = a.list[pos];
+      off = a.offsets[m];
+      n = (int)(a.offsets[m + 1] - off);
     }
-    __syncthreads();  // totals + w[j] visible
-    double tw = sTot[0], ta = sTot[1], tc = sTot[2];
-    if constexpr (FAST) {
-#pragma unroll
-      for (int w = 1; w < NW; ++w) {
-        tw += sTot[3 * w];
-        ta += sTot[3 * w + 1];
-        tc += sTot[3 * w + 2];
+  };
+  int32_t m;
+  int64_t off;
+  int n;
+  market_of(cur, m, off, n);
+  wide_load<NW, R>(a, off, n, t, ps, pp);
+  for (;;) {
+    if (t0 == 0) {  // the claim after nxt (past the end once a claim has landed there)
+      int c = q.n_items;
+      if (claiming) {
+        c = atomicAdd(&q.queue[0], 1);
+        claiming = c < q.n_items;
       }
+      sItem[slot] = c;
     }
-    if (t == 0) {
-      const bool null_ = (n == 0) || (tw == 0.0);
-      a.consensus[m] = null_ ? 0.0 : ta / tw;
-      a.confidence[m] = null_ ? 0.0 : tc / tw;
-      a.total_weight[m] = tw;
-      a.n_unique[m] = u;
-      if (a.err_idx) a.err_idx[m] = (sErr == kNoErr) ? -1 : sErr;
-    }
-    if (a.nweight) {  // core.py:151
-      if constexpr (!FAST) {
-        // every read-back issued before any nweight store: loads retire behind earlier
-        // stores (vmcnt is in order), so a load/store per iteration waits out each store
-        // (C3 exact -2.6%; FAST: batches of kWideNWBF, a full batch costs it spills)
-        double wj[R];
-#pragma unroll
-        for (int k = 0; k < R; ++k) {
-          const int jj = t + NT * k;
-          wj[k] = (jj < u) ? (wback ? a.weight[off + jj] : sA[jj]) : 0.0;
-        }
-#pragma unroll
-        for (int k = 0; k < R; ++k) {
-          const int jj = t + NT * k;
-          if (jj < u) a.nweight[off + jj] = (tw > 0.0) ? wj[k] / tw : 0.0;
-        }
-      } else {
-        constexpr int NB = (kWideNWBF < R) ? kWideNWBF : R;  // read-backs per batch
-        for (int j0 = t; j0 < u; j0 += NB * NT) {
-          double wj[NB];
-#pragma unroll
-          for (int k = 0; k < NB; ++k) {
-            const int jj = j0 + NT * k;
-            wj[k] = (jj < u) ? (park ? sW[jj] : wback ? a.weight[off + jj] : sA[jj]) : 0.0;
-          }
-#pragma unroll
-          for (int k = 0; k < NB; ++k) {
-            const int jj = j0 + NT * k;
-            if (jj < u) __builtin_nontemporal_store((tw > 0.0) ? wj[k] / tw : 0.0, &a.nweight[off + jj]);
-          }
-        }
+    const bool same = nxt < q.n_items && team_bin_of(q, nxt) == K;
+    int32_t m2 = -1;
+    int64_t off2 = 0;
+    int n2 = 0;
+    wide_market<NW, R, FAST, NW, true>(a, L, t, m, off, n, ps, pp, [&]() {
+      if (same) {
+        market_of(nxt, m2, off2, n2);
+        wide_load<NW, R>(a, off2, n2, t, ps, pp);
       }
+    });
+    __syncthreads();  // the item's LDS is free; the next claim is visible
+    cur = nxt;
+    nxt = sItem[slot];
+    slot ^= 1;
+    if (!same) return;
+    m = m2;
+    off = off2;
+    n = n2;
+  }
+}
+
+template <bool FAST>
+__global__ __launch_bounds__(64 * kTeamWaves) __attribute__((amdgpu_waves_per_eu(4, 8))) void consensus_wide_team_kernel(
+    ConsArgs a, WideItems q) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[team_lds_bytes<FAST>()];
+  __shared__ int sItem[2];
+  if (threadIdx.x == 0) {
+    sItem[0] = atomicAdd(&q.queue[0], 1);
+    sItem[1] = atomicAdd(&q.queue[0], 1);
+  }
+  __syncthreads();
+  int cur = sItem[0], nxt = sItem[1], slot = 0;
+  bool claiming = nxt < q.n_items;  // thread 0's: keep claiming while claims land in range
+  __syncthreads();                   // both slots read before thread 0 reuses one
+  while (cur < q.n_items) {
+    switch (team_bin_of(q, cur)) {
+      case 0: team_run<0, FAST>(a, q, smem, sItem, cur, nxt, slot, claiming); break;
+      case 1: team_run<1, FAST>(a, q, smem, sItem, cur, nxt, slot, claiming); break;
+      case 2: team_run<2, FAST>(a, q, smem, sItem, cur, nxt, slot, claiming); break;
+      case 3: team_run<3, FAST>(a, q, smem, sItem, cur, nxt, slot, claiming); break;
+      case 4: team_run<4, FAST>(a, q, smem, sItem, cur, nxt, slot, claiming); break;
+      case 5: team_run<5, FAST>(a, q, smem, sItem, cur, nxt, slot, claiming); break;
+      case 6: team_run<6, FAST>(a, q, smem, sItem, cur, nxt, slot, claiming); break;
+      default: team_run<7, FAST>(a, q, smem, sItem, cur, nxt, slot, claiming); break;
+    }
+  }
+  // every claim of this workgroup is made: the last workgroup out resets the queue
+  if (threadIdx.x == 0) {
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+    if (atomicAdd(&q.queue[1], 1) == (int)gridDim.x - 1) {
+      atomicExch(&q.queue[0], 0);
+      atomicExch(&q.queue[1], 0);
     }
   }
 }
@@ -934,6 +1138,40 @@ extern "C" int bce_debug_lane_selftest(unsigned* out, void* stream) {
 int wide_key_bits(int64_t max_len) {
   return max_len <= 128 ? 7 : max_len <= 256 ? 8 : max_len <= 512 ? 9 : max_len <= 1024 ? 10 : max_len <= 2048 ? 11
                                                                                                                  : 12;
+}
+
+// All wide bins of a plan (bins 4..11 of bce_plan_bins, 65..4096 signals) in one launch of
+// the team kernel.  a.list = the plan's order; bin_start_host = its bin boundaries.
+int launch_wide_team(const ConsArgs& a, const int64_t* bin_start_host, hipStream_t st) {
+  WideItems q{};
+  q.queue = team_queue_slot();
+  if (!q.queue) {
+    set_error("wide team kernel: no queue words on this device");
+    return BCE_EHIP;
+  }
+  int64_t items = 0;
+  for (int k = 0; k < kTeamBins; ++k) {
+    const int b = 11 - k;  // team bin k <-> plan bin 11 - k (longest first)
+    const int teams = kTeamWaves / (k <= 1 ? 8 : k <= 3 ? 4 : k == 4 ? 2 : 1);
+    q.item_start[k] = (int32_t)items;
+    q.first[k] = (int32_t)bin_start_host[b];
+    q.end[k] = (int32_t)bin_start_host[b + 1];
+    items += (bin_start_host[b + 1] - bin_start_host[b] + teams - 1) / teams;
+  }
+  q.item_start[kTeamBins] = (int32_t)items;
+  q.n_items = (int32_t)items;
+  if (items == 0) return BCE_OK;
+  BCE_REQUIRE(items < (1ll << 30), "wide team kernel: too many items");
+  const void* fn = (a.mode == BCE_MODE_FAST) ? reinterpret_cast<const void*>(&consensus_wide_team_kernel<true>)
+                                             : reinterpret_cast<const void*>(&consensus_wide_team_kernel<false>);
+  const int per_cu = blocks_per_cu(fn, 64 * kTeamWaves, 0, 1, "consensus_wide_team_kernel");
+  int64_t grid = (int64_t)cu_count() * per_cu;
+  if (grid > items) grid = items;
+  if (a.mode == BCE_MODE_FAST)
+    hipLaunchKernelGGL((consensus_wide_team_kernel<true>), dim3((int)grid), dim3(64 * kTeamWaves), 0, st, a, q);
+  else
+    hipLaunchKernelGGL((consensus_wide_team_kernel<false>), dim3((int)grid), dim3(64 * kTeamWaves), 0, st, a, q);
+  return check_launch("consensus_wide_team_kernel");
 }
 
 int launch_wide_len(int64_t max_len, const ConsArgs& a, hipStream_t st) {

@@ -729,3 +729,63 @@ def test_reestimate_mfma_out_of_range_cells_redone_exactly():
     hit = odd & ((P < 0) | (P > 1)).any(axis=0)
     assert hit.sum() > 1000
     assert np.array_equal(cf[hit], ce[hit])
+
+
+@pytest.mark.parametrize("nd", [23, 30, 100, 300, 323, -16, -100, -308])
+def test_tiebreak_every_precision_matches_python_round(nd):
+    """DeterministicTieBreaker(precision=nd) for the precisions whose 10^|nd| is not an exact
+    double (tiebreak.py:46-47,54 accept any int): the EXOTIC kernels' big-integer round()
+    against CPython's round() on random, tiny, subnormal and huge predictions, in markets of
+    every kernel's length range (lane per market, wave per market, workgroup per market).
+    All outputs bit-exact against the oracle fed Python's own round() keys."""
+    import struct
+    import torch
+    from bayesian_engine import batch
+    from oracle import oracle as orc
+    rng = np.random.default_rng(500 + nd)
+    lens = np.array([2, 5, 17, 32, 33, 48, 64, 65, 200, 31, 8] * 6, np.int64)
+    off = np.zeros(len(lens) + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    n = int(off[-1])
+    kind = rng.integers(0, 5, n)
+    pred = rng.random(n)
+    pred[kind == 1] = rng.random((kind == 1).sum()) * 10.0 ** rng.integers(-320, -5, (kind == 1).sum())
+    sub = np.nonzero(kind == 2)[0]
+    pred[sub] = [struct.unpack("<d", struct.pack("<q", int(b)))[0] for b in rng.integers(1, 1 << 52, len(sub))]
+    pred[kind == 3] = rng.random((kind == 3).sum()) * 10.0 ** rng.integers(10, 300, (kind == 3).sum())
+    pred[kind == 4] = np.round(rng.random((kind == 4).sum()) * 8) / 8.0  # forced ties
+    pred[rng.random(n) < 0.3] *= -1.0
+    if nd < 0:  # whole markets whose keys collapse to one multiple of 10^-nd
+        pred[off[3]:off[4]] = 10.0 ** (-nd) * 3.0
+    keys = np.array([round(float(p), nd) for p in pred])
+    conf, weight, rel = rng.random(n), rng.random(n), rng.random(n)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    r = batch.tiebreak(T(off), T(pred), T(conf), T(weight), T(rel), precision=nd, offsets_host=off)
+    torch.cuda.synchronize()
+    exp = orc.tiebreak_csr(off, pred, conf, weight, rel, keys=keys)
+    for k in ("winner", "label", "n_groups", "variance"):
+        assert np.array_equal(getattr(r, k).cpu().numpy(), exp[k]), (nd, k)
+    gk = r.g_key.cpu().numpy()
+    for m in range(len(lens)):
+        a, ng = int(off[m]), int(exp["n_groups"][m])
+        assert gk[a:a + ng].tobytes() == exp["g_key"][a:a + ng].tobytes(), (nd, m)
+
+
+def test_tiebreak_round_overflow_raises_like_cpython():
+    """round(1.7e308, -308) is 2e308: CPython raises OverflowError ("rounded value too large
+    to represent"); the batched tie-break raises the same error (device fault 6)."""
+    import torch
+    from bayesian_engine import batch
+    with pytest.raises(OverflowError):
+        round(1.7e308, -308)
+    off = np.array([0, 3], np.int64)
+    pred = np.array([0.5, 1.7e308, 0.25])
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    ones = np.ones(3)
+    with pytest.raises(OverflowError, match="too large"):
+        batch.tiebreak(T(off), T(pred), T(ones * 0.5), T(ones), T(ones * 0.5), precision=-308, offsets_host=off)
+    # the fault word is cleared by the check: a valid call afterwards succeeds
+    r = batch.tiebreak(T(off), T(pred[[0, 2, 0]]), T(ones * 0.5), T(ones), T(ones * 0.5), precision=-308,
+                       offsets_host=off)
+    torch.cuda.synchronize()
+    assert float(r.winner[0].item()) == 0.0
