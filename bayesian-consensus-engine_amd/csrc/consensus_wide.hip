@@ -40,6 +40,7 @@
 constexpr int kWideHR = 1;       // rounds of NT uniques whose gathers are in flight together (2: C3 fast +6%)
 constexpr int kWideWPE = 4;      // min waves per SIMD (register budget; 4 vs 2: exact -1.3%, fast unchanged)
 constexpr int kWideNWBF = 4;     // FAST nweight read-backs per batch (1: 1.645, 2: 1.634, 4: 1.587 ms C3)
+constexpr bool kWideSwz = true;  // sorted probabilities in region A rotated per thread block (below)
 
 namespace bce {
 namespace {
@@ -349,12 +350,26 @@ __device__ __forceinline__ double wave_sum_fixed(double v) {
   return (readlane_f64(v, 0) + readlane_f64(v, 16)) + (readlane_f64(v, 32) + readlane_f64(v, 48));
 }
 
+// Address of sorted position q in region A.  Thread t holds positions t*R .. t*R + R-1 after
+// the sort; written thread-major they put the R stores of a wave 8R bytes apart per lane (a
+// 4-way bank conflict on every ds_write_b128 at R = 8).  Rotating each thread's block by
+// (t >> log2(32/R)) & (R-1) -- (q >> 5) for every R -- spreads 32 consecutive lanes over all
+// 32 bank pairs for each register, so the R ds_write_b64 of the sorted probabilities are
+// conflict-free; a run of consecutive positions stays inside its blocks.  The map is a
+// bijection on [0, P), so slot j of the parked weights uses it too.
+template <int R>
+__device__ __forceinline__ int sq_addr(int q) {
+  if constexpr (kWideSwz) return (q & ~(R - 1)) | (((q & (R - 1)) + (q >> 5)) & (R - 1));
+  else return q;
+}
+
 // builtin sum() from 0 over a run of len sorted probabilities in input order (core.py:116);
 // terms past the run add +0.0, exact since the sum starts at +0.0 and is never -0.0.
-__device__ __forceinline__ double run_sum(const double* rp, int len) {
+template <int R>
+__device__ __forceinline__ double run_sum(const double* sA, int q0, int len) {
   double x[4];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) x[e] = rp[e];
+  for (int e = 0; e < 4; ++e) x[e] = sA[sq_addr<R>(q0 + e)];
   double sum = 0.0;
 #pragma unroll
   for (int e = 0; e < 4; ++e) sum += (e < len) ? x[e] : 0.0;
@@ -362,11 +377,11 @@ __device__ __forceinline__ double run_sum(const double* rp, int len) {
     int e0 = 4;
     double xa[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) xa[e] = rp[e0 + e];
+    for (int e = 0; e < 8; ++e) xa[e] = sA[sq_addr<R>(q0 + e0 + e)];
     for (; e0 + 8 <= len; e0 += 8) {
       double xb[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) xb[e] = rp[e0 + 8 + e];
+      for (int e = 0; e < 8; ++e) xb[e] = sA[sq_addr<R>(q0 + e0 + 8 + e)];
 #pragma unroll
       for (int e = 0; e < 8; ++e) sum += xa[e];
 #pragma unroll
@@ -584,9 +599,14 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
   const int incl = wave_incl_scan(cnt);
   if (lane == 63) L.sCnt[wv] = incl;
   team_sync<NW, TEAM>();  // (b) every read of the input-order probs done; counts visible
+  if constexpr (kWideSwz) {
 #pragma unroll
-  for (int r = 0; r < R; r += 2)
-    *reinterpret_cast<double2*>(sA + t * R + r) = make_double2(x[r], x[r + 1]);
+    for (int r = 0; r < R; ++r) sA[sq_addr<R>(t * R + r)] = x[r];
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; r += 2)
+      *reinterpret_cast<double2*>(sA + t * R + r) = make_double2(x[r], x[r + 1]);
+  }
   int base = incl - cnt, u = 0;
 #pragma unroll
   for (int w = 0; w < NW; ++w) {
@@ -665,7 +685,7 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
           const int jj = (h + i) * NP + pt;
           vw[i] = va[i] = vc[i] = 0.0;
           if (jj < u) {
-            const double avg = run_sum(sA + q0s[i], q1s[i] - q0s[i]);  // core.py:116
+            const double avg = run_sum<R>(sA, q0s[i], q1s[i] - q0s[i]);  // core.py:116
             const double w = rc[i].x;  // core.py:111,119
             vw[i] = w;
             va[i] = avg * w;        // core.py:136
@@ -741,19 +761,19 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
       if constexpr (FAST) {
         // runs longer than kWaveRun (hot sources) are summed by the whole wave in a fixed
         // order instead of by their own lane, so one hot source does not hold the wave
-        avg = (jj < u && len <= kWaveRun) ? run_sum(sA + q0s[i], len) : 0.0;
+        avg = (jj < u && len <= kWaveRun) ? run_sum<R>(sA, q0s[i], len) : 0.0;
         unsigned long long lm = ballot(jj < u && len > kWaveRun);
         while (lm) {
           const int LL = __builtin_ctzll(lm);
           lm &= lm - 1;
           const int lq0 = __builtin_amdgcn_readlane(q0s[i], LL), llen = __builtin_amdgcn_readlane(len, LL);
           double part = 0.0;
-          for (int e = lane; e < llen; e += 64) part += sA[lq0 + e];
+          for (int e = lane; e < llen; e += 64) part += sA[sq_addr<R>(lq0 + e)];
           part = wave_sum_fixed(part);
           if (lane == LL) avg = part / (double)llen;
         }
       } else if (jj < u) {
-        avg = run_sum(sA + q0s[i], len);
+        avg = run_sum<R>(sA, q0s[i], len);
       }
       vw[i] = va[i] = vc[i] = 0.0;
       if (jj < u) {
@@ -775,7 +795,7 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
 #pragma unroll
         for (int i = 0; i < HR; ++i) {
           const int jj = (h + i) * NT + t;
-          if (jj < u) sA[jj] = vw[i];  // later groups read only slots > jj
+          if (jj < u) sA[sq_addr<R>(jj)] = vw[i];  // later groups read only positions > jj
         }
       }
     } else {
@@ -788,7 +808,7 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
           buf[2 * NT + t] = vc[i];
           team_sync<NW, TEAM>();  // round staged; every sorted-prob read of this group is done
           const int jj = (h + i) * NT + t;
-          if (jj < u && !wback) sA[jj] = vw[i];  // slot jj is only read by uniques <= jj
+          if (jj < u && !wback) sA[sq_addr<R>(jj)] = vw[i];  // position jj is only read by uniques <= jj
           if (wv == 0) {
             __builtin_amdgcn_s_setprio(2);  // the chain is the critical path
             const int ce = (u - (h + i) * NT < NT) ? u - (h + i) * NT : NT;
@@ -853,7 +873,7 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
 #pragma unroll
       for (int k = 0; k < R; ++k) {
         const int jj = t + NT * k;
-        wj[k] = (jj < u) ? (wback ? a.weight[off + jj] : sA[jj]) : 0.0;
+        wj[k] = (jj < u) ? (wback ? a.weight[off + jj] : sA[sq_addr<R>(jj)]) : 0.0;
       }
 #pragma unroll
       for (int k = 0; k < R; ++k) {
@@ -867,7 +887,7 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
 #pragma unroll
         for (int k = 0; k < NB; ++k) {
           const int jj = j0 + NT * k;
-          wj[k] = (jj < u) ? (park ? sW[jj] : wback ? a.weight[off + jj] : sA[jj]) : 0.0;
+          wj[k] = (jj < u) ? (park ? sW[jj] : wback ? a.weight[off + jj] : sA[sq_addr<R>(jj)]) : 0.0;
         }
 #pragma unroll
         for (int k = 0; k < NB; ++k) {

@@ -500,13 +500,20 @@ def test_tiebreak_any_precision_vs_python_round(precision):
     _tb_check(r, exp, off)
 
 
-def test_tiebreak_unsupported_precision_raises():
+def test_tiebreak_precision_30_is_supported():
+    """precision=30 (10^30 is not a double) used to return BCE_EUNSUPPORTED; it now runs the
+    exact big-integer round() like every other int precision (tiebreak.py:46-47,54)."""
     import torch
-    from bayesian_engine import _native as N, batch
+    from bayesian_engine import batch
     off, pred, conf, weight, rel = _tb_inputs(np.array([5, 6], np.int64), 3)
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
-    with pytest.raises(N.BCEError, match="precision 30"):
-        batch.tiebreak(T(off), T(pred), T(conf), T(weight), T(rel), precision=30, offsets_host=off)
+    r = batch.tiebreak(T(off), T(pred), T(conf), T(weight), T(rel), precision=30, offsets_host=off)
+    torch.cuda.synchronize()
+    gk = r.g_key.cpu().numpy()
+    for m in range(2):
+        a = int(off[m])
+        first = round(float(pred[a]), 30)
+        assert gk[a] == first
 
 
 def test_tiebreak_markets_longer_than_4096_vs_oracle():

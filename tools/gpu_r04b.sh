@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round 4: the all-bins team kernel for C3 -- wide/consensus/drop-in parity (incl. the new
-# exotic-precision tie-break tests), then C3 A/B (team vs one launch per bin) and the 8-shard
-# strong-scaling prediction with each.
+# Round 4: the all-bins team kernel for C3 + the rotated sorted-probability layout -- wide /
+# consensus / drop-in parity, C3 A/B (team vs one launch per bin), the 8-shard strong-scaling
+# prediction with each, a kernel trace, and the layout A/B (parity-gated harness).
 set -u
 o=gpurun_out/r04b
 mkdir -p $o
@@ -13,4 +13,5 @@ BCE_WIDE_TEAM=0 timeout -k 10 200 python3 bench.py --config c3 --steps 30 --warm
 timeout -k 10 200 python3 bench.py --config c3 --shard all/8 --steps 30 --warmup 5 > $o/c3_shards_team.json 2> $o/c3_shards_team.err && \
 BCE_WIDE_TEAM=0 timeout -k 10 200 python3 bench.py --config c3 --shard all/8 --steps 30 --warmup 5 > $o/c3_shards_bins.json 2> $o/c3_shards_bins.err && \
 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $o/prof -o run --output-format csv -- \
-  python3 bench.py --config c3 --steps 20 --warmup 3 --no-cpu-baseline --no-parity > $o/prof.log 2>&1
+  python3 bench.py --config c3 --steps 20 --warmup 3 --no-cpu-baseline --no-parity > $o/prof.log 2>&1 && \
+timeout -k 10 400 python3 tools/wide_variants.py run wbase wnoswz --modes fast,exact --reps 20 > $o/swz_ab.txt 2>&1

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Experiment harness (not product code): build variants of libbce_hip.so as SOURCE PATCHES of
 csrc/ (the product source carries no experiment switches) and time them on the config-2
-workload.
+workload.  Every timed variant is checked against the C restatement (all eight outputs, bit
+for bit) before its time is printed: a variant that computes something else prints
+{"parity": false} and no time, and the run stops.
 
   python tools/tab_variants.py build [names...]     # here (hipcc cross-compiles)
   python tools/tab_variants.py run [--rounds 3]      # on the GPU box: one process per variant
@@ -117,9 +119,16 @@ def one(name, reps):
         e1.record()
     torch.cuda.synchronize()
     ms = sorted(a.elapsed_time(b) for a, b in ev)
-    out = {"variant": name, "median_ms": ms[len(ms) // 2], "min_ms": ms[0]}
     if os.environ.get("TAB_NOCHECK") is None:
         N.check_faults()
+    # parity gate: a variant whose outputs differ from the restatement prints no time
+    from bench import cpu_consensus_threaded, host_threads, parity_all_outputs
+    cpu = cpu_consensus_threaded(off, sid, prob, rel, conf, present, host_threads())
+    ok = parity_all_outputs(res, cpu, off, True)
+    if not all(ok.values()):
+        print(json.dumps({"variant": name, "parity": False, "outputs": ok}), flush=True)
+        raise SystemExit(3)
+    out = {"variant": name, "parity": True, "median_ms": ms[len(ms) // 2], "min_ms": ms[0]}
     print(json.dumps(out), flush=True)
 
 
