@@ -51,6 +51,13 @@ _SIGS = {
     "bce_debug_lane_selftest": (C.c_int, [_vp, _vp]),
     "bce_debug_py_round": (_f64, [_f64, _i32, _vp]),
     "bce_debug_set_wide_team": (C.c_int, [C.c_int]),
+    "bce_jsonl_parse": (C.c_int, [_vp, _i64, _i32, _vp]),
+    "bce_jsonl_counts": (C.c_int, [_vp, _vp]),
+    "bce_jsonl_arrays": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "bce_jsonl_render": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _vp,
+                                   _vp, _vp, _vp]),
+    "bce_jsonl_free": (None, [_vp]),
+    "bce_debug_float_repr": (_i32, [_f64, _vp, _i32]),
     "bce_consensus_csr": (C.c_int, [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _i32, _vp, _i64, _i32,
                                     _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "bce_table_pack": (C.c_int, [_i64, _vp, _vp, _vp, _vp, _vp, _vp]),

@@ -73,17 +73,35 @@ def _consensus(args: argparse.Namespace, use_store: bool) -> None:
 
 
 def _consensus_batch(args: argparse.Namespace) -> None:
-    from .jsonl import consensus_jsonl
-
     if args.input:
         with open(args.input, "r", encoding="utf-8") as fh:
             lines = fh.readlines()
     else:
         lines = sys.stdin.readlines()
+    # the native front end (csrc/jsonl.cpp) renders every result; runs of results go to
+    # stdout as bytes (they are ASCII: ids are \u-escaped), error lines through print() in
+    # line order, as the per-line loop would write them
+    from .jsonl import _consensus_jsonl_native
+
+    texts, _ = _consensus_jsonl_native([ln for ln in lines if ln.strip()], None, dry_run=args.dry_run,
+                                       mode="exact")
     failed = False
-    for ok, text in consensus_jsonl(lines, dry_run=args.dry_run):
-        print(text, file=sys.stdout if ok else sys.stderr)
-        failed = failed or not ok
+    run: list = []
+    for ok, text in texts:
+        if ok:
+            run.append(text)
+            continue
+        if run:
+            sys.stdout.flush()
+            sys.stdout.buffer.write(b"\n".join(run) + b"\n")
+            sys.stdout.buffer.flush()
+            run = []
+        print(text.decode("utf-8", "surrogatepass"), file=sys.stderr)
+        failed = True
+    if run:
+        sys.stdout.flush()
+        sys.stdout.buffer.write(b"\n".join(run) + b"\n")
+        sys.stdout.buffer.flush()
     if failed:
         raise SystemExit(1)
 

@@ -31,7 +31,7 @@ from . import batch
 from .config import DEFAULT_CONFIDENCE, DEFAULT_RELIABILITY, SCHEMA_VERSION
 from .core import ValidationError, _as_float, _check_number, _no_signals, check_structure
 
-__all__ = ["consensus_many", "consensus_jsonl", "parse_batch", "render"]
+__all__ = ["consensus_many", "consensus_jsonl", "consensus_jsonl_bytes", "parse_batch", "render"]
 
 _INF = float("inf")
 _TOP = ["schemaVersion", "consensus", "confidence", "sourceWeights", "normalization", "diagnostics"]
@@ -199,10 +199,196 @@ def parse_batch(lines: Iterable[str]) -> Tuple[List[Any], List[Optional[str]], L
 
 
 def consensus_jsonl(lines: Iterable[str], source_reliability: Optional[dict] = None, *,
-                    dry_run: bool = False, mode: str = "exact") -> List[Tuple[bool, str]]:
+                    dry_run: bool = False, mode: str = "exact", native: bool = True) -> List[Tuple[bool, str]]:
     """One ``(ok, text)`` per non-blank JSONL line: ``text`` is what ``bayesian-engine
     consensus`` prints for that payload alone -- the ``json.dumps(indent=2)`` result on
-    success, the ``Validation error: ...`` line otherwise (cli.py:46-52)."""
+    success, the ``Validation error: ...`` line otherwise (cli.py:46-52).
+
+    ``native`` (default): parsing, structure checks, interning and rendering run in the
+    library's C++ front end on host threads (csrc/jsonl.cpp); a line it does not reproduce
+    exactly (malformed JSON, a non-object payload, a non-string schemaVersion, a line with
+    an embedded newline) goes through the Python path below on its own.  Both paths give
+    byte-identical texts."""
+    lines = [ln for ln in lines if ln.strip()]  # parse_batch skips blank lines
+    if not native:
+        return _consensus_jsonl_py(lines, source_reliability, dry_run=dry_run, mode=mode)
+    texts, _ = _consensus_jsonl_native(lines, source_reliability, dry_run=dry_run, mode=mode)
+    return [(bool(ok), t.decode("utf-8", "surrogatepass")) for ok, t in texts]
+
+
+def consensus_jsonl_bytes(lines: Sequence[str], source_reliability: Optional[dict] = None, *,
+                          dry_run: bool = False, mode: str = "exact") -> Tuple[bytes, bytes, bool]:
+    """What ``consensus-batch`` writes: (stdout bytes, stderr bytes, any line failed) -- each
+    text plus a newline, in line order, without building a Python string per result."""
+    lines = [ln for ln in lines if ln.strip()]
+    texts, _ = _consensus_jsonl_native(lines, source_reliability, dry_run=dry_run, mode=mode)
+    out = b"".join(t + b"\n" for ok, t in texts if ok)
+    err = b"".join(t + b"\n" for ok, t in texts if not ok)
+    return out, err, len(err) > 0
+
+
+def _threads() -> int:
+    import os
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+class _NativeBatch:
+    """A parsed batch (bce_jsonl_parse) and its arrays on the host."""
+
+    def __init__(self, text: bytes, threads: int):
+        import ctypes as C
+        self._L = N.lib()
+        h = C.c_void_p()
+        N.check(self._L.bce_jsonl_parse(text, len(text), threads, C.byref(h)), "bce_jsonl_parse")
+        self.h = h
+        cnt = np.zeros(4, np.int64)
+        N.check(self._L.bce_jsonl_counts(h, N.ptr(cnt)), "bce_jsonl_counts")
+        nl, nv, nn, nb = (int(x) for x in cnt)
+        self.kind = np.empty(nl, np.int32)
+        self.type_err = np.empty(nl, np.int32)
+        self.n_signals = np.empty(nl, np.int32)
+        self.voff = np.empty(nl + 1, np.int64)
+        self.prob = np.empty(max(nv, 1), np.float64)
+        self.sid = np.empty(max(nv, 1), np.int32)
+        self._names = np.empty(max(nb, 1), np.uint8)
+        self.name_off = np.empty(nn + 1, np.int64)
+        N.check(self._L.bce_jsonl_arrays(h, N.ptr(self.kind), N.ptr(self.type_err), N.ptr(self.n_signals), None,
+                                         N.ptr(self.voff), N.ptr(self.prob), N.ptr(self.sid), N.ptr(self._names),
+                                         N.ptr(self.name_off)), "bce_jsonl_arrays")
+        self.n_lines, self.n_checked, self.n_names = nl, nv, nn
+
+    def names(self) -> List[str]:
+        raw, o = self._names.tobytes(), self.name_off.tolist()
+        return [raw[o[i]:o[i + 1]].decode("utf-8", "surrogatepass") for i in range(self.n_names)]
+
+    def __del__(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            self._L.bce_jsonl_free(self.h)
+            self.h = None
+
+
+def _weight_texts(nb: "_NativeBatch", sr: dict, used: np.ndarray):
+    """Per interned name: json.dumps of its weight object (reliability, or the default 0.5 --
+    an int stays an int, core.py:111,119), and the host table rows; the reference's
+    TypeError for a non-numeric value of a name some computed market uses."""
+    S = nb.n_names
+    if not sr:
+        return (b"0.5" * S, np.arange(S + 1, dtype=np.int64) * 3, np.full(S, DEFAULT_RELIABILITY),
+                np.full(S, DEFAULT_CONFIDENCE), np.zeros(S, np.uint8), None)
+    names = nb.names()
+    rel, conf, present = np.empty(S), np.empty(S), np.zeros(S, np.uint8)
+    parts = []
+    usedset = set(used.tolist())
+    for i, n in enumerate(names):
+        d = sr.get(n, {})
+        r = d.get("reliability", DEFAULT_RELIABILITY)
+        c = d.get("confidence", DEFAULT_CONFIDENCE)
+        if i in usedset:
+            _check_number(r, None)
+            if not isinstance(c, (int, float)):
+                c * r  # noqa: B018  -- the reference's TypeError at core.py:142
+        ok_r, ok_c = isinstance(r, (int, float)), isinstance(c, (int, float))
+        rel[i] = _as_float(r) if ok_r else DEFAULT_RELIABILITY
+        conf[i] = _as_float(c) if ok_c else DEFAULT_CONFIDENCE
+        present[i] = n in sr
+        parts.append(_num(r).encode() if ok_r else b"null")
+    off = np.zeros(S + 1, np.int64)
+    np.cumsum([len(x) for x in parts], out=off[1:])
+    return b"".join(parts), off, rel, conf, present, names
+
+
+def _consensus_jsonl_native(lines: List[str], source_reliability: Optional[dict], *, dry_run: bool,
+                            mode: str) -> Tuple[List[Tuple[bool, bytes]], int]:
+    """The native front end over `lines` (non-blank); returns ((ok, text bytes) per line,
+    number of lines the Python path handled)."""
+    import ctypes as C
+    M = len(lines)
+    if M == 0:
+        return [], 0
+    bodies, py_idx = [], []
+    for i, ln in enumerate(lines):
+        b = ln[:-1] if ln.endswith("\n") else ln
+        if "\n" in b:
+            py_idx.append(i)  # a payload spanning lines: json.loads of the whole string
+        else:
+            bodies.append(b)
+    skip = set(py_idx)
+    nat_idx = [i for i in range(M) if i not in skip] if skip else list(range(M))
+    text = "\n".join(bodies).encode("utf-8", "surrogatepass")
+    T = _threads()
+    nb = _NativeBatch(text, T)
+    if nb.n_lines != len(bodies):
+        raise RuntimeError(f"bce_jsonl_parse split {nb.n_lines} lines, expected {len(bodies)}")
+    L = nb.n_lines
+    err = np.full(L, -1, np.int32)
+    if nb.n_checked > 0:  # one range-check launch for the whole batch (core.py:59-60)
+        N.require_gpu()
+        dev = N.device()
+        err = batch.validate(torch.from_numpy(nb.voff).to(dev),
+                             torch.from_numpy(nb.prob[:nb.n_checked]).to(dev)).cpu().numpy().astype(np.int32)
+    rows = np.nonzero((nb.kind == 0) & (err < 0) & (nb.type_err < 0) & (nb.n_signals > 0))[0]
+    res_of = np.full(L, -1, np.int64)
+    res_of[rows] = np.arange(len(rows))
+    lens = (nb.voff[rows + 1] - nb.voff[rows]).astype(np.int64)
+    roff = np.zeros(len(rows) + 1, np.int64)
+    np.cumsum(lens, out=roff[1:])
+    Ns = int(roff[-1])
+    flat = np.repeat(nb.voff[rows] - roff[:-1], lens) + np.arange(Ns, dtype=np.int64)
+    sid = nb.sid[flat] if Ns else np.zeros(1, np.int32)
+    sr = source_reliability or {}
+    wtext, wtext_off, rel, conf, present, names = _weight_texts(nb, sr, np.unique(sid[:Ns]) if Ns else sid[:0])
+    R = len(rows)
+    f64, i32 = np.float64, np.int32
+    cons, confd, total = np.zeros(max(R, 1), f64), np.zeros(max(R, 1), f64), np.zeros(max(R, 1), f64)
+    nu = np.zeros(max(R, 1), i32)
+    usid, nweight = np.zeros(max(Ns, 1), i32), np.zeros(max(Ns, 1), f64)
+    if R:
+        N.require_gpu()
+        dev = N.device()
+        Tt = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+        table = batch.SourceTable.from_arrays(Tt(rel), Tt(conf), Tt(present), names)
+        max_len = int(lens.max())
+        plan = None if max_len <= 64 else batch.Plan.build(roff, dev)
+        res = batch.consensus(Tt(roff), Tt(sid[:Ns]), Tt(nb.prob[flat]), table, plan=plan,
+                              max_len=max_len if plan is None else None, mode=mode, validate=False, check=True)
+        cons, confd, total = res.consensus.cpu().numpy(), res.confidence.cpu().numpy(), res.total_weight.cpu().numpy()
+        nu = res.n_unique.cpu().numpy()
+        usid, nweight = res.usid[:Ns].cpu().numpy(), res.nweight[:Ns].cpu().numpy()
+    wt = np.frombuffer(wtext, np.uint8) if wtext else np.zeros(1, np.uint8)
+    n_bytes = C.c_int64(0)
+    args = [nb.h, N.ptr(err), N.ptr(res_of), N.ptr(cons), N.ptr(confd), N.ptr(total), N.ptr(nu), N.ptr(roff),
+            N.ptr(usid), N.ptr(nweight), N.ptr(wt), N.ptr(wtext_off), int(bool(dry_run)), T]
+    N.check(nb._L.bce_jsonl_render(*args, None, None, None, C.byref(n_bytes)), "bce_jsonl_render")
+    buf = np.empty(max(n_bytes.value, 1), np.uint8)
+    toff = np.empty(L + 1, np.int64)
+    okf = np.empty(max(L, 1), np.uint8)
+    N.check(nb._L.bce_jsonl_render(*args, N.ptr(buf), N.ptr(toff), N.ptr(okf), C.byref(n_bytes)),
+            "bce_jsonl_render")
+    raw = buf.tobytes()
+    to = toff.tolist()
+    out: List[Optional[Tuple[bool, bytes]]] = [None] * M
+    fb = []
+    for j, i in enumerate(nat_idx):
+        if nb.kind[j] == 2:
+            fb.append(i)
+        else:
+            out[i] = (bool(okf[j]), raw[to[j]:to[j + 1]])
+    py = sorted(fb + py_idx)
+    if py:  # lines the native parser hands over: the Python path, on their own
+        for i, (ok, t) in zip(py, _consensus_jsonl_py([lines[i] for i in py], source_reliability,
+                                                      dry_run=dry_run, mode=mode)):
+            out[i] = (ok, t.encode("utf-8", "surrogatepass"))
+    return out, len(py)
+
+
+def _consensus_jsonl_py(lines: Iterable[str], source_reliability: Optional[dict] = None, *,
+                        dry_run: bool = False, mode: str = "exact") -> List[Tuple[bool, str]]:
+    """The Python path: json.loads + check_structure per line, one validation launch, one
+    consensus launch (consensus_many), render per result."""
     payloads, errors, probs, type_errors = parse_batch(lines)
     M = len(payloads)
     lens = np.fromiter((len(p) for p in probs), np.int64, M)

@@ -367,6 +367,10 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
       }
     }
     oem_sort_kv(u, kp);
+    // every member carries its run head's key: a group's dict key is its FIRST member's
+    // rounded prediction (tiebreak.py:54-55), and -0.0 / 0.0 share a group with different bits
+#pragma unroll
+    for (int p = 1; p < kTbLpmMax; ++p) kp[p] = run_start(u, p) ? kp[p] : kp[p - 1];
 
     // ---- 2. group keys and counts (registers only) ------------------------------------------
     if (a.g_key || a.g_count) {

@@ -304,6 +304,38 @@ int bce_reestimate_consensus_votes_mfma(const double* P, int64_t A, int64_t M, i
                                         int64_t scratch_bytes, void* stream);
 int64_t bce_reestimate_mfma_scratch_bytes(int64_t M);
 
+/* ---- JSONL front end (host C++, no GPU): SURVEY §8 f2 -----------------------------------
+ *
+ * Replaces, for a batch: cli._cmd_consensus_legacy / _cmd_consensus (cli.py:25-52,163-174)
+ * per payload = json.load + core.validate_input_payload (core.py:24-60) + the result's
+ * json.dumps(indent=2).  bce_jsonl_parse splits `text` (UTF-8; lone surrogates as 3-byte
+ * sequences) on '\n', parses each non-blank line as CPython's json.loads would and runs
+ * check_structure (core.py:34-58) with the reference's messages; lines it cannot restate
+ * exactly get kind 2 (the caller's Python path handles them).  sourceIds of every checked
+ * signal are interned over the batch in code-point order.  bce_jsonl_counts: [lines, checked
+ * probabilities, names, name bytes].  bce_jsonl_arrays: per line kind (0 structure ok, 1 header
+ * error, 2 hand over), first type-error index (-1), len(signals), byte span (2 x int64); the
+ * CSR voff [L+1] of the checked probabilities (those before a line's first type error), their
+ * values and sourceId ranks; the sorted names (bytes + [N+1] offsets).  NULL outputs skipped.
+ * bce_jsonl_render: after the caller's range check (err_idx per line, bce_validate_csr) and
+ * consensus launch over the computed lines (res_of: line -> row or -1; res_off: row -> CSR
+ * start of its per-unique outputs; usid / nweight as bce_consensus_* writes them), every
+ * line's text: "Validation error: ..." or json.dumps(result, indent=2) byte for byte (wtext:
+ * per name, the JSON text of its weight object).  Call with out == NULL to render and size,
+ * then with buffers to copy (text_off [L+1], ok [L]).  `threads` host threads. */
+int bce_jsonl_parse(const char* text, int64_t len, int32_t threads, void** handle);
+int bce_jsonl_counts(void* handle, int64_t* counts);
+int bce_jsonl_arrays(void* handle, int32_t* kind, int32_t* type_err, int32_t* n_signals, int64_t* span,
+                     int64_t* voff, double* prob, int32_t* sid, char* names, int64_t* name_off);
+int bce_jsonl_render(void* handle, const int32_t* err_idx, const int64_t* res_of, const double* consensus,
+                     const double* confidence, const double* total_weight, const int32_t* n_unique,
+                     const int64_t* res_off, const int32_t* usid, const double* nweight, const char* wtext,
+                     const int64_t* wtext_off, int32_t dry_run, int32_t threads, char* out, int64_t* text_off,
+                     uint8_t* ok, int64_t* n_bytes);
+void bce_jsonl_free(void* handle);
+/* Test hook: float.__repr__ of x (the renderer's number format) into buf; returns its length. */
+int32_t bce_debug_float_repr(double x, char* buf, int32_t cap);
+
 #ifdef __cplusplus
 }
 #endif

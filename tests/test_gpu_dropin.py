@@ -796,3 +796,36 @@ def test_tiebreak_round_overflow_raises_like_cpython():
                        offsets_host=off)
     torch.cuda.synchronize()
     assert float(r.winner[0].item()) == 0.0
+
+
+@pytest.mark.parametrize("n_agents", [3, 40, 100])
+def test_tiebreak_signed_zero_group_key_is_first_member(n_agents):
+    """round(-1e-9, 6) is -0.0 and round(1e-9, 6) is 0.0: one dict slot (== compares them
+    equal) whose key is the FIRST member's (tiebreak.py:54-55).  Every kernel (lane, wave and
+    workgroup per market) reports that key's sign for the group and the winner."""
+    import struct
+    import torch
+    from bayesian_engine import batch
+    from oracle import oracle as orc
+    rng = np.random.default_rng(n_agents)
+    markets = []
+    for first in (-1e-9, 1e-9, -0.0, 0.0):
+        p = list(rng.choice([1e-9, -1e-9, 0.0, -0.0, 2e-9], n_agents - 1)) + []
+        markets.append([first] + p)
+    lens = np.array([len(m) for m in markets], np.int64)
+    off = np.zeros(len(lens) + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    pred = np.concatenate(markets)
+    n = len(pred)
+    conf, weight, rel = rng.random(n), np.ones(n), np.ones(n)  # one group: it must win
+    keys = np.array([round(float(p), 6) for p in pred])
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    r = batch.tiebreak(T(off), T(pred), T(conf), T(weight), T(rel), precision=6, offsets_host=off)
+    torch.cuda.synchronize()
+    exp = orc.tiebreak_csr(off, pred, conf, weight, rel, keys=keys)
+    sign = lambda x: struct.pack("<d", float(x))[7] >> 7  # noqa: E731
+    gk, win = r.g_key.cpu().numpy(), r.winner.cpu().numpy()
+    for m in range(len(markets)):
+        a = int(off[m])
+        assert sign(gk[a]) == sign(keys[a]) == sign(exp["g_key"][a]), (m, gk[a], keys[a])
+        assert sign(win[m]) == sign(exp["winner"][m]), (m, win[m], exp["winner"][m])
