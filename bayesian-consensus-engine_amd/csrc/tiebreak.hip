@@ -219,6 +219,8 @@ __global__ __launch_bounds__(256) void tiebreak_wave_kernel(TbArgs a, const int3
 constexpr int kTbLpmMax = 32;
 constexpr int kTbLpmWaves = 4;
 constexpr int kTbStage = 64 * kTbLpmMax + 64;  // doubles per wave buffer: a tile's agents + pads
+constexpr int kTbStageIt = 64 * kTbLpmMax / 128;  // 16-B loads per lane for a full tile
+constexpr int kTbStageBatch = 4;                  // of them in flight together (2 x 8 VGPRs each)
 
 __device__ __forceinline__ int tb_pad(int i) { return i + (i >> 5); }
 
@@ -273,18 +275,48 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     const int last = n > 0 ? n - 1 : 0;
     const int rbase = n > 0 ? lrow : 0;
     const int64_t gbase = n > 0 ? off : B;
-    // global [B, E) -> LDS (padded), coalesced 16-B loads
+    // global [B, E) -> LDS (padded), coalesced 16-B loads issued kTbStageBatch at a time
+    // before any is written to LDS: one memory round trip per batch, not one per load (the
+    // per-iteration loop paid ~16 serial HBM latencies per array and tile)
     auto stage = [&](const double* src) {
       wave_sync_lds();  // the buffer's previous readers (this wave) are done
-      const bool al = ((uintptr_t)(src + B) & 15) == 0;
-      for (int e = 2 * lane; e < cnt_tile; e += 128) {
-        if (al && e + 1 < cnt_tile) {
-          const double2 v = *reinterpret_cast<const double2*>(src + B + e);
-          buf[tb_pad(e)] = v.x;
-          buf[tb_pad(e + 1)] = v.y;
-        } else {
-          buf[tb_pad(e)] = src[B + e];
-          if (e + 1 < cnt_tile) buf[tb_pad(e + 1)] = src[B + e + 1];
+      if (((uintptr_t)(src + B) & 15) == 0) {
+#pragma unroll 1
+        for (int k0 = 0; k0 < kTbStageIt; k0 += kTbStageBatch) {
+          if (k0 * 128 >= cnt_tile) break;  // wave-uniform
+          double2 v[kTbStageBatch];
+#pragma unroll
+          for (int k = 0; k < kTbStageBatch; ++k) {
+            const int e = 2 * lane + 128 * (k0 + k);
+            v[k] = make_double2(0.0, 0.0);
+            if (e + 1 < cnt_tile) v[k] = *reinterpret_cast<const double2*>(src + B + e);
+          }
+#pragma unroll
+          for (int k = 0; k < kTbStageBatch; ++k) {
+            const int e = 2 * lane + 128 * (k0 + k);
+            if (e + 1 < cnt_tile) {
+              buf[tb_pad(e)] = v[k].x;
+              buf[tb_pad(e + 1)] = v[k].y;
+            }
+          }
+        }
+        if ((cnt_tile & 1) && lane == 0) buf[tb_pad(cnt_tile - 1)] = src[B + cnt_tile - 1];  // odd tail
+      } else {
+#pragma unroll 1
+        for (int k0 = 0; k0 < 2 * kTbStageIt; k0 += 2 * kTbStageBatch) {
+          if (k0 * 64 >= cnt_tile) break;  // wave-uniform
+          double v[2 * kTbStageBatch];
+#pragma unroll
+          for (int k = 0; k < 2 * kTbStageBatch; ++k) {
+            const int e = lane + 64 * (k0 + k);
+            v[k] = 0.0;
+            if (e < cnt_tile) v[k] = src[B + e];
+          }
+#pragma unroll
+          for (int k = 0; k < 2 * kTbStageBatch; ++k) {
+            const int e = lane + 64 * (k0 + k);
+            if (e < cnt_tile) buf[tb_pad(e)] = v[k];
+          }
         }
       }
       wave_sync_lds();

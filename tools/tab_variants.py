@@ -25,6 +25,7 @@ CSRC = os.path.join(ROOT, "bayesian-consensus-engine_amd", "csrc")
 OUT = os.path.join(ROOT, "tools", "ablate_build")
 SRCS = ["capi.hip", "consensus.hip", "consensus_tab.hip", "consensus_wide.hip", "elementwise.hip", "tiebreak.hip",
         "stats.hip", "aggregate.hip"]
+CPP_SRCS = ["jsonl.cpp"]
 
 _XPOSE_NEW = """  for (int i = 0; i < N; ++i)
     if (!(i & 4)) bfly_r8(r[i], r[i | 4], lane);
@@ -89,7 +90,12 @@ def build(names, variants=None):
             if p.wait() != 0:
                 raise SystemExit(f"build of {name} failed")
         procs = []
-        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o",
+        for fn in CPP_SRCS:  # host-only C++ (the JSONL front end)
+            o = os.path.join(d, fn.replace(".cpp", ".o"))
+            objs.append(o)
+            subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-pthread", "-D__HIP_PLATFORM_AMD__",
+                            "-I/opt/rocm/include", "-w", "-I", src, "-c", os.path.join(src, fn), "-o", o], check=True)
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-pthread", "-o",
                         os.path.join(d, "libbce_hip.so"), *objs], check=True)
         print("built", name, flush=True)
 

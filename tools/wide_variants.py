@@ -33,6 +33,30 @@ VARIANTS = {
     "wbase": [],
     # round-3 thread-major sorted-probability layout (4-way conflicts on the step-3 stores)
     "wnoswz": [("consensus_wide.hip", "constexpr bool kWideSwz = true;", "constexpr bool kWideSwz = false;")],
+    # (thread-major layout) the short-market side-stream kernels launched after the team kernel
+    "tafter": [("consensus_wide.hip", "constexpr bool kWideSwz = true;", "constexpr bool kWideSwz = false;"),
+               ("consensus.hip", """  if (team) {
+    for (int b = 0; b <= side_last && !rc; ++b) {""", """  if (team) {
+    if (!rc) {
+      ConsArgs a = base;
+      a.list = order;
+      a.n_list = bin_start_host[BCE_NBINS - 1] - bin_start_host[kPlanSideLast + 1];
+      rc = launch_wide_team(a, bin_start_host, st);
+    }
+    for (int b = 0; b <= side_last && !rc; ++b) {"""),
+               ("consensus.hip", """      rc = seg_ok ? launch_seg_for_len(lens[b], a, side) : launch_long_lds(a, side);
+    }
+    if (!rc) {
+      ConsArgs a = base;
+      a.list = order;
+      a.n_list = bin_start_host[BCE_NBINS - 1] - bin_start_host[kPlanSideLast + 1];
+      rc = launch_wide_team(a, bin_start_host, st);
+    }""", """      rc = seg_ok ? launch_seg_for_len(lens[b], a, side) : launch_long_lds(a, side);
+    }""")],
+    # (thread-major layout) the team kernel one workgroup short per two CUs (room for the side stream)
+    "tless": [("consensus_wide.hip", "constexpr bool kWideSwz = true;", "constexpr bool kWideSwz = false;"),
+              ("consensus_wide.hip", "  int64_t grid = (int64_t)cu_count() * per_cu;\n  if (grid > items) grid = items;",
+               "  int64_t grid = (int64_t)cu_count() * per_cu - cu_count() / 2;\n  if (grid > items) grid = items;")],
     # ---- ablations (timing only; outputs are wrong by construction -- no parity gate) ----
     # the sort network run twice (the second pass on sorted keys costs the same)
     "xsort2": [("consensus_wide.hip", "  wide_sort<NN, NW, R>(key, sX, t, lane);\n",
