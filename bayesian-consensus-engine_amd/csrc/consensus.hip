@@ -1725,13 +1725,14 @@ extern "C" int64_t bce_consensus_scratch_bytes(const int64_t* offsets_host, cons
   return (int64_t)grid * 4 * next_pow2(mx) * 8;
 }
 
-// BCE_WIDE_TEAM=0 in the environment, or bce_debug_set_wide_team(0), selects one launch per
-// wide bin instead of the team kernel (A/B and parity tests of the two paths).
+// BCE_WIDE_TEAM=1 in the environment, or bce_debug_set_wide_team(1), selects the all-bins
+// team kernel instead of one launch per wide bin (the default: C3 fast 1.314 vs 1.393 ms on
+// one GPU, profiles/r04c/ab_*.txt).
 static int g_wide_team = -1;
 static bool wide_team_enabled() {
   if (g_wide_team < 0) {
     const char* e = getenv("BCE_WIDE_TEAM");
-    g_wide_team = (e && e[0] == '0') ? 0 : 1;
+    g_wide_team = (e && e[0] == '1') ? 1 : 0;  // default: one launch per bin (faster on one GPU)
   }
   return g_wide_team != 0;
 }
@@ -1783,7 +1784,7 @@ extern "C" int bce_consensus_planned(const int64_t* offsets, int64_t n_markets, 
   // needs the weight output (its lockstep teams read w back instead of parking it behind
   // barriers) and keys of 20 + 12 bits.  The short bins go to the side stream first, so
   // their workgroups are dispatched before the team kernel's fill the rest of the chip.
-  // BCE_WIDE_TEAM=0 keeps one launch per bin (the A/B baseline).
+  // Off by default (bce_debug_set_wide_team / BCE_WIDE_TEAM=1 turn it on).
   const bool team_env = wide_team_enabled();
   int64_t wide_markets = 0;
   for (int b = kPlanSideLast + 1; b <= BCE_NBINS - 2; ++b) wide_markets += bin_start_host[b + 1] - bin_start_host[b];

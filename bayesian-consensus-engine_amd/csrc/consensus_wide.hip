@@ -40,7 +40,11 @@
 constexpr int kWideHR = 1;       // rounds of NT uniques whose gathers are in flight together (2: C3 fast +6%)
 constexpr int kWideWPE = 4;      // min waves per SIMD (register budget; 4 vs 2: exact -1.3%, fast unchanged)
 constexpr int kWideNWBF = 4;     // FAST nweight read-backs per batch (1: 1.645, 2: 1.634, 4: 1.587 ms C3)
-constexpr bool kWideSwz = true;  // sorted probabilities in region A rotated per thread block (below)
+// Sorted probabilities in region A rotated per thread block (sq_addr below): conflict-free
+// step-3 stores, but the per-element read addresses spill 4-10 VGPRs in the FAST kernels --
+// C3 fast 1.505 vs 1.314 ms per bin, 1.633 vs 1.393 ms in the team kernel, parity green
+// (profiles/r04c/ab_*.txt): kept off.
+constexpr bool kWideSwz = false;
 
 namespace bce {
 namespace {

@@ -53,13 +53,53 @@ struct Line {
   std::string msg;              // header error / type error message
 };
 
-// One worker's share of the batch.
-struct Part {
+// sourceId -> local id: open addressing over 64-bit FNV-1a hashes (std::unordered_map's
+// node chasing and std::hash were the parser's largest cost)
+struct Intern {
+  std::vector<std::string> names;
+  std::vector<uint64_t> hash;   // per id
+  std::vector<int32_t> slot;    // -1 empty
+  size_t mask = 0;
+  static uint64_t fnv(const std::string& k) {
+    uint64_t h = 1469598103934665603ull;
+    for (unsigned char c : k) h = (h ^ c) * 1099511628211ull;
+    return h ^ (h >> 29);
+  }
+  void grow() {
+    const size_t n = slot.empty() ? 1024 : slot.size() * 2;
+    slot.assign(n, -1);
+    mask = n - 1;
+    for (size_t i = 0; i < names.size(); ++i) {
+      size_t j = hash[i] & mask;
+      while (slot[j] >= 0) j = (j + 1) & mask;
+      slot[j] = (int32_t)i;
+    }
+  }
+  int32_t id(const std::string& k) {
+    if (2 * (names.size() + 1) > slot.size()) grow();
+    const uint64_t h = fnv(k);
+    size_t j = h & mask;
+    for (;;) {
+      const int32_t v = slot[j];
+      if (v < 0) break;
+      if (hash[(size_t)v] == h && names[(size_t)v] == k) return v;
+      j = (j + 1) & mask;
+    }
+    const int32_t v = (int32_t)names.size();
+    names.push_back(k);
+    hash.push_back(h);
+    slot[j] = v;
+    return v;
+  }
+};
+
+// One worker's share of the batch (cache-line aligned: the vectors' end pointers move on
+// every push_back, and adjacent parts sharing a line serialised the workers).
+struct alignas(128) Part {
   std::vector<Line> lines;
   std::vector<double> prob;      // checked probabilities of every line, in order
   std::vector<int32_t> local;    // their sourceIds as ids into `names` below
-  std::vector<std::string> names;
-  std::unordered_map<std::string, int32_t> ids;
+  Intern ids;
 };
 
 struct Batch {
@@ -227,6 +267,54 @@ struct Parser {
     }
     *is_int = integral;
     if (!v) return;
+    // Exact fast path (Clinger): a significand of <= 15 digits is an exact double and so is
+    // 10^k for k <= 22, so one IEEE multiply / divide is the correctly rounded value
+    {
+      uint64_t sig = 0;
+      int nd = 0, frac = 0, ex = 0;
+      bool ok = true, seen_dot = false, nz = false;
+      const char* q = (*s == '-') ? s + 1 : s;
+      for (; q < p && *q != 'e' && *q != 'E'; ++q) {
+        if (*q == '.') {
+          seen_dot = true;
+          continue;
+        }
+        const int d = *q - '0';
+        if (d != 0 || nz) {
+          nz = true;
+          if (++nd > 15) {
+            ok = false;
+            break;
+          }
+        }
+        sig = sig * 10 + (uint64_t)d;
+        if (seen_dot) ++frac;
+      }
+      if (ok && q < p) {  // exponent
+        ++q;
+        bool eneg = false;
+        if (*q == '+' || *q == '-') eneg = (*q++ == '-');
+        int ev = 0;
+        for (; q < p; ++q) {
+          ev = ev * 10 + (*q - '0');
+          if (ev > 400) {
+            ok = false;
+            break;
+          }
+        }
+        ex = eneg ? -ev : ev;
+      }
+      const int k = ex - frac;
+      if (ok && k >= -22 && k <= 22) {
+        static const double p10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                                       1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+        double x = (double)sig;
+        x = (k >= 0) ? x * p10[k] : x / p10[-k];
+        if (*s == '-' && !(integral && x == 0.0)) x = -x;  // int -0 is 0 -> float 0.0
+        *v = x;
+        return;
+      }
+    }
     // strtod in the C locale: correctly rounded like float(str) and float(int) (ties to
     // even), subnormals kept, +-inf past the double range (_as_float's OverflowError
     // branch, float('1e999')), 0 below it (float('1e-999'))
@@ -531,15 +619,7 @@ void parse_line(Part& pt, const char* b, const char* e, Line& ln) {
             ln.msg = (why[0] == '.') ? "signals[" + std::to_string(idx) + "]" + why : std::string(why);
             stopped = true;
           } else {
-            auto it = pt.ids.find(sidv);
-            int32_t id;
-            if (it == pt.ids.end()) {
-              id = (int32_t)pt.names.size();
-              pt.names.push_back(sidv);
-              pt.ids.emplace(sidv, id);
-            } else {
-              id = it->second;
-            }
+            const int32_t id = pt.ids.id(sidv);
             pt.prob.push_back(pv);
             pt.local.push_back(id);
             ++ln.n_checked;
@@ -819,7 +899,7 @@ extern "C" int bce_jsonl_parse(const char* text, int64_t len, int32_t threads, v
   std::unordered_map<std::string_view, int32_t> all;
   std::vector<std::string_view> uniq;
   for (auto& pt : parts)
-    for (auto& nm : pt.names)
+    for (auto& nm : pt.ids.names)
       if (all.emplace(std::string_view(nm), 0).second) uniq.push_back(std::string_view(nm));
   std::sort(uniq.begin(), uniq.end());
   B->names.reserve(uniq.size());
@@ -841,8 +921,8 @@ extern "C" int bce_jsonl_parse(const char* text, int64_t len, int32_t threads, v
   B->sid.resize((size_t)nv);
   int64_t at = 0;
   for (auto& pt : parts) {
-    std::vector<int32_t> rank(pt.names.size());
-    for (size_t i = 0; i < pt.names.size(); ++i) rank[i] = all[std::string_view(pt.names[i])];
+    std::vector<int32_t> rank(pt.ids.names.size());
+    for (size_t i = 0; i < pt.ids.names.size(); ++i) rank[i] = all[std::string_view(pt.ids.names[i])];
     for (size_t i = 0; i < pt.prob.size(); ++i) {
       B->prob[(size_t)at] = pt.prob[i];
       B->sid[(size_t)at] = rank[(size_t)pt.local[i]];

@@ -80,6 +80,8 @@ def parse(argv=None):
     p.add_argument("--shard", default=None,
                    help="c3 only: R/N or all/N -- time rank R's (or every rank's) market shard of an N-rank "
                         "run in this one process, no process group (predicted strong scaling)")
+    p.add_argument("--graph", action="store_true",
+                   help="c3: replay each step as a captured HIP graph (one launch per step)")
     p.add_argument("--no-secondary", action="store_true",
                    help="c2 at N=1 only: skip the secondary lines (c3, c4, c5, tb) the default run appends "
                         "under 'secondary' (each a reduced-step run of its own --config line)")

@@ -32,9 +32,9 @@ OUT = tab_variants.OUT
 VARIANTS = {
     "wbase": [],
     # round-3 thread-major sorted-probability layout (4-way conflicts on the step-3 stores)
-    "wnoswz": [("consensus_wide.hip", "constexpr bool kWideSwz = true;", "constexpr bool kWideSwz = false;")],
+    "wswz": [("consensus_wide.hip", "constexpr bool kWideSwz = false;", "constexpr bool kWideSwz = true;")],
     # (thread-major layout) the short-market side-stream kernels launched after the team kernel
-    "tafter": [("consensus_wide.hip", "constexpr bool kWideSwz = true;", "constexpr bool kWideSwz = false;"),
+    "tafter": [
                ("consensus.hip", """  if (team) {
     for (int b = 0; b <= side_last && !rc; ++b) {""", """  if (team) {
     if (!rc) {
@@ -54,7 +54,7 @@ VARIANTS = {
     }""", """      rc = seg_ok ? launch_seg_for_len(lens[b], a, side) : launch_long_lds(a, side);
     }""")],
     # (thread-major layout) the team kernel one workgroup short per two CUs (room for the side stream)
-    "tless": [("consensus_wide.hip", "constexpr bool kWideSwz = true;", "constexpr bool kWideSwz = false;"),
+    "tless": [
               ("consensus_wide.hip", "  int64_t grid = (int64_t)cu_count() * per_cu;\n  if (grid > items) grid = items;",
                "  int64_t grid = (int64_t)cu_count() * per_cu - cu_count() / 2;\n  if (grid > items) grid = items;")],
     # ---- ablations (timing only; outputs are wrong by construction -- no parity gate) ----
