@@ -221,54 +221,123 @@ constexpr int kTbLpmWaves = 4;
 constexpr int kTbStage = 64 * kTbLpmMax + 64;  // doubles per wave buffer: a tile's agents + pads
 constexpr int kTbStageIt = 64 * kTbLpmMax / 128;  // 16-B loads per lane for a full tile
 constexpr int kTbStageBatch = 4;                  // of them in flight together (2 x 8 VGPRs each)
+// STAGED tiles with two LDS buffers per wave filled by LDS-DMA (global_load_lds_dword, 64
+// per array): the next array streams in while this one is computed on.  One workgroup of
+// four waves per CU (1 wave per SIMD, the LDS is 135 KB), so nothing else hides latency.
+constexpr bool kTbDMA = true;
 
 __device__ __forceinline__ int tb_pad(int i) { return i + (i >> 5); }
 
+template <bool STAGED>
+struct TbLpmCfg {
+  static constexpr bool DB = STAGED && kTbDMA;
+  static constexpr int WPE = DB ? 1 : 2;  // waves per SIMD (VGPR budget 512 / 256)
+};
+
+// s_waitcnt vmcnt(63): everything but the last 63 vector-memory instructions has landed --
+// with the 64 DMAs of the next array just issued, the array before them is in LDS
+__device__ __forceinline__ void tb_wait_dma_but_next() { __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | (15 << 8) | (3 << 14)); }
+__device__ __forceinline__ void tb_wait_dma_all() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0)
+
 template <bool STAGED, bool EXOTIC>
-__global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_eu(2, 2))) void tiebreak_lpm_kernel(TbArgs a, const int32_t* list,
+__global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_eu(TbLpmCfg<STAGED>::WPE, TbLpmCfg<STAGED>::WPE))) void tiebreak_lpm_kernel(TbArgs a, const int32_t* list,
                                                                          int64_t n_list, int* fault) {
-  // one buffer per wave (16.9 KB): two workgroups of four waves per CU
-  __shared__ double sBuf[STAGED ? kTbLpmWaves : 1][STAGED ? kTbStage : 1];
+  constexpr bool DB = TbLpmCfg<STAGED>::DB;
+  // one buffer per wave (16.9 KB; two workgroups of four waves per CU), or two (DB)
+  __shared__ double sBuf[STAGED ? kTbLpmWaves : 1][DB ? 2 : 1][STAGED ? kTbStage : 1];
   const int lane = lane_id();
-  const int wv = STAGED ? (int)(threadIdx.x >> 6) : 0;
-  double* const buf = sBuf[wv];
-  int32_t* const ibuf = reinterpret_cast<int32_t*>(buf);
+  const int wv = STAGED ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;  // uniform: LDS bases in SGPRs
+  double* buf = sBuf[wv][0];
+  int32_t* ibuf = reinterpret_cast<int32_t*>(buf);
+  auto use_buf = [&](int k) {
+    buf = sBuf[wv][DB ? k : 0];
+    ibuf = reinterpret_cast<int32_t*>(buf);
+  };
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t tile = wave; tile * 64 < n_list; tile += nwaves) {
+  // a tile's metadata: this lane's market and the tile's agent range [B, B + cnt)
+  struct Meta {
+    int64_t m, off;
+    int n;
+    bool has;
+    int64_t B;
+    int cnt;
+    int skip;  // 0 process, 1 every market empty, 2 a market longer than kTbLpmMax inside
+  };
+  auto meta_of = [&](int64_t tile) -> Meta {
+    Meta t{};
     const int64_t li = tile * 64 + lane;
-    const bool has = li < n_list;
-    const int64_t m = has ? (list ? (int64_t)list[li] : li) : 0;
-    const int64_t off = has ? a.offsets[m] : 0;
-    int n = has ? (int)(a.offsets[m + 1] - off) : 0;
-    if (ballot(n > kTbLpmMax || n < 0)) {
+    t.has = tile * 64 < n_list && li < n_list;
+    t.m = t.has ? (list ? (int64_t)list[li] : li) : 0;
+    t.off = t.has ? a.offsets[t.m] : 0;
+    t.n = t.has ? (int)(a.offsets[t.m + 1] - t.off) : 0;
+    if (ballot(t.n > kTbLpmMax || t.n < 0)) {
       raise_fault(fault, kFaultTooLong);
-      if (n > kTbLpmMax || n < 0) n = 0;
+      if (t.n > kTbLpmMax || t.n < 0) t.n = 0;
     }
-    if (!ballot(n > 0)) {
-      if (has) {
-        a.winner[m] = 0.0; a.label[m] = -1; a.n_groups[m] = -1; a.variance[m] = 0.0;
-      }
-      continue;
+    if (!ballot(t.n > 0)) {
+      t.skip = 1;
+      return t;
     }
     // STAGED: the tile's agents [B, E) (lane 0's market starts it, the last lane's ends it)
-    const int64_t B = ((int64_t)__builtin_amdgcn_readfirstlane((int)(off >> 32)) << 32) |
-                      (uint32_t)__builtin_amdgcn_readfirstlane((int)off);
-    const int last_lane = 63 - __builtin_clzll(ballot(has));
-    const int64_t endl = off + n;
+    t.B = ((int64_t)__builtin_amdgcn_readfirstlane((int)(t.off >> 32)) << 32) |
+          (uint32_t)__builtin_amdgcn_readfirstlane((int)t.off);
+    const int last_lane = 63 - __builtin_clzll(ballot(t.has));
+    const int64_t endl = t.off + t.n;
     const int64_t E = ((int64_t)__builtin_amdgcn_readlane((int)(endl >> 32), last_lane) << 32) |
                       (uint32_t)__builtin_amdgcn_readlane((int)endl, last_lane);
-    const int cnt_tile = (int)(E - B);  // <= 64 * 32 unless a market inside [B, E) was too long
-    if (STAGED && (E - B > 64 * kTbLpmMax || E < B)) {
-      // a market longer than kTbLpmMax (already faulted and zeroed above) still lies inside
-      // [B, E): staging the range would run past this wave's buffer, so the tile is skipped
-      // (every market gets the empty marker; the fault word reports the call as failed)
+    t.cnt = (int)(E - t.B);  // <= 64 * 32 unless a market inside [B, E) was too long
+    // a market longer than kTbLpmMax (already faulted and zeroed above) still lies inside
+    // [B, E): staging the range would run past this wave's buffer, so the tile is skipped
+    // (every market gets the empty marker; the fault word reports the call as failed)
+    if (STAGED && (E - t.B > 64 * kTbLpmMax || E < t.B)) {
       raise_fault(fault, kFaultTooLong);
+      t.skip = 2;
+    }
+    return t;
+  };
+  // DB: one array of a tile into buffer k by LDS-DMA -- 256-B segments (32 doubles, one padded
+  // row) per instruction, always 64 of them (vmcnt accounting); lanes past the data re-read
+  // the tile's first dword into slack
+  auto dma_arr = [&](const double* src, int k, const Meta& t) {
+    const uint32_t* g = reinterpret_cast<const uint32_t*>(src + t.B);
+    const int nd = 2 * t.cnt;
+    double* dst = sBuf[wv][DB ? k : 0];
+    wave_sync_lds();  // this wave's reads of the buffer (the last flush) are done
+#pragma unroll 1
+    for (int q = 0; q < 64; ++q) {
+      const int d = 64 * q + lane;
+      dma_b32(g + (d < nd ? d : 0), dst + 33 * q);
+    }
+  };
+  Meta cur{};
+  if constexpr (DB) {
+    cur = meta_of(wave);
+    if (cur.skip == 0) dma_arr(a.pred, 0, cur);
+  }
+  for (int64_t tile = wave; tile * 64 < n_list; tile += nwaves) {
+    Meta nxt{};
+    if constexpr (DB) {
+      nxt = meta_of(tile + nwaves);  // (its loads wait out this tile's prediction DMA too)
+      nxt.skip = (tile + nwaves) * 64 < n_list ? nxt.skip : 3;
+    } else {
+      cur = meta_of(tile);
+    }
+    const int64_t m = cur.m, off = cur.off;
+    const bool has = cur.has;
+    const int n = cur.n;
+    if (cur.skip) {
       if (has) {
         a.winner[m] = 0.0; a.label[m] = -1; a.n_groups[m] = -1; a.variance[m] = 0.0;
       }
+      if constexpr (DB) {
+        if (nxt.skip == 0) dma_arr(a.pred, 0, nxt);
+        cur = nxt;
+      }
       continue;
     }
+    const int64_t B = cur.B;
+    const int cnt_tile = cur.cnt;
     const int lrow = (int)(off - B);    // this lane's row in the staged buffer
     // every lane reads inside its own row (positions past n re-read the last agent); a lane
     // with an empty market reads the tile's first agent (masked later)
@@ -374,7 +443,13 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     unsigned u[kTbLpmMax];
     double kp[kTbLpmMax];
     int ng = 0;
-    if constexpr (STAGED) stage(a.pred);
+    if constexpr (DB) {
+      dma_arr(a.weight, 1, cur);  // streams in under phase 1
+      tb_wait_dma_but_next();     // the predictions are in buffer 0
+      use_buf(0);
+    } else if constexpr (STAGED) {
+      stage(a.pred);
+    }
     const double praw0 = at(a.pred, 0);  // a single agent keeps its raw prediction (tiebreak.py:89-96)
     {
 #pragma unroll
@@ -435,7 +510,13 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     // A group's outputs overwrite slot g of its market's row in place: group g ends only after
     // every group <= g, and agent g (ordinal <= g) belongs to one of those -- consumed.
     double densp[kTbLpmMax];
-    if constexpr (STAGED) stage(a.weight);
+    if constexpr (DB) {
+      dma_arr(a.rel, 0, cur);
+      tb_wait_dma_but_next();  // the weights are in buffer 1
+      use_buf(1);
+    } else if constexpr (STAGED) {
+      stage(a.weight);
+    }
     {
       double tot = 0.0;
       int cnt = 0;
@@ -459,7 +540,13 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     // ---- 4. reliabilities: max per group (first maximum kept), the winner ------------------
     double bd = 0.0, bm = 0.0, bk = 0.0;
     bool tie = false;
-    if constexpr (STAGED) stage(a.rel);
+    if constexpr (DB) {
+      dma_arr(a.conf, 1, cur);
+      tb_wait_dma_but_next();  // the reliabilities are in buffer 0
+      use_buf(0);
+    } else if constexpr (STAGED) {
+      stage(a.rel);
+    }
     {
       double mx = 0.0;
 #pragma unroll
@@ -488,7 +575,17 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     }
 
     // ---- 5. confidences: variance (input order), then the per-group means -----------------
-    if constexpr (STAGED) stage(a.conf);
+    if constexpr (DB) {
+      if (nxt.skip == 0) {
+        dma_arr(a.pred, 0, nxt);  // the next tile's predictions stream in under phase 5
+        tb_wait_dma_but_next();
+      } else {
+        tb_wait_dma_all();
+      }
+      use_buf(1);  // the confidences
+    } else if constexpr (STAGED) {
+      stage(a.conf);
+    }
     double variance;
     {
       double cs = 0.0;
@@ -544,7 +641,9 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
         a.variance[m] = (n == 1) ? 0.0 : variance;
       }
     }
+    if constexpr (DB) cur = nxt;
   }
+  if constexpr (DB) tb_wait_dma_all();  // no DMA outlives the wave
 }
 
 // n > 64: one workgroup per market.  (rounded key, index) pairs are bitonic-sorted in
