@@ -11,7 +11,7 @@
       as MI355X_MICROARCH.md §HBM prescribes: FETCH_SIZE (KB) reports 1/2 of the bytes of a
       wide coalesced read on gfx950 -> x2; WRITE_SIZE (KB) is exact for 16-B streaming stores.
       (stream_read_bytes=B: the kernel also gathers.  tools/fetch_calib.hip measured a random
-      16-B gather at 64 B of FETCH_SIZE, i.e. counted in full (profiles/r03_fetch_calib.txt),
+      16-B gather at 64 B of FETCH_SIZE, i.e. counted in full (profiles/archive/r03_fetch_calib.txt),
       so only the B bytes of coalesced streaming reads are under-counted: read = FETCH + B/2.
       Gathers served by the Infinity Cache are counted too, so this is an upper bound on HBM
       reads for a table that stays MALL-resident.)
@@ -95,7 +95,7 @@ def main():
     else:
         rd = f_kb * 1024.0 + 0.5 * float(stream_rd)
         corr = (f"FETCH_SIZE + half of the {stream_rd} streamed read bytes (gathers counted in full, "
-                "profiles/r03_fetch_calib.txt), WRITE_SIZE as is")
+                "profiles/archive/r03_fetch_calib.txt), WRITE_SIZE as is")
     wr = w_kb * 1024.0
     j = dict(meta, kernel=kern, fetch_size_kb=f_kb, write_size_kb=w_kb, launches=[nf, nw],
              read_bytes_corrected=rd, write_bytes=wr, hbm_bytes_per_launch=rd + wr, correction=corr)

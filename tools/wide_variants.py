@@ -26,7 +26,7 @@ OUT = tab_variants.OUT
 # Variants of rounds 2-3 (row exchange layout, 6-wave occupancy, no-park, power-of-two bins,
 # EXACT np2 split, FAST np2 merge, no DPP fusion, no swap stages, the s_memtime phase timer,
 # gather windows, late probabilities, dedup-before-sort, M0 save/restore) were source patches
-# of the pre-round-4 kernel; their results are in DESIGN.md §4.2 and profiles/r03*/.  They no
+# of the pre-round-4 kernel; their results are in DESIGN.md §4.2 and profiles/archive/r03*/.  They no
 # longer apply to the refactored per-market body and were dropped.  The all-bins team kernel
 # against one launch per bin is a runtime switch: BCE_WIDE_TEAM=0 with "wbase".
 VARIANTS = {
@@ -57,6 +57,8 @@ VARIANTS = {
     "tless": [
               ("consensus_wide.hip", "  int64_t grid = (int64_t)cu_count() * per_cu;\n  if (grid > items) grid = items;",
                "  int64_t grid = (int64_t)cu_count() * per_cu - cu_count() / 2;\n  if (grid > items) grid = items;")],
+    # tie-break lane kernel with round 3's single LDS buffer and register-staged loads
+    "tbnodma": [("tiebreak.hip", "constexpr bool kTbDMA = true;", "constexpr bool kTbDMA = false;")],
     # ---- ablations (timing only; outputs are wrong by construction -- no parity gate) ----
     # the sort network run twice (the second pass on sorted keys costs the same)
     "xsort2": [("consensus_wide.hip", "  wide_sort<NN, NW, R>(key, sX, t, lane);\n",
