@@ -221,10 +221,15 @@ constexpr int kTbLpmWaves = 4;
 constexpr int kTbStage = 64 * kTbLpmMax + 64;  // doubles per wave buffer: a tile's agents + pads
 constexpr int kTbStageIt = 64 * kTbLpmMax / 128;  // 16-B loads per lane for a full tile
 constexpr int kTbStageBatch = 4;                  // of them in flight together (2 x 8 VGPRs each)
-// STAGED tiles with two LDS buffers per wave filled by LDS-DMA (global_load_lds_dword, 64
-// per array): the next array streams in while this one is computed on.  One workgroup of
-// four waves per CU (1 wave per SIMD, the LDS is 135 KB), so nothing else hides latency.
-constexpr bool kTbDMA = true;
+// How a STAGED tile's arrays reach LDS:
+//   0  16-B loads into registers, kTbStageBatch in flight, then ds_writes (two workgroups of
+//      four waves per CU): 0.851 ms for the 1M x 32 tb line;
+//   1  LDS-DMA (global_load_lds_dword, 64 per array) into the one buffer, then vmcnt(0);
+//   2  two buffers per wave filled by LDS-DMA, the next array streaming in under the current
+//      phase -- one workgroup per CU (1 wave per SIMD, 135 KB of LDS): 1.316 ms, VALU active
+//      32% of wave cycles but nothing else issues while that wave waits (profiles/r04e/).
+constexpr int kTbStageMode = 0;
+constexpr bool kTbDMA = kTbStageMode == 2;
 
 __device__ __forceinline__ int tb_pad(int i) { return i + (i >> 5); }
 
@@ -349,6 +354,11 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     // per-iteration loop paid ~16 serial HBM latencies per array and tile)
     auto stage = [&](const double* src) {
       wave_sync_lds();  // the buffer's previous readers (this wave) are done
+      if constexpr (kTbStageMode == 1) {
+        dma_arr(src, 0, cur);
+        tb_wait_dma_all();
+        return;
+      }
       if (((uintptr_t)(src + B) & 15) == 0) {
 #pragma unroll 1
         for (int k0 = 0; k0 < kTbStageIt; k0 += kTbStageBatch) {

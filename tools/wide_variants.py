@@ -57,8 +57,9 @@ VARIANTS = {
     "tless": [
               ("consensus_wide.hip", "  int64_t grid = (int64_t)cu_count() * per_cu;\n  if (grid > items) grid = items;",
                "  int64_t grid = (int64_t)cu_count() * per_cu - cu_count() / 2;\n  if (grid > items) grid = items;")],
-    # tie-break lane kernel with round 3's single LDS buffer and register-staged loads
-    "tbnodma": [("tiebreak.hip", "constexpr bool kTbDMA = true;", "constexpr bool kTbDMA = false;")],
+    # tie-break lane kernel: LDS-DMA staging into the one buffer (1) / two buffers (2)
+    "tbdma1": [("tiebreak.hip", "constexpr int kTbStageMode = 0;", "constexpr int kTbStageMode = 1;")],
+    "tbdma2": [("tiebreak.hip", "constexpr int kTbStageMode = 0;", "constexpr int kTbStageMode = 2;")],
     # ---- ablations (timing only; outputs are wrong by construction -- no parity gate) ----
     # the sort network run twice (the second pass on sorted keys costs the same)
     "xsort2": [("consensus_wide.hip", "  wide_sort<NN, NW, R>(key, sX, t, lane);\n",
