@@ -80,6 +80,9 @@ def parse(argv=None):
     p.add_argument("--shard", default=None,
                    help="c3 only: R/N or all/N -- time rank R's (or every rank's) market shard of an N-rank "
                         "run in this one process, no process group (predicted strong scaling)")
+    p.add_argument("--single-mode", action="store_true",
+                   help="c3 / c5: time only the line's own summation mode (profiling runs: every "
+                        "dispatch of a kernel then belongs to that mode)")
     p.add_argument("--graph", action="store_true",
                    help="c3: replay each step as a captured HIP graph (one launch per step)")
     p.add_argument("--no-secondary", action="store_true",

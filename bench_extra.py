@@ -281,7 +281,9 @@ def _c3(args, world, rank, barrier, max_over, sum_over):
     import copy
     a2 = copy.copy(args)
     a2.steps, a2.warmup, a2.prewarm_s = max(5, args.steps // 4), 3, 0.0
-    wall2, per2 = _timed(step_other, a2, world, torch.cuda.current_stream(dev), barrier, max_over)
+    wall2 = per2 = None
+    if not getattr(args, "single_mode", False):
+        wall2, per2 = _timed(step_other, a2, world, torch.cuda.current_stream(dev), barrier, max_over)
     wall, per = _timed(step, args, world, torch.cuda.current_stream(dev), barrier, max_over)
     from bayesian_engine import _native as N
 
@@ -322,8 +324,8 @@ def _c3(args, world, rank, barrier, max_over, sum_over):
                      "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc("pmc_c3.json", signals_this_rank=n),
                      "kernel": "consensus (all bins, one step)",
                      "bytes_per_launch": bytes_step, "avg_launch_ms": per * 1e3,
-                     f"{other}_mode": {"ms_per_step": wall2 / a2.steps * 1e3, "avg_launch_ms": per2 * 1e3,
-                                       "frac": bytes_step / per2 / 1e9 / HBM_PEAK_GBS}},
+                     f"{other}_mode": ({"ms_per_step": wall2 / a2.steps * 1e3, "avg_launch_ms": per2 * 1e3,
+                                        "frac": bytes_step / per2 / 1e9 / HBM_PEAK_GBS} if per2 else None)},
         "cpu_baseline": cpu_line,
         "parity_vs_oracle": parity,
     }
@@ -511,18 +513,21 @@ def _c5(args, world, rank, barrier, max_over, sum_over):
     # the other pass-1 mode, same loop on fewer steps, from the same starting weights
     import copy
     main_mode = mode["m"]
-    mode["m"] = "exact" if main_mode == "fast" else "fast"
-    w.copy_(w_init)
-    a2 = copy.copy(args)
-    a2.steps, a2.warmup, a2.prewarm_s = max(2, args.steps // 2), 1, 0.0
-    ev_k.clear()
-    wall2, _ = _timed(step, a2, world, torch.cuda.current_stream(dev), barrier, max_over)
-    kern2 = float(np.mean([a.elapsed_time(b) for a, b in ev_k[-a2.steps:]])) / 1e3
-    other = {"mode": mode["m"], "ms_per_step": wall2 / a2.steps * 1e3, "avg_launch_ms": kern2 * 1e3,
-             "frac": (8 * A * Mloc + 16 * A + 9 * Mloc) / kern2 / 1e9 / HBM_PEAK_GBS,
-             "traffic": _pmc("pmc_c5_fast.json" if mode["m"] == "fast" else "pmc_c5.json", markets_this_rank=Mloc)}
-    mode["m"] = main_mode
-    t_fast = kern if main_mode == "fast" else kern2
+    other, kern2 = {"mode": "exact" if main_mode == "fast" else "fast", "skipped": "--single-mode"}, None
+    if not getattr(args, "single_mode", False):
+        mode["m"] = "exact" if main_mode == "fast" else "fast"
+        w.copy_(w_init)
+        a2 = copy.copy(args)
+        a2.steps, a2.warmup, a2.prewarm_s = max(2, args.steps // 2), 1, 0.0
+        ev_k.clear()
+        wall2, _ = _timed(step, a2, world, torch.cuda.current_stream(dev), barrier, max_over)
+        kern2 = float(np.mean([a.elapsed_time(b) for a, b in ev_k[-a2.steps:]])) / 1e3
+        other = {"mode": mode["m"], "ms_per_step": wall2 / a2.steps * 1e3, "avg_launch_ms": kern2 * 1e3,
+                 "frac": (8 * A * Mloc + 16 * A + 9 * Mloc) / kern2 / 1e9 / HBM_PEAK_GBS,
+                 "traffic": _pmc("pmc_c5_fast.json" if mode["m"] == "fast" else "pmc_c5.json",
+                                 markets_this_rank=Mloc)}
+        mode["m"] = main_mode
+    t_fast = kern if main_mode == "fast" else (kern2 or float("nan"))
     parity = None
     if rank == 0 and world == 1 and not args.no_parity and not args.no_cpu_baseline:
         parity = _parity_c5(P, L, N, st, args)

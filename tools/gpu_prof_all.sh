@@ -1,9 +1,16 @@
 #!/bin/bash
-# rocprofv3 stats + PMC for the headline and the secondary HBM configs (GPU box, repo root).
+# rocprofv3 stats + PMC for every bench line's dominant kernel (GPU box, repo root).  The PMC
+# meta keys are what bench.py / bench_extra.py match before using a file's `traffic`.
 # steps_total = consensus launches per PMC pass of that bench command (warmup + timed, plus
-# the c3 line's other-mode steps), so the PMC figures are per step.
+# the c3 line's other-mode steps), so the C3 figure is per step; stream_read_bytes = the
+# streamed (coalesced) read bytes per step, whose FETCH_SIZE alone is doubled -- the table
+# gathers are counted in full (profiles/archive/r03_fetch_calib.txt).
 set -u
-bash tools/gpu_profile.sh c2 consensus_tab32_kernel markets=1000000 signals_per_market=32 kernel=consensus_tab32_kernel -- --no-secondary && \
+bash tools/gpu_profile.sh c2 consensus_tab32_kernel markets=1000000 signals_per_market=32 sources=10000 kernel=consensus_tab32_kernel -- --no-secondary && \
 bash tools/gpu_profile.sh c4 replay_step_kernel sources_this_rank=10000000 -- --config c4 && \
-bash tools/gpu_profile.sh c3 consensus signals_this_rank=100000000 steps_total=15 -- --config c3 && \
-bash tools/gpu_profile.sh c5 reestimate markets_this_rank=1000000 steps_total=7 -- --config c5
+bash tools/gpu_profile.sh c3 consensus signals_this_rank=100000000 steps_total=7 stream_read_bytes=1201627112 -- --config c3 --single-mode && \
+bash tools/gpu_profile.sh tb tiebreak_lpm_kernel markets=1000000 -- --config tb && \
+bash tools/gpu_profile.sh c5 reestimate_consensus_votes_kernel markets_this_rank=1000000 mode=exact -- --config c5 --steps 2 --warmup 1 --single-mode && \
+python3 tools/pmc_summary.py stats gpurun_out/prof_c5/stats reestimate_agreement_votes_kernel > gpurun_out/prof_c5/stats_agreement.json && \
+python3 tools/pmc_summary.py pmc gpurun_out/prof_c5/fetch gpurun_out/prof_c5/write reestimate_agreement_votes_kernel \
+  gpurun_out/prof_c5/pmc_agreement.json markets_this_rank=1000000
