@@ -90,6 +90,10 @@ __device__ __forceinline__ unsigned bitonic_sort_seg(unsigned key, int l) {
 __device__ __forceinline__ double py_min(double a, double b) { return (b < a) ? b : a; }
 __device__ __forceinline__ double py_max(double a, double b) { return (b > a) ? b : a; }
 
+// k integer-valued: k * 0.5 is exact, and an integer exactly when k is even (every double
+// >= 2^53 is an even integer) -- fmod(k, 2.0) == 0.0 without ocml's fmod loop
+__device__ __forceinline__ bool is_even(double k) { return rint(k * 0.5) == k * 0.5; }
+
 // CPython round(x, nd) for 0 <= nd <= 22 (10^nd exact): the correctly rounded decimal (half-even on
 // the exact binary value) converted back to the nearest double.  x*10^nd is split
 // exactly (hi + lo via the fma error term), the nearest integer k of hi+lo is found with
@@ -107,11 +111,32 @@ __device__ __forceinline__ double py_round_nd(double x, double scale, double thr
     if (lo != 0.0) k = ((d > 0.0) == (lo > 0.0)) ? k0 + (d > 0.0 ? 1.0 : -1.0) : k0;
   } else if (d == 0.0 && (lo == 0.5 || lo == -0.5)) {
     const double k1 = k0 + (lo > 0.0 ? 1.0 : -1.0);
-    k = (fmod(k0, 2.0) == 0.0) ? k0 : k1;
+    k = is_even(k0) ? k0 : k1;
   }
   double r = k / scale;
   if (r == 0.0) r = copysign(0.0, x);
   return r;
+}
+
+// py_round_nd as selects (no divergent branches in an unrolled loop), and the division by
+// 10^nd as q = RN(k * rinv) with one FMA correction, rinv = RN(10^-nd): k is an integer
+// below 2^53 and 10^nd <= 10^22, so the residual k - q*10^nd is exact and RN(q + r*rinv) is
+// the correctly rounded k / 10^nd (Markstein's theorem; checked against IEEE division by
+// tools/check_markstein.c over every nd in 0..22).
+__device__ __forceinline__ double py_round_nd_sel(double x, double scale, double rinv, double thresh) {
+  const double hi = x * scale;
+  const double lo = __builtin_fma(x, scale, -hi);
+  const double k0 = rint(hi);
+  const double d = hi - k0;
+  const bool dhalf = (d == 0.5) | (d == -0.5);
+  const bool up1 = dhalf & (lo != 0.0) & ((d > 0.0) == (lo > 0.0));
+  const bool up2 = (d == 0.0) & ((lo == 0.5) | (lo == -0.5)) & !is_even(k0);
+  const double step = (up1 ? (d > 0.0) : (lo > 0.0)) ? 1.0 : -1.0;
+  const double k = (up1 | up2) ? k0 + step : k0;
+  const double q = k * rinv;
+  double r = __builtin_fma(__builtin_fma(-q, scale, k), rinv, q);
+  r = (r == 0.0) ? copysign(0.0, x) : r;
+  return (fabs(x) < thresh) ? r : x;
 }
 
 // CPython round(x, nd) for -15 <= nd < 0 (P = 10^-nd, exact): the correctly rounded
@@ -129,7 +154,7 @@ __device__ __forceinline__ double py_round_neg(double x, double P) {
     k = k0 + (r > 0.0 ? 1.0 : -1.0);
   } else if (fabs(r) == h) {
     const double k1 = k0 + (r > 0.0 ? 1.0 : -1.0);
-    k = (fmod(k0, 2.0) == 0.0) ? k0 : k1;
+    k = is_even(k0) ? k0 : k1;
   }
   double out = k * P;
   if (out == 0.0) out = copysign(0.0, x);

@@ -38,6 +38,7 @@ struct TbArgs {
   int32_t* g_of;   // nullable: per agent, the ordinal of its group (dict insertion order)
   double rscale;   // 10^ndigits (ndigits >= 0) or 10^-ndigits (ndigits < 0)
   double rthresh;  // see py_round_nd
+  double rinv;     // RN(1 / rscale) (mode 0)
   int rmode;       // 0: py_round_nd, 1: py_round_neg, 2: identity (nd > 323), 3: signed zero (nd < -308),
                    // 4: big-integer path 23 <= nd <= 323, 5: big-integer path -308 <= nd <= -16
   int rnd;         // ndigits (modes 4, 5)
@@ -76,6 +77,13 @@ __device__ __forceinline__ bool tb_better(double d1, double m1, double k1, doubl
   if (d1 != d2) return d1 > d2;
   if (m1 != m2) return m1 > m2;
   return (-k1) > (-k2);
+}
+
+// tb_better without short-circuit returns
+__device__ __forceinline__ bool tb_better_sel(double d1, double m1, double k1, double d2, double m2,
+                                              double k2) {
+  const bool nd = d1 != d2, nm = m1 != m2;
+  return nd ? (d1 > d2) : (nm ? (m1 > m2) : ((-k1) > (-k2)));
 }
 
 __device__ __forceinline__ double rl_f64(double v, int l) {
@@ -224,7 +232,8 @@ constexpr int kTbStageBatch = 4;                  // of them in flight together 
 // How a STAGED tile's arrays reach LDS:
 //   0  16-B loads into registers, kTbStageBatch in flight, then ds_writes (two workgroups of
 //      four waves per CU): 0.851 ms for the 1M x 32 tb line;
-//   1  LDS-DMA (global_load_lds_dword, 64 per array) into the one buffer, then vmcnt(0);
+//   1  LDS-DMA (global_load_lds_dword, 64 per array) into the one buffer, then vmcnt(0):
+//      1.070 ms (0.849-0.866 for mode 0 on the same box, profiles/r04f/);
 //   2  two buffers per wave filled by LDS-DMA, the next array streaming in under the current
 //      phase -- one workgroup per CU (1 wave per SIMD, 135 KB of LDS): 1.316 ms, VALU active
 //      32% of wave cycles but nothing else issues while that wave waits (profiles/r04e/).
@@ -232,6 +241,14 @@ constexpr int kTbStageMode = 0;
 constexpr bool kTbDMA = kTbStageMode == 2;
 
 __device__ __forceinline__ int tb_pad(int i) { return i + (i >> 5); }
+constexpr int kTbDump = 64;  // per-lane sink slots after a wave buffer (FULL tiles' masked stores)
+
+// A per-lane bit set hidden from the compiler: each phase re-derives its run-boundary
+// compares from it instead of keeping 32 lane masks (64 SGPRs) alive across the tile.
+__device__ __forceinline__ unsigned tb_bits(unsigned m) {
+  asm volatile("" : "+v"(m));
+  return m;
+}
 
 template <bool STAGED>
 struct TbLpmCfg {
@@ -244,12 +261,14 @@ struct TbLpmCfg {
 __device__ __forceinline__ void tb_wait_dma_but_next() { __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | (15 << 8) | (3 << 14)); }
 __device__ __forceinline__ void tb_wait_dma_all() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0)
 
-template <bool STAGED, bool EXOTIC>
+// PART (STAGED launches): 1 = only FULL tiles, 2 = every other tile; 0 = all tiles, one body.
+template <bool STAGED, bool EXOTIC, int PART = 0>
 __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_eu(TbLpmCfg<STAGED>::WPE, TbLpmCfg<STAGED>::WPE))) void tiebreak_lpm_kernel(TbArgs a, const int32_t* list,
                                                                          int64_t n_list, int* fault) {
   constexpr bool DB = TbLpmCfg<STAGED>::DB;
+  static_assert(PART == 0 || (STAGED && !DB && !EXOTIC), "FULL / rest split: staged register-batch kernels only");
   // one buffer per wave (16.9 KB; two workgroups of four waves per CU), or two (DB)
-  __shared__ double sBuf[STAGED ? kTbLpmWaves : 1][DB ? 2 : 1][STAGED ? kTbStage : 1];
+  __shared__ double sBuf[STAGED ? kTbLpmWaves : 1][DB ? 2 : 1][STAGED ? kTbStage + kTbDump : 1];
   const int lane = lane_id();
   const int wv = STAGED ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;  // uniform: LDS bases in SGPRs
   double* buf = sBuf[wv][0];
@@ -268,6 +287,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     int64_t B;
     int cnt;
     int skip;  // 0 process, 1 every market empty, 2 a market longer than kTbLpmMax inside
+    bool full;  // every lane holds a market of exactly kTbLpmMax agents
   };
   auto meta_of = [&](int64_t tile) -> Meta {
     Meta t{};
@@ -292,6 +312,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     const int64_t E = ((int64_t)__builtin_amdgcn_readlane((int)(endl >> 32), last_lane) << 32) |
                       (uint32_t)__builtin_amdgcn_readlane((int)endl, last_lane);
     t.cnt = (int)(E - t.B);  // <= 64 * 32 unless a market inside [B, E) was too long
+    t.full = ballot(t.has && t.n == kTbLpmMax) == ~0ull;
     // a market longer than kTbLpmMax (already faulted and zeroed above) still lies inside
     // [B, E): staging the range would run past this wave's buffer, so the tile is skipped
     // (every market gets the empty marker; the fault word reports the call as failed)
@@ -327,6 +348,11 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
       nxt.skip = (tile + nwaves) * 64 < n_list ? nxt.skip : 3;
     } else {
       cur = meta_of(tile);
+    }
+    if constexpr (PART == 1) {
+      if (!cur.full) continue;  // (skipped tiles are never full)
+    } else if constexpr (PART == 2) {
+      if (cur.full) continue;
     }
     const int64_t m = cur.m, off = cur.off;
     const bool has = cur.has;
@@ -448,6 +474,169 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
       return (p + 1 >= n) || ((u[p] >> 5) != (u[p + 1 < kTbLpmMax ? p + 1 : p] >> 5));
     };
     const double nd = (double)(n > 0 ? n : 1);
+
+    // ---- FULL tile: 64 markets of exactly kTbLpmMax agents, lane L's row at 33 L ------------
+    // The same four phases as below with n a compile-time 32: no per-position validity masks,
+    // row reads at immediate offsets (or one shift-add for a sorted position), and every
+    // conditional store a store to a selected address (the lane's sink slot when masked).
+    if constexpr (PART == 1) {
+      {
+        constexpr int N = kTbLpmMax;
+        double* row = buf + 33 * lane;
+        int32_t* irow = ibuf + 33 * lane;
+        double* sink = buf + kTbStage + lane;
+        int32_t* isink = ibuf + 2 * kTbStage + lane;
+        auto put_sel = [&](unsigned bits, int p, unsigned g, double v) {
+          *(((bits >> p) & 1u) ? row + g : sink) = v;
+        };
+        auto put_sel_i32 = [&](unsigned bits, int p, unsigned g, int v) {
+          *(((bits >> p) & 1u) ? irow + g : isink) = v;
+        };
+        // 1. keys, first-seen ordinals, sort
+        stage(a.pred);
+        double kp[N];  // (PART 1 runs only for round mode 0, see launch_tb_short)
+#pragma unroll
+        for (int t = 0; t < N; ++t) kp[t] = py_round_nd_sel(row[t], a.rscale, a.rinv, a.rthresh);
+        unsigned u[N];
+        int ngf = 0;
+        {
+          int go[N];
+#pragma unroll
+          for (int t = 0; t < N; ++t) {
+            int g = -1;
+#pragma unroll
+            for (int s2 = 0; s2 < t; ++s2) g = key_eq(kp[s2], kp[t]) ? go[s2] : g;
+            go[t] = g < 0 ? ngf : g;
+            ngf += g < 0 ? 1 : 0;
+            u[t] = ((unsigned)go[t] << 5) | (unsigned)t;
+          }
+          if (a.g_of) {
+            wave_sync_lds();
+#pragma unroll
+            for (int t = 0; t < N; ++t) irow[t] = go[t];
+            flush_i32(a.g_of);
+          }
+        }
+        oem_sort_kv(u, kp);
+        // run boundaries: bit p of stm / enm = a run starts / ends at sorted position p
+        unsigned stm = 1u, enm = 1u << (N - 1);
+#pragma unroll
+        for (int p = 1; p < N; ++p) {
+          const unsigned d = ((u[p] >> 5) != (u[p - 1] >> 5)) ? 1u : 0u;
+          stm |= d << p;
+          enm |= d << (p - 1);
+        }
+#pragma unroll
+        for (int p = 1; p < N; ++p) kp[p] = ((stm >> p) & 1u) ? kp[p] : kp[p - 1];  // run head's key
+        // 2. group keys and counts
+        if (a.g_key) {
+          wave_sync_lds();
+          const unsigned en_ = tb_bits(enm);
+#pragma unroll
+          for (int p = 0; p < N; ++p) put_sel(en_, p, u[p] >> 5, kp[p]);
+          flush(a.g_key);
+        }
+        if (a.g_count) {
+          wave_sync_lds();
+          const unsigned st_ = tb_bits(stm), en_ = tb_bits(enm);
+          int cnt = 0;
+#pragma unroll
+          for (int p = 0; p < N; ++p) {
+            cnt = (((st_ >> p) & 1u) ? 0 : cnt) + 1;
+            put_sel_i32(en_, p, u[p] >> 5, cnt);
+          }
+          flush_i32(a.g_count);
+        }
+        // 3. densities
+        double densp[N];
+        stage(a.weight);
+        {
+          const unsigned st_ = tb_bits(stm), en_ = tb_bits(enm);
+          double tot = 0.0;
+          int cnt = 0;
+#pragma unroll
+          for (int p = 0; p < N; ++p) {
+            const bool st = (st_ >> p) & 1u;
+            tot = (st ? 0.0 : tot) + row[u[p] & 31u];  // tiebreak.py:60, sum from int 0
+            cnt = (st ? 0 : cnt) + 1;
+            densp[p] = tot / (double)cnt;
+            put_sel(en_, p, u[p] >> 5, densp[p]);
+          }
+          if (a.g_density) flush(a.g_density);
+        }
+        // 4. max reliability per group, the winner and the tie flag
+        double bd = 0.0, bm = 0.0, bk = 0.0;
+        bool tie = false;
+        stage(a.rel);
+        {
+          const unsigned st_ = tb_bits(stm), en_ = tb_bits(enm);
+          double mx = 0.0;
+#pragma unroll
+          for (int p = 0; p < N; ++p) {
+            const unsigned g = u[p] >> 5;
+            const double r = row[u[p] & 31u];
+            mx = ((st_ >> p) & 1u) ? r : ((r > mx) ? r : mx);  // tiebreak.py:62
+            put_sel(en_, p, g, mx);
+            const bool en = (en_ >> p) & 1u;
+            const double dens = densp[p];
+            const bool same = (dens == bd) && (mx == bm);
+            const bool better = (g == 0) | tb_better_sel(dens, mx, kp[p], bd, bm, bk);  // tiebreak.py:113-117
+            tie = en ? (better ? ((g != 0) && same) : (tie || same)) : tie;     // tiebreak.py:123-133
+            const bool upd = en && better;
+            bd = upd ? dens : bd;
+            bm = upd ? mx : bm;
+            bk = upd ? kp[p] : bk;
+          }
+          if (a.g_maxrel) flush(a.g_maxrel);
+        }
+        // 5. variance (input order), per-group mean confidences
+        stage(a.conf);
+        double variance;
+        {
+          double cs = 0.0;
+#pragma unroll
+          for (int t = 0; t < N; ++t) cs += row[t];
+          const double mean = cs / (double)N;
+          double sq[N];
+          unsigned slow = 0;
+#pragma unroll
+          for (int t = 0; t < N; ++t) {
+            bool ok;
+            sq[t] = bce_pow::pow2_fast(row[t] - mean, ok);
+            slow |= ok ? 0u : (1u << t);
+          }
+          while (ballot(slow != 0u)) {
+            const int t1 = slow ? (int)__builtin_ctz(slow) : 0;
+            slow &= slow - 1u;
+            const double v = bce_pow::pow2_full(row[t1] - mean);
+#pragma unroll
+            for (int t = 0; t < N; ++t) sq[t] = (t == t1) ? v : sq[t];
+          }
+          double vs = 0.0;
+#pragma unroll
+          for (int t = 0; t < N; ++t) vs += sq[t];
+          variance = vs / (double)N;
+        }
+        if (a.g_avgconf) {
+          const unsigned st_ = tb_bits(stm), en_ = tb_bits(enm);
+          double gcs = 0.0;
+          int cnt = 0;
+#pragma unroll
+          for (int p = 0; p < N; ++p) {
+            const bool st = (st_ >> p) & 1u;
+            gcs = (st ? 0.0 : gcs) + row[u[p] & 31u];  // tiebreak.py:61
+            cnt = (st ? 0 : cnt) + 1;
+            put_sel(en_, p, u[p] >> 5, gcs / (double)cnt);
+          }
+          flush(a.g_avgconf);
+        }
+        a.winner[m] = bk;
+        a.label[m] = (ngf == 1) ? BCE_TB_UNANIMOUS : tie ? BCE_TB_PREDICTION_VALUE_SMALLEST : BCE_TB_WEIGHT_DENSITY;
+        a.n_groups[m] = ngf;
+        a.variance[m] = variance;
+        continue;
+      }
+    }
 
     // ---- 1. keys, group ordinals (first-seen order), sort with the key as payload ---------
     unsigned u[kTbLpmMax];
@@ -882,17 +1071,27 @@ static int launch_tb_short(const TbArgs& a, const int32_t* market_list, int64_t 
     const int64_t tiles = (nl + 63) / 64;
     int64_t blocks = (tiles + kTbLpmWaves - 1) / kTbLpmWaves;
     // contiguous markets stage each wave's agent range in LDS; a market list gathers rows
+    // contiguous markets, register-batch staging: the FULL tiles (64 markets of 32 agents)
+    // run a kernel specialised for them, then a second launch takes every other tile (each
+    // launch only reads the offsets of the tiles it leaves to the other)
+    const bool split = kTbStageMode != 2 && !EXOTIC && a.rmode == 0;
     const void* fn = market_list ? reinterpret_cast<const void*>(&tiebreak_lpm_kernel<false, EXOTIC>)
+                     : split     ? reinterpret_cast<const void*>(&tiebreak_lpm_kernel<true, false, 1>)
                                  : reinterpret_cast<const void*>(&tiebreak_lpm_kernel<true, EXOTIC>);
     const int per_cu = blocks_per_cu(fn, 64 * kTbLpmWaves, 0, 1, "tiebreak_lpm_kernel");
     const int64_t cap = (int64_t)cu_count() * per_cu;
     if (blocks > cap) blocks = cap;
-    if (market_list)
-      hipLaunchKernelGGL((tiebreak_lpm_kernel<false, EXOTIC>), dim3((int)blocks), dim3(64 * kTbLpmWaves), 0,
-                         as_stream(stream), a, market_list, nl, fault_word());
-    else
-      hipLaunchKernelGGL((tiebreak_lpm_kernel<true, EXOTIC>), dim3((int)blocks), dim3(64 * kTbLpmWaves), 0,
-                         as_stream(stream), a, market_list, nl, fault_word());
+    hipStream_t st = as_stream(stream);
+    const dim3 grid((int)blocks), block(64 * kTbLpmWaves);
+    if (market_list) {
+      hipLaunchKernelGGL((tiebreak_lpm_kernel<false, EXOTIC>), grid, block, 0, st, a, market_list, nl, fault_word());
+    } else if (split) {
+      hipLaunchKernelGGL((tiebreak_lpm_kernel<true, false, 1>), grid, block, 0, st, a, market_list, nl, fault_word());
+      if (int rc = check_launch("tiebreak_lpm_kernel<full>")) return rc;
+      hipLaunchKernelGGL((tiebreak_lpm_kernel<true, false, 2>), grid, block, 0, st, a, market_list, nl, fault_word());
+    } else {
+      hipLaunchKernelGGL((tiebreak_lpm_kernel<true, EXOTIC>), grid, block, 0, st, a, market_list, nl, fault_word());
+    }
     return check_launch("tiebreak_lpm_kernel");
   }
   int64_t blocks = (nl + 3) / 4;
@@ -919,7 +1118,7 @@ extern "C" int bce_tiebreak_csr(const int64_t* offsets, int64_t n_markets, const
   double rs = 1.0, rt = 0.0;
   const int rmode = tb_round_mode(ndigits, &rs, &rt);
   TbArgs a{offsets, n_markets, pred, conf, weight, rel, winner, label, n_groups, variance,
-           g_key, g_count, g_density, g_avgconf, g_maxrel, g_of, rs, rt, rmode, ndigits, fault_word()};
+           g_key, g_count, g_density, g_avgconf, g_maxrel, g_of, rs, rt, 1.0 / rs, rmode, ndigits, fault_word()};
   return rmode >= 4 ? launch_tb_short<true>(a, market_list, nl, max_len, stream)
                     : launch_tb_short<false>(a, market_list, nl, max_len, stream);
 }
@@ -970,7 +1169,7 @@ extern "C" int bce_tiebreak_csr_long(const int64_t* offsets, int64_t n_markets, 
   double rs = 1.0, rt = 0.0;
   const int rmode = tb_round_mode(ndigits, &rs, &rt);
   TbArgs a{offsets, n_markets, pred, conf, weight, rel, winner, label, n_groups, variance,
-           g_key, g_count, g_density, g_avgconf, g_maxrel, g_of, rs, rt, rmode, ndigits, fault_word()};
+           g_key, g_count, g_density, g_avgconf, g_maxrel, g_of, rs, rt, 1.0 / rs, rmode, ndigits, fault_word()};
   return rmode >= 4 ? launch_tb_long<true>(a, list, n_list, max_len, stream)
                     : launch_tb_long<false>(a, list, n_list, max_len, stream);
 }

@@ -829,3 +829,60 @@ def test_tiebreak_signed_zero_group_key_is_first_member(n_agents):
         a = int(off[m])
         assert sign(gk[a]) == sign(keys[a]) == sign(exp["g_key"][a]), (m, gk[a], keys[a])
         assert sign(win[m]) == sign(exp["winner"][m]), (m, win[m], exp["winner"][m])
+
+
+@pytest.mark.parametrize("precision", [6, 0, 2, 10, 22])
+def test_tiebreak_full_tiles_vs_oracle(precision):
+    """Tiles of 64 markets of exactly 32 agents run a kernel specialised for them
+    (tiebreak_lpm_kernel PART 1: n a compile-time 32, selects instead of branches, the
+    division by 10^precision as a reciprocal product with one FMA correction); every other
+    tile runs the general body (PART 2).  A batch of both kinds -- full tiles around ragged
+    ones, adversarial predictions (exact halves at the precision, -0.0, huge, NaN, inf),
+    weights with 0 and inf -- matches the oracle bit for bit in every output, the group
+    ordinals and per-group mean confidences included."""
+    import torch
+    from bayesian_engine import batch
+    from oracle import oracle as orc
+    rng = np.random.default_rng(900 + precision)
+    lens = np.full(64 * 40, 32, np.int64)
+    lens[64 * 17 + 5] = 31                        # one ragged tile among full ones
+    lens[64 * 30:64 * 31] = rng.integers(0, 33, 64)  # a tile of mixed lengths, empty markets included
+    off, pred, conf, weight, rel = _tb_inputs(lens, 4000 + precision)
+    n = len(pred)
+    half = (rng.integers(-5000, 5000, n) + 0.5) * 10.0 ** -precision  # exact ties at the precision
+    pred = np.where(rng.random(n) < 0.1, half, pred)
+    pred[rng.random(n) < 0.003] = np.nan
+    pred[rng.random(n) < 0.003] = np.inf
+    pred[rng.random(n) < 0.003] = -np.inf
+    weight[rng.random(n) < 0.01] = 0.0
+    weight[rng.random(n) < 0.002] = np.inf
+    keys = np.array([round(float(x), precision) for x in pred], np.float64)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    r = batch.tiebreak(T(off), T(pred), T(conf), T(weight), T(rel), precision=precision, offsets_host=off)
+    torch.cuda.synchronize()
+    exp = orc.tiebreak_csr(off, pred, conf, weight, rel, keys=keys)
+    for k in ("winner", "label", "n_groups", "variance"):
+        assert getattr(r, k).cpu().numpy().tobytes() == exp[k].astype(getattr(r, k).cpu().numpy().dtype).tobytes(), k
+    gk, gc, gd, ga, gm, go = (x.cpu().numpy() for x in (r.g_key, r.g_count, r.g_density, r.g_avgconf,
+                                                          r.g_maxrel, r.g_of))
+    with np.errstate(invalid="ignore"):
+        dens = exp["g_total"] / np.maximum(exp["g_count"], 1)
+    for m in range(len(lens)):
+        a, b, g = int(off[m]), int(off[m + 1]), int(exp["n_groups"][m])
+        if b == a:
+            continue
+        sl = slice(a, a + g)
+        assert gk[sl].tobytes() == exp["g_key"][sl].tobytes(), m
+        assert np.array_equal(gc[sl], exp["g_count"][sl]), m
+        assert gd[sl].tobytes() == dens[sl].tobytes(), m
+        assert ga[sl].tobytes() == exp["g_avgconf"][sl].tobytes(), m
+        assert gm[sl].tobytes() == exp["g_maxrel"][sl].tobytes(), m
+        uniq, ords = [], []
+        for k in map(float, keys[a:b]):
+            # first-seen ordinal under ==: -0.0 joins 0.0, a NaN key is never equal (own group)
+            j = next((i for i, x in enumerate(uniq) if x == k), None)
+            if j is None:
+                uniq.append(k)
+                j = len(uniq) - 1
+            ords.append(j)
+        assert list(go[a:b]) == ords, m

@@ -1,0 +1,57 @@
+// check_markstein.c -- the FULL tie-break kernel divides an integer k (|k| < 2^53) by
+// 10^nd (nd in 0..22) as q = RN(k * rinv), r = fma(-q, 10^nd, k), RN(q + r * rinv) with
+// rinv = RN(10^-nd) (bce_device.hpp py_round_nd_sel).  This compares that against the IEEE
+// quotient k / 10^nd for every nd: all k below 2^20, and 2e7 random k per nd drawn with
+// a log-uniform magnitude up to 2^53 (plus k near 2^53 and near multiples of 10^nd).
+//   gcc -O2 -ffp-contract=off -o /tmp/check_markstein tools/check_markstein.c -lm && /tmp/check_markstein
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+
+static uint64_t rng = 0x9E3779B97F4A7C15ull;
+static uint64_t next(void) {
+  rng ^= rng << 13;
+  rng ^= rng >> 7;
+  rng ^= rng << 17;
+  return rng;
+}
+
+static long bad = 0, tried = 0;
+static void one(double k, double s, double rinv) {
+  const double q0 = k * rinv;
+  const double q = fma(fma(-q0, s, k), rinv, q0);
+  const double ref = k / s;
+  ++tried;
+  if (q != ref) {
+    if (bad < 10) printf("MISMATCH k=%.17g s=%.17g q=%.17g ref=%.17g\n", k, s, q, ref);
+    ++bad;
+  }
+}
+
+int main(void) {
+  for (int nd = 0; nd <= 22; ++nd) {
+    double s = 1.0;
+    for (int i = 0; i < nd; ++i) s *= 10.0;
+    const double rinv = 1.0 / s;
+    for (int64_t k = 0; k < (1 << 20); ++k) {
+      one((double)k, s, rinv);
+      one(-(double)k, s, rinv);
+    }
+    for (int i = 0; i < 20000000; ++i) {
+      const int bits = 1 + (int)(next() % 53);
+      const uint64_t k = next() >> (64 - bits);
+      one((double)k, s, rinv);
+    }
+    for (int64_t j = 0; j < 100000; ++j) {
+      one(9007199254740991.0 - (double)j, s, rinv);
+      const double m = floor((double)(next() >> 11) / s) * s;  // a multiple of 10^nd below 2^53
+      if (m + 1 < 9007199254740992.0) {
+        one(m, s, rinv);
+        one(m + 1, s, rinv);
+        if (m >= 1) one(m - 1, s, rinv);
+      }
+    }
+  }
+  printf("%ld of %ld quotients differ from IEEE division\n", bad, tried);
+  return bad != 0;
+}

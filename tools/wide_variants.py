@@ -60,6 +60,9 @@ VARIANTS = {
     # tie-break lane kernel: LDS-DMA staging into the one buffer (1) / two buffers (2)
     "tbdma1": [("tiebreak.hip", "constexpr int kTbStageMode = 0;", "constexpr int kTbStageMode = 1;")],
     "tbdma2": [("tiebreak.hip", "constexpr int kTbStageMode = 0;", "constexpr int kTbStageMode = 2;")],
+    # tie-break without the FULL-tile kernel (one general launch, round 3's body)
+    "tbnofull": [("tiebreak.hip", "const bool split = kTbStageMode != 2 && !EXOTIC && a.rmode == 0;",
+                  "const bool split = false;")],
     # ---- ablations (timing only; outputs are wrong by construction -- no parity gate) ----
     # the sort network run twice (the second pass on sorted keys costs the same)
     "xsort2": [("consensus_wide.hip", "  wide_sort<NN, NW, R>(key, sX, t, lane);\n",
