@@ -86,6 +86,10 @@ __device__ __forceinline__ bool tb_better_sel(double d1, double m1, double k1, d
   return nd ? (d1 > d2) : (nm ? (m1 > m2) : ((-k1) > (-k2)));
 }
 
+// The rare exact square (pow2_fast's near-midpoint cases) out of line: inlined, its log/exp
+// polynomial constants were hoisted out of the tile loop and held in (spilled) registers.
+__device__ __noinline__ double tb_pow2_full(double d) { return bce_pow::pow2_full(d); }
+
 __device__ __forceinline__ double rl_f64(double v, int l) {
   int2 x = *reinterpret_cast<int2*>(&v);
   int2 y;
@@ -241,6 +245,7 @@ constexpr int kTbStageMode = 0;
 constexpr bool kTbDMA = kTbStageMode == 2;
 
 __device__ __forceinline__ int tb_pad(int i) { return i + (i >> 5); }
+constexpr bool kTbFullKeysInLds = true;  // FULL tiles: sort (ordinal, agent) alone, keys via LDS
 constexpr int kTbDump = 64;  // per-lane sink slots after a wave buffer (FULL tiles' masked stores)
 
 // A per-lane bit set hidden from the compiler: each phase re-derives its run-boundary
@@ -492,12 +497,18 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
         auto put_sel_i32 = [&](unsigned bits, int p, unsigned g, int v) {
           *(((bits >> p) & 1u) ? irow + g : isink) = v;
         };
+        unsigned u[N];
+        // each phase re-derives its row addresses from u (CSE across phases kept 64 address
+        // registers alive through the tile and spilled)
+        auto refresh_u = [&]() {
+#pragma unroll
+          for (int p = 0; p < N; ++p) u[p] = tb_bits(u[p]);
+        };
         // 1. keys, first-seen ordinals, sort
         stage(a.pred);
         double kp[N];  // (PART 1 runs only for round mode 0, see launch_tb_short)
 #pragma unroll
         for (int t = 0; t < N; ++t) kp[t] = py_round_nd_sel(row[t], a.rscale, a.rinv, a.rthresh);
-        unsigned u[N];
         int ngf = 0;
         {
           int go[N];
@@ -517,21 +528,44 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
             flush_i32(a.g_of);
           }
         }
-        oem_sort_kv(u, kp);
         // run boundaries: bit p of stm / enm = a run starts / ends at sorted position p
         unsigned stm = 1u, enm = 1u << (N - 1);
+        if constexpr (kTbFullKeysInLds) {
+          // the rounded keys wait in the lane's row while only the 32-bit (ordinal, agent)
+          // keys go through the network; each sorted position then reads its run head's key
+          wave_sync_lds();
 #pragma unroll
-        for (int p = 1; p < N; ++p) {
-          const unsigned d = ((u[p] >> 5) != (u[p - 1] >> 5)) ? 1u : 0u;
-          stm |= d << p;
-          enm |= d << (p - 1);
+          for (int t = 0; t < N; ++t) row[t] = kp[t];
+          oem_sort(u);
+#pragma unroll
+          for (int p = 1; p < N; ++p) {
+            const unsigned d = ((u[p] >> 5) != (u[p - 1] >> 5)) ? 1u : 0u;
+            stm |= d << p;
+            enm |= d << (p - 1);
+          }
+          unsigned ht = u[0] & 31u;
+          kp[0] = row[ht];
+#pragma unroll
+          for (int p = 1; p < N; ++p) {
+            ht = ((stm >> p) & 1u) ? (u[p] & 31u) : ht;
+            kp[p] = row[ht];
+          }
+        } else {
+          oem_sort_kv(u, kp);
+#pragma unroll
+          for (int p = 1; p < N; ++p) {
+            const unsigned d = ((u[p] >> 5) != (u[p - 1] >> 5)) ? 1u : 0u;
+            stm |= d << p;
+            enm |= d << (p - 1);
+          }
+#pragma unroll
+          for (int p = 1; p < N; ++p) kp[p] = ((stm >> p) & 1u) ? kp[p] : kp[p - 1];  // run head's key
         }
-#pragma unroll
-        for (int p = 1; p < N; ++p) kp[p] = ((stm >> p) & 1u) ? kp[p] : kp[p - 1];  // run head's key
         // 2. group keys and counts
         if (a.g_key) {
           wave_sync_lds();
           const unsigned en_ = tb_bits(enm);
+          refresh_u();
 #pragma unroll
           for (int p = 0; p < N; ++p) put_sel(en_, p, u[p] >> 5, kp[p]);
           flush(a.g_key);
@@ -539,6 +573,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
         if (a.g_count) {
           wave_sync_lds();
           const unsigned st_ = tb_bits(stm), en_ = tb_bits(enm);
+          refresh_u();
           int cnt = 0;
 #pragma unroll
           for (int p = 0; p < N; ++p) {
@@ -552,6 +587,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
         stage(a.weight);
         {
           const unsigned st_ = tb_bits(stm), en_ = tb_bits(enm);
+          refresh_u();
           double tot = 0.0;
           int cnt = 0;
 #pragma unroll
@@ -570,6 +606,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
         stage(a.rel);
         {
           const unsigned st_ = tb_bits(stm), en_ = tb_bits(enm);
+          refresh_u();
           double mx = 0.0;
 #pragma unroll
           for (int p = 0; p < N; ++p) {
@@ -597,28 +634,32 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
 #pragma unroll
           for (int t = 0; t < N; ++t) cs += row[t];
           const double mean = cs / (double)N;
-          double sq[N];
+          // squares summed as they come (no array of 32): the fast square is exact unless
+          // flagged; a lane with a flagged square redoes the ordered sum with exact ones
+          wave_sync_lds();  // re-read the confidences instead of holding all 32
+          double vs = 0.0;
           unsigned slow = 0;
 #pragma unroll
           for (int t = 0; t < N; ++t) {
             bool ok;
-            sq[t] = bce_pow::pow2_fast(row[t] - mean, ok);
+            vs += bce_pow::pow2_fast(row[t] - mean, ok);
             slow |= ok ? 0u : (1u << t);
           }
-          while (ballot(slow != 0u)) {
-            const int t1 = slow ? (int)__builtin_ctz(slow) : 0;
-            slow &= slow - 1u;
-            const double v = bce_pow::pow2_full(row[t1] - mean);
-#pragma unroll
-            for (int t = 0; t < N; ++t) sq[t] = (t == t1) ? v : sq[t];
+          if (slow) {
+            vs = 0.0;
+#pragma unroll 1
+            for (int t = 0; t < N; ++t) {
+              const double d = row[t] - mean;
+              bool ok;
+              const double q = bce_pow::pow2_fast(d, ok);
+              vs += ((slow >> t) & 1u) ? tb_pow2_full(d) : q;
+            }
           }
-          double vs = 0.0;
-#pragma unroll
-          for (int t = 0; t < N; ++t) vs += sq[t];
           variance = vs / (double)N;
         }
         if (a.g_avgconf) {
           const unsigned st_ = tb_bits(stm), en_ = tb_bits(enm);
+          refresh_u();
           double gcs = 0.0;
           int cnt = 0;
 #pragma unroll

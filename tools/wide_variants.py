@@ -61,6 +61,7 @@ VARIANTS = {
     "tbdma1": [("tiebreak.hip", "constexpr int kTbStageMode = 0;", "constexpr int kTbStageMode = 1;")],
     "tbdma2": [("tiebreak.hip", "constexpr int kTbStageMode = 0;", "constexpr int kTbStageMode = 2;")],
     # tie-break without the FULL-tile kernel (one general launch, round 3's body)
+    "tbkvsort": [("tiebreak.hip", "constexpr bool kTbFullKeysInLds = true;", "constexpr bool kTbFullKeysInLds = false;")],
     "tbnofull": [("tiebreak.hip", "const bool split = kTbStageMode != 2 && !EXOTIC && a.rmode == 0;",
                   "const bool split = false;")],
     # ---- ablations (timing only; outputs are wrong by construction -- no parity gate) ----
