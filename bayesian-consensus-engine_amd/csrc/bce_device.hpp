@@ -139,6 +139,22 @@ __device__ __forceinline__ double py_round_nd_sel(double x, double scale, double
   return (fabs(x) < thresh) ? r : x;
 }
 
+// py_round_nd_sel without its tie analysis: k = rint(x * 10^nd) is the answer unless the
+// product sits exactly on a half (|d| == 0.5) or is an integer with |lo| == 0.5 -- then
+// `slow` is set and the caller reruns py_round_nd_sel for that lane.
+__device__ __forceinline__ double py_round_nd_fast(double x, double scale, double rinv, double thresh, bool& slow) {
+  const double hi = x * scale;
+  const double lo = __builtin_fma(x, scale, -hi);
+  const double k = rint(hi);
+  const double d = hi - k;
+  const bool in = fabs(x) < thresh;
+  slow = in & ((fabs(d) == 0.5) | ((d == 0.0) & (fabs(lo) == 0.5)));
+  const double q = k * rinv;
+  double r = __builtin_fma(__builtin_fma(-q, scale, k), rinv, q);
+  r = (r == 0.0) ? copysign(0.0, x) : r;
+  return in ? r : x;
+}
+
 // CPython round(x, nd) for -15 <= nd < 0 (P = 10^-nd, exact): the correctly rounded
 // (half-even) multiple of P, converted back with one rounding.  k0 = rint(x / P) is at most
 // one off; the remainder r = x - k0 * P is exact under the FMA (|r| <= |x| with x's

@@ -49,6 +49,8 @@ struct DevCtx {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int* queue = nullptr;               // kQueueSlots pairs of team-kernel queue words
   std::atomic<unsigned> queue_next{0};
+  int* split = nullptr;               // kQueueSlots tie-break FULL/rest ticket words
+  std::atomic<unsigned> split_next{0};
 };
 constexpr int kQueueSlots = 64;
 DevCtx g_dev[kMaxDev];
@@ -70,6 +72,10 @@ DevCtx* dev_ctx() {
     if (e == hipSuccess) e = hipMalloc((void**)&qw, 2 * kQueueSlots * sizeof(int));
     if (e == hipSuccess) e = hipMemset(qw, 0, 2 * kQueueSlots * sizeof(int));
     if (e == hipSuccess) c->queue = qw;
+    int* sw = nullptr;
+    if (e == hipSuccess) e = hipMalloc((void**)&sw, kQueueSlots * sizeof(int));
+    if (e == hipSuccess) e = hipMemset(sw, 0, kQueueSlots * sizeof(int));
+    if (e == hipSuccess) c->split = sw;
     c->init_err = e;
     if (e == hipSuccess) c->fault = p;
   });
@@ -100,6 +106,13 @@ int* team_queue_slot() {
   if (!c || !c->queue) return nullptr;
   // a slot is reused after kQueueSlots launches; each launch zeroes its pair when it ends
   return c->queue + 2 * (c->queue_next.fetch_add(1) % kQueueSlots);
+}
+
+int* split_slot() {
+  DevCtx* c = dev_ctx();
+  if (!c || !c->split) return nullptr;
+  // tickets make reuse safe: a launch pair only reacts to its own ticket
+  return c->split + (c->split_next.fetch_add(1) % kQueueSlots);
 }
 
 int* fault_word() {

@@ -9,6 +9,8 @@
 // maximum (builtin max), and the winner is the lexicographic max of
 // (density, max_rel, -key) -- distinct groups never tie on the full tuple, so any
 // reduction order selects the same winner.
+#include <atomic>
+
 #include "bce_device.hpp"
 #include "bce_internal.hpp"
 #include "consensus_common.hpp"
@@ -43,6 +45,8 @@ struct TbArgs {
                    // 4: big-integer path 23 <= nd <= 323, 5: big-integer path -308 <= nd <= -16
   int rnd;         // ndigits (modes 4, 5)
   int* fault;      // device fault word: kFaultRoundOverflow (CPython's OverflowError)
+  int* split;      // PART 1/2 launches: PART 1 writes `ticket` here when it leaves a tile to PART 2
+  int ticket;      // this launch pair's number (host counter, never 0): no reset needed
 };
 
 constexpr int kFaultRoundOverflow = 6;  // round(x, nd) too large to represent (mode 5)
@@ -89,6 +93,19 @@ __device__ __forceinline__ bool tb_better_sel(double d1, double m1, double k1, d
 // The rare exact square (pow2_fast's near-midpoint cases) out of line: inlined, its log/exp
 // polynomial constants were hoisted out of the tile loop and held in (spilled) registers.
 __device__ __noinline__ double tb_pow2_full(double d) { return bce_pow::pow2_full(d); }
+
+// x / c for a group size c in 1..32: RN(x * rc) with one FMA correction, rc = RN(1 / c)
+// (Markstein; tools/check_markstein.c checks 3e9 quotients against IEEE division), exact
+// for |x| in [2^-1000, 2^1000]; a wave with any other x (0, subnormal, huge, inf, NaN)
+// divides those lanes.
+__device__ __forceinline__ double tb_div_small(double x, int c, const double* rc_tab) {
+  const double rc = rc_tab[c];
+  const double b = (double)c;
+  const double q0 = x * rc;
+  const double q = __builtin_fma(__builtin_fma(-q0, b, x), rc, q0);
+  const bool ok = (fabs(x) >= 0x1p-1000) & (fabs(x) <= 0x1p1000);
+  return ballot(!ok) ? (ok ? q : x / b) : q;
+}
 
 __device__ __forceinline__ double rl_f64(double v, int l) {
   int2 x = *reinterpret_cast<int2*>(&v);
@@ -246,7 +263,26 @@ constexpr bool kTbDMA = kTbStageMode == 2;
 
 __device__ __forceinline__ int tb_pad(int i) { return i + (i >> 5); }
 constexpr bool kTbFullKeysInLds = true;  // FULL tiles: sort (ordinal, agent) alone, keys via LDS
-constexpr int kTbDump = 64;  // per-lane sink slots after a wave buffer (FULL tiles' masked stores)
+constexpr int kTbDump = 64;
+// FULL tiles: 16-B loads per lane in flight while staging the predictions / confidences (few
+// registers live then; the weights / reliabilities, with keys and densities live, use stage())
+constexpr int kTbFullBatchPC = 8;
+// nontemporal hints on the staged input loads / the flushed output stores (A/B switches)
+constexpr bool kTbNtLoad = false;
+constexpr bool kTbNtStore = false;
+typedef double tb_d2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ double2 tb_ld2(const double* p) {
+  const tb_d2 v = kTbNtLoad ? __builtin_nontemporal_load(reinterpret_cast<const tb_d2*>(p))
+                            : *reinterpret_cast<const tb_d2*>(p);
+  return make_double2(v.x, v.y);
+}
+__device__ __forceinline__ void tb_st2(double* p, double x, double y) {
+  tb_d2 v;
+  v.x = x;
+  v.y = y;
+  if constexpr (kTbNtStore) __builtin_nontemporal_store(v, reinterpret_cast<tb_d2*>(p));
+  else *reinterpret_cast<tb_d2*>(p) = v;
+}  // per-lane sink slots after a wave buffer (FULL tiles' masked stores)
 
 // A per-lane bit set hidden from the compiler: each phase re-derives its run-boundary
 // compares from it instead of keeping 32 lane masks (64 SGPRs) alive across the tile.
@@ -274,6 +310,12 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
   static_assert(PART == 0 || (STAGED && !DB && !EXOTIC), "FULL / rest split: staged register-batch kernels only");
   // one buffer per wave (16.9 KB; two workgroups of four waves per CU), or two (DB)
   __shared__ double sBuf[STAGED ? kTbLpmWaves : 1][DB ? 2 : 1][STAGED ? kTbStage + kTbDump : 1];
+  // FULL tiles: RN(1 / c) for group sizes c = 1..32 (tb_div_small)
+  __shared__ double sRc[PART == 1 ? kTbLpmMax + 1 : 1];
+  if constexpr (PART == 1) {
+    if (threadIdx.x <= (unsigned)kTbLpmMax) sRc[threadIdx.x] = 1.0 / (double)(threadIdx.x ? threadIdx.x : 1);
+    __syncthreads();
+  }
   const int lane = lane_id();
   const int wv = STAGED ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;  // uniform: LDS bases in SGPRs
   double* buf = sBuf[wv][0];
@@ -317,7 +359,8 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     const int64_t E = ((int64_t)__builtin_amdgcn_readlane((int)(endl >> 32), last_lane) << 32) |
                       (uint32_t)__builtin_amdgcn_readlane((int)endl, last_lane);
     t.cnt = (int)(E - t.B);  // <= 64 * 32 unless a market inside [B, E) was too long
-    t.full = ballot(t.has && t.n == kTbLpmMax) == ~0ull;
+    // (PART 1 launches only with 16-B aligned arrays, so an even B aligns every row load)
+    t.full = ballot(t.has && t.n == kTbLpmMax) == ~0ull && (t.B & 1) == 0;
     // a market longer than kTbLpmMax (already faulted and zeroed above) still lies inside
     // [B, E): staging the range would run past this wave's buffer, so the tile is skipped
     // (every market gets the empty marker; the fault word reports the call as failed)
@@ -346,7 +389,11 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     cur = meta_of(wave);
     if (cur.skip == 0) dma_arr(a.pred, 0, cur);
   }
-  for (int64_t tile = wave; tile * 64 < n_list; tile += nwaves) {
+  // PART 2 has nothing to do when PART 1 found every tile full (the common uniform batch):
+  // it then only counts itself out
+  bool run = true;
+  if constexpr (PART == 2) run = __hip_atomic_load(a.split, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.ticket;
+  for (int64_t tile = wave; run && tile * 64 < n_list; tile += nwaves) {
     Meta nxt{};
     if constexpr (DB) {
       nxt = meta_of(tile + nwaves);  // (its loads wait out this tile's prediction DMA too)
@@ -355,7 +402,10 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
       cur = meta_of(tile);
     }
     if constexpr (PART == 1) {
-      if (!cur.full) continue;  // (skipped tiles are never full)
+      if (!cur.full) {  // (skipped tiles are never full)
+        if (lane == 0) __hip_atomic_store(a.split, a.ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        continue;
+      }
     } else if constexpr (PART == 2) {
       if (cur.full) continue;
     }
@@ -399,7 +449,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
           for (int k = 0; k < kTbStageBatch; ++k) {
             const int e = 2 * lane + 128 * (k0 + k);
             v[k] = make_double2(0.0, 0.0);
-            if (e + 1 < cnt_tile) v[k] = *reinterpret_cast<const double2*>(src + B + e);
+            if (e + 1 < cnt_tile) v[k] = tb_ld2(src + B + e);
           }
 #pragma unroll
           for (int k = 0; k < kTbStageBatch; ++k) {
@@ -431,13 +481,31 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
       }
       wave_sync_lds();
     };
+    // FULL tiles (2048 agents): no bounds checks, NB 16-B loads per lane in flight
+    auto stage_full = [&](const double* src, auto nb) {
+      constexpr int NB = decltype(nb)::value;  // (src + B is 16-B aligned: see Meta::full)
+      wave_sync_lds();
+#pragma unroll 1
+      for (int k0 = 0; k0 < kTbStageIt; k0 += NB) {
+        double2 v[NB];
+#pragma unroll
+        for (int k = 0; k < NB; ++k) v[k] = tb_ld2(src + B + 2 * lane + 128 * (k0 + k));
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+          const int e = 2 * lane + 128 * (k0 + k);
+          buf[tb_pad(e)] = v[k].x;
+          buf[tb_pad(e + 1)] = v[k].y;
+        }
+      }
+      wave_sync_lds();
+    };
     // LDS (padded) -> global [B, E), coalesced 16-B stores
     auto flush = [&](double* dst) {
       wave_sync_lds();
       const bool al = ((uintptr_t)(dst + B) & 15) == 0;
       for (int e = 2 * lane; e < cnt_tile; e += 128) {
         if (al && e + 1 < cnt_tile) {
-          *reinterpret_cast<double2*>(dst + B + e) = make_double2(buf[tb_pad(e)], buf[tb_pad(e + 1)]);
+          tb_st2(dst + B + e, buf[tb_pad(e)], buf[tb_pad(e + 1)]);
         } else {
           dst[B + e] = buf[tb_pad(e)];
           if (e + 1 < cnt_tile) dst[B + e + 1] = buf[tb_pad(e + 1)];
@@ -505,10 +573,14 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
           for (int p = 0; p < N; ++p) u[p] = tb_bits(u[p]);
         };
         // 1. keys, first-seen ordinals, sort
-        stage(a.pred);
+        stage_full(a.pred, std::integral_constant<int, kTbFullBatchPC>{});
         double kp[N];  // (PART 1 runs only for round mode 0, see launch_tb_short)
 #pragma unroll
-        for (int t = 0; t < N; ++t) kp[t] = py_round_nd_sel(row[t], a.rscale, a.rinv, a.rthresh);
+        for (int t = 0; t < N; ++t) {
+          bool slow;
+          kp[t] = py_round_nd_fast(row[t], a.rscale, a.rinv, a.rthresh, slow);
+          if (ballot(slow)) kp[t] = slow ? py_round_nd_sel(row[t], a.rscale, a.rinv, a.rthresh) : kp[t];
+        }
         int ngf = 0;
         {
           int go[N];
@@ -595,7 +667,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
             const bool st = (st_ >> p) & 1u;
             tot = (st ? 0.0 : tot) + row[u[p] & 31u];  // tiebreak.py:60, sum from int 0
             cnt = (st ? 0 : cnt) + 1;
-            densp[p] = tot / (double)cnt;
+            densp[p] = tb_div_small(tot, cnt, sRc);
             put_sel(en_, p, u[p] >> 5, densp[p]);
           }
           if (a.g_density) flush(a.g_density);
@@ -627,7 +699,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
           if (a.g_maxrel) flush(a.g_maxrel);
         }
         // 5. variance (input order), per-group mean confidences
-        stage(a.conf);
+        stage_full(a.conf, std::integral_constant<int, kTbFullBatchPC>{});
         double variance;
         {
           double cs = 0.0;
@@ -667,7 +739,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
             const bool st = (st_ >> p) & 1u;
             gcs = (st ? 0.0 : gcs) + row[u[p] & 31u];  // tiebreak.py:61
             cnt = (st ? 0 : cnt) + 1;
-            put_sel(en_, p, u[p] >> 5, gcs / (double)cnt);
+            put_sel(en_, p, u[p] >> 5, tb_div_small(gcs, cnt, sRc));
           }
           flush(a.g_avgconf);
         }
@@ -1115,7 +1187,9 @@ static int launch_tb_short(const TbArgs& a, const int32_t* market_list, int64_t 
     // contiguous markets, register-batch staging: the FULL tiles (64 markets of 32 agents)
     // run a kernel specialised for them, then a second launch takes every other tile (each
     // launch only reads the offsets of the tiles it leaves to the other)
-    const bool split = kTbStageMode != 2 && !EXOTIC && a.rmode == 0;
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    const bool split = kTbStageMode != 2 && !EXOTIC && a.rmode == 0 && al16(a.pred) && al16(a.conf) &&
+                       al16(a.weight) && al16(a.rel);
     const void* fn = market_list ? reinterpret_cast<const void*>(&tiebreak_lpm_kernel<false, EXOTIC>)
                      : split     ? reinterpret_cast<const void*>(&tiebreak_lpm_kernel<true, false, 1>)
                                  : reinterpret_cast<const void*>(&tiebreak_lpm_kernel<true, EXOTIC>);
@@ -1127,9 +1201,17 @@ static int launch_tb_short(const TbArgs& a, const int32_t* market_list, int64_t 
     if (market_list) {
       hipLaunchKernelGGL((tiebreak_lpm_kernel<false, EXOTIC>), grid, block, 0, st, a, market_list, nl, fault_word());
     } else if (split) {
-      hipLaunchKernelGGL((tiebreak_lpm_kernel<true, false, 1>), grid, block, 0, st, a, market_list, nl, fault_word());
+      static std::atomic<int> tickets{0};
+      TbArgs b = a;
+      b.split = split_slot();
+      do b.ticket = tickets.fetch_add(1) + 1; while (b.ticket == 0);
+      if (!b.split) {
+        set_error("tiebreak: no device split words");
+        return BCE_EHIP;
+      }
+      hipLaunchKernelGGL((tiebreak_lpm_kernel<true, false, 1>), grid, block, 0, st, b, market_list, nl, fault_word());
       if (int rc = check_launch("tiebreak_lpm_kernel<full>")) return rc;
-      hipLaunchKernelGGL((tiebreak_lpm_kernel<true, false, 2>), grid, block, 0, st, a, market_list, nl, fault_word());
+      hipLaunchKernelGGL((tiebreak_lpm_kernel<true, false, 2>), grid, block, 0, st, b, market_list, nl, fault_word());
     } else {
       hipLaunchKernelGGL((tiebreak_lpm_kernel<true, EXOTIC>), grid, block, 0, st, a, market_list, nl, fault_word());
     }
@@ -1159,7 +1241,7 @@ extern "C" int bce_tiebreak_csr(const int64_t* offsets, int64_t n_markets, const
   double rs = 1.0, rt = 0.0;
   const int rmode = tb_round_mode(ndigits, &rs, &rt);
   TbArgs a{offsets, n_markets, pred, conf, weight, rel, winner, label, n_groups, variance,
-           g_key, g_count, g_density, g_avgconf, g_maxrel, g_of, rs, rt, 1.0 / rs, rmode, ndigits, fault_word()};
+           g_key, g_count, g_density, g_avgconf, g_maxrel, g_of, rs, rt, 1.0 / rs, rmode, ndigits, fault_word(), nullptr, 0};
   return rmode >= 4 ? launch_tb_short<true>(a, market_list, nl, max_len, stream)
                     : launch_tb_short<false>(a, market_list, nl, max_len, stream);
 }
@@ -1210,7 +1292,7 @@ extern "C" int bce_tiebreak_csr_long(const int64_t* offsets, int64_t n_markets, 
   double rs = 1.0, rt = 0.0;
   const int rmode = tb_round_mode(ndigits, &rs, &rt);
   TbArgs a{offsets, n_markets, pred, conf, weight, rel, winner, label, n_groups, variance,
-           g_key, g_count, g_density, g_avgconf, g_maxrel, g_of, rs, rt, 1.0 / rs, rmode, ndigits, fault_word()};
+           g_key, g_count, g_density, g_avgconf, g_maxrel, g_of, rs, rt, 1.0 / rs, rmode, ndigits, fault_word(), nullptr, 0};
   return rmode >= 4 ? launch_tb_long<true>(a, list, n_list, max_len, stream)
                     : launch_tb_long<false>(a, list, n_list, max_len, stream);
 }

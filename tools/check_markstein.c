@@ -2,7 +2,8 @@
 // 10^nd (nd in 0..22) as q = RN(k * rinv), r = fma(-q, 10^nd, k), RN(q + r * rinv) with
 // rinv = RN(10^-nd) (bce_device.hpp py_round_nd_sel).  This compares that against the IEEE
 // quotient k / 10^nd for every nd: all k below 2^20, and 2e7 random k per nd drawn with
-// a log-uniform magnitude up to 2^53 (plus k near 2^53 and near multiples of 10^nd).
+// a log-uniform magnitude up to 2^53 (plus k near 2^53 and near multiples of 10^nd); and the
+// group means a / c, c in 1..32, the same way with rinv = RN(1 / c).
 //   gcc -O2 -ffp-contract=off -o /tmp/check_markstein tools/check_markstein.c -lm && /tmp/check_markstein
 #include <math.h>
 #include <stdint.h>
@@ -51,6 +52,23 @@ int main(void) {
         if (m >= 1) one(m - 1, s, rinv);
       }
     }
+  }
+  // the FULL kernel's group means: a / c for c in 1..32 with a in [2^-1000, 2^1000] (the
+  // kernel divides outside that range), rinv = RN(1 / c)
+  for (int c = 1; c <= 32; ++c) {
+    const double b = (double)c, rinv = 1.0 / b;
+    for (int i = 0; i < 20000000; ++i) {
+      const uint64_t r = next();
+      const int e = (int)(r % 2000) - 1000;                              // exponent in [-1000, 1000)
+      const double m = 1.0 + (double)(next() >> 12) * 0x1p-52;          // random significand
+      one(ldexp(m, e), b, rinv);
+      const double q = ldexp(1.0 + (double)(next() >> 12) * 0x1p-52, (int)(r % 40) - 20);
+      const double a0 = q * b;                                           // near-exact multiples
+      one(a0, b, rinv);
+      one(nextafter(a0, 0.0), b, rinv);
+      one(nextafter(a0, 1e300), b, rinv);
+    }
+    for (int k = 1; k < (1 << 16); ++k) one((double)k, b, rinv);         // small integer sums
   }
   printf("%ld of %ld quotients differ from IEEE division\n", bad, tried);
   return bad != 0;

@@ -61,9 +61,15 @@ VARIANTS = {
     "tbdma1": [("tiebreak.hip", "constexpr int kTbStageMode = 0;", "constexpr int kTbStageMode = 1;")],
     "tbdma2": [("tiebreak.hip", "constexpr int kTbStageMode = 0;", "constexpr int kTbStageMode = 2;")],
     # tie-break without the FULL-tile kernel (one general launch, round 3's body)
+    "tbpc16": [("tiebreak.hip", "constexpr int kTbFullBatchPC = 8;", "constexpr int kTbFullBatchPC = 16;")],
+    "tbpc4": [("tiebreak.hip", "constexpr int kTbFullBatchPC = 8;", "constexpr int kTbFullBatchPC = 4;")],
+    "tbntld": [("tiebreak.hip", "constexpr bool kTbNtLoad = false;", "constexpr bool kTbNtLoad = true;")],
+    "tbntst": [("tiebreak.hip", "constexpr bool kTbNtStore = false;", "constexpr bool kTbNtStore = true;")],
+    "tbntboth": [("tiebreak.hip", "constexpr bool kTbNtLoad = false;", "constexpr bool kTbNtLoad = true;"),
+                 ("tiebreak.hip", "constexpr bool kTbNtStore = false;", "constexpr bool kTbNtStore = true;")],
     "tbkvsort": [("tiebreak.hip", "constexpr bool kTbFullKeysInLds = true;", "constexpr bool kTbFullKeysInLds = false;")],
-    "tbnofull": [("tiebreak.hip", "const bool split = kTbStageMode != 2 && !EXOTIC && a.rmode == 0;",
-                  "const bool split = false;")],
+    "tbnofull": [("tiebreak.hip", "const bool split = kTbStageMode != 2 && !EXOTIC && a.rmode == 0 && al16(a.pred)",
+                  "const bool split = false && al16(a.pred)")],
     # ---- ablations (timing only; outputs are wrong by construction -- no parity gate) ----
     # the sort network run twice (the second pass on sorted keys costs the same)
     "xsort2": [("consensus_wide.hip", "  wide_sort<NN, NW, R>(key, sX, t, lane);\n",
