@@ -318,13 +318,17 @@ class TieBreakResult:
 
 def tiebreak(offsets: torch.Tensor, pred: torch.Tensor, conf: torch.Tensor, weight: torch.Tensor,
              rel: torch.Tensor, *, precision: int = 6, offsets_host: Optional[np.ndarray] = None,
-             out: Optional[TieBreakResult] = None) -> TieBreakResult:
+             out: Optional[TieBreakResult] = None, max_len: Optional[int] = None) -> TieBreakResult:
     """DeterministicTieBreaker(precision).resolve for every CSR market (tiebreak.py:73-152).
 
     Any market length (> 4096 agents sort in a global scratch slice).  ``precision`` as
     CPython round() for every int, bit for bit (exact big integers where 10^|precision| is
     not a double); a rounded key too large for a double raises OverflowError, as CPython's
-    round() does (precision <= -16 only, checked with one stream synchronisation)."""
+    round() does (precision <= -16 only, checked with one stream synchronisation).
+
+    ``max_len`` (optional, <= 64): the caller's bound on every market's length; the host then
+    skips its length scan of the offsets (a market longer than the bound fails the call with
+    a device fault, as the C ABI does)."""
     L = N.require_gpu()
     M = offsets.numel() - 1
     Nsig = pred.numel()
@@ -336,13 +340,17 @@ def tiebreak(offsets: torch.Tensor, pred: torch.Tensor, conf: torch.Tensor, weig
                               torch.empty(max(Nsig, 1), **i32), torch.empty(max(Nsig, 1), **f64),
                               torch.empty(max(Nsig, 1), **f64), torch.empty(max(Nsig, 1), **f64),
                               torch.empty(max(Nsig, 1), **i32))
-    offh = offsets_host if offsets_host is not None else offsets.cpu().numpy()
-    lens = np.diff(offh)
-    long_ = np.nonzero(lens > 64)[0]
     outs = (N.ptr(r.winner), N.ptr(r.label), N.ptr(r.n_groups), N.ptr(r.variance), N.ptr(r.g_key),
             N.ptr(r.g_count), N.ptr(r.g_density), N.ptr(r.g_avgconf), N.ptr(r.g_maxrel), N.ptr(r.g_of))
     ins = (N.ptr(pred), N.ptr(conf), N.ptr(weight), N.ptr(rel))
     st = N.stream(dev)
+    if max_len is not None and 0 < int(max_len) <= 64:
+        N.check(L.bce_tiebreak_csr(N.ptr(offsets), M, N.ptr(None), 0, *ins, int(max_len), int(precision), *outs, st),
+                "bce_tiebreak_csr")
+        return _round_overflow_check(r, precision, dev)
+    offh = offsets_host if offsets_host is not None else offsets.cpu().numpy()
+    lens = np.diff(offh)
+    long_ = np.nonzero(lens > 64)[0]
     if len(long_) == 0:
         N.check(L.bce_tiebreak_csr(N.ptr(offsets), M, N.ptr(None), 0, *ins, int(max(int(lens.max(initial=1)), 1)),
                                    int(precision), *outs, st), "bce_tiebreak_csr")

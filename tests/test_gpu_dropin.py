@@ -886,3 +886,29 @@ def test_tiebreak_full_tiles_vs_oracle(precision):
                 j = len(uniq) - 1
             ords.append(j)
         assert list(go[a:b]) == ords, m
+
+
+def test_tiebreak_max_len_skips_host_scan():
+    """batch.tiebreak(max_len=L): the caller's bound replaces the host scan of the offsets
+    (the bench's per-step path); outputs identical to the scanned call, and a market longer
+    than the bound is reported by the device fault word, not silently truncated."""
+    import torch
+    from bayesian_engine import _native as N
+    from bayesian_engine import batch
+    lens = np.full(64 * 6, 32, np.int64)
+    lens[100] = 7
+    off, pred, conf, weight, rel = _tb_inputs(lens, 31)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    d = [T(off), T(pred), T(conf), T(weight), T(rel)]
+    r1 = batch.tiebreak(*d, offsets_host=off)
+    r2 = batch.tiebreak(*d, max_len=32)
+    torch.cuda.synchronize()
+    for k in ("winner", "label", "n_groups", "variance", "g_key", "g_count", "g_density", "g_avgconf",
+              "g_maxrel", "g_of"):
+        assert getattr(r1, k).cpu().numpy().tobytes() == getattr(r2, k).cpu().numpy().tobytes(), k
+    N.check_faults(torch.device("cuda", 0), "max_len ok")
+    lens = np.array([32, 40, 3], np.int64)
+    off, pred, conf, weight, rel = _tb_inputs(lens, 32)
+    batch.tiebreak(T(off), T(pred), T(conf), T(weight), T(rel), max_len=32)
+    with pytest.raises(N.BCEError, match="longer than"):
+        N.check_faults(torch.device("cuda", 0), "max_len too small")

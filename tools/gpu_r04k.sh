@@ -1,14 +1,14 @@
 #!/bin/bash
-# Round 4: tie-break FULL kernel -- nontemporal load / store A/B, ticket-based PART 2 skip, next-tile offsets prefetch (tbnopre: off).
+# Round 4: tie-break FULL kernel -- L2 touch of the next phase array (tbnotouch: off), nontemporal (tbnont: off).
 
 set -u
-o=gpurun_out/r04j
+o=gpurun_out/r04k
 mkdir -p $o
 export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest tests/test_gpu_dropin.py -m gpu -x -q -k "tiebreak" --timeout 120 \
   --timeout-method thread > $o/pytest_tb.txt 2>&1 && \
 timeout -k 10 200 python3 bench.py --config tb --steps 20 --warmup 3 > $o/tb.json 2> $o/tb.err && \
-for v in tbnofull tbntld tbntst tbntboth tbnopre; do
+for v in tbnofull tbnont tbnotouch; do
   BCE_LIB=tools/ablate_build/$v/libbce_hip.so timeout -k 10 200 python3 bench.py --config tb --steps 20 --warmup 3 --no-cpu-baseline > $o/tb_$v.json 2> $o/tb_$v.err || exit 1
 done && \
 timeout -k 10 200 python3 bench.py --config tb --steps 20 --warmup 3 --no-cpu-baseline > $o/tb_again.json 2> $o/tb_again.err && \
