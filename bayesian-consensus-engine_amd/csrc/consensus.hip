@@ -1818,6 +1818,10 @@ extern "C" int bce_consensus_planned(const int64_t* offsets, int64_t n_markets, 
     ConsArgs a = base;
     a.list = order + bin_start_host[b0];
     a.n_list = bin_start_host[b + 1] - bin_start_host[b0];
+    if (b0 != b) {  // merged: this bin's (longer) markets first, then the bin below
+      a.list_hi = order + bin_start_host[b];
+      a.n_hi = bin_start_host[b + 1] - bin_start_host[b];
+    }
     if (a.n_list == 0) continue;
     hipStream_t sb = (b <= side_last) ? side : st;
     if (b <= 3 && seg_ok) {

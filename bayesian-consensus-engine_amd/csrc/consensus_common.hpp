@@ -19,6 +19,10 @@ struct ConsArgs {
   int64_t n_signals;
   const int32_t* list;  // nullable
   int64_t n_list;       // number of markets to process
+  // consensus_wide_kernel only: positions li < n_hi come from list_hi[li], the rest from
+  // list[li - n_hi] (EXACT's merged launch: the longer bin's markets first, longest-first overall)
+  const int32_t* list_hi;
+  int64_t n_hi;
   double* consensus;
   double* confidence;
   double* total_weight;

@@ -923,7 +923,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
   int vn = 0;
   auto refill = [&](int64_t base) {
     const int64_t li = base + G * lane;
-    vm = (li < a.n_list) ? (a.list ? a.list[li] : (int32_t)li) : 0;
+    vm = (li < a.n_list) ? (a.list ? (li < a.n_hi ? a.list_hi[li] : a.list[li - a.n_hi]) : (int32_t)li) : 0;
     voff = (li < a.n_list) ? a.offsets[vm] : 0;
     vn = (li < a.n_list) ? (int)(a.offsets[vm + 1] - voff) : 0;
   };
