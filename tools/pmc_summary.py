@@ -4,6 +4,10 @@
   python tools/pmc_summary.py stats <dir> <kernel-substring> [last]
       average duration (ms) from the *kernel_stats.csv of a --kernel-trace --stats run (and of
       the last `last` dispatches in the kernel trace: the timed steps)
+  python tools/pmc_summary.py span <dir> <kernel-substring> <kernels-per-step>
+      per-step span (first start to last end, ms) of a multi-kernel step from the kernel trace:
+      the matching dispatches in start order, chunked by kernels-per-step (side-stream kernels
+      overlap the main stream's, so per-kernel averages do not add up to the step)
   python tools/pmc_summary.py pmc <fetch-dir> <write-dir> <kernel-substring> <out.json> [k=v ...]
       (steps_total=N: sum every matching dispatch and divide by N -- per step of a
       multi-kernel config -- instead of averaging per dispatch)
@@ -68,7 +72,25 @@ def counter(d, kern, name, per_step=None):
     return sum(vals) / len(vals), len(vals)
 
 
+def span(d, kern, per_step):
+    rows = [r for r in _rows(d, "*kernel_trace.csv") if kern in r["Kernel_Name"] and "table_pack" not in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    out = []
+    for i in range(0, len(rows) - per_step + 1, per_step):
+        ch = rows[i:i + per_step]
+        if len({r["Kernel_Name"] for r in ch}) != per_step:
+            raise SystemExit(f"step {i // per_step}: kernels do not chunk by {per_step}")
+        out.append((max(int(r["End_Timestamp"]) for r in ch) - min(int(r["Start_Timestamp"]) for r in ch)) / 1e6)
+    srt = sorted(out)
+    return {"kernel_substring": kern, "kernels_per_step": per_step, "steps": len(out),
+            "median_span_ms": srt[len(srt) // 2], "mean_span_ms": sum(out) / len(out),
+            "mean_span_ms_last_50": sum(out[-50:]) / len(out[-50:])}
+
+
 def main():
+    if sys.argv[1] == "span":
+        print(json.dumps(span(sys.argv[2], sys.argv[3], int(sys.argv[4]))))
+        return
     if sys.argv[1] == "stats":
         ms, calls, name, every = stats(sys.argv[2], sys.argv[3])
         out = {"kernel": name, "avg_ms": ms, "calls": calls}
