@@ -269,8 +269,10 @@ constexpr int kTbDump = 64;
 constexpr int kTbFullBatchPC = 8;
 constexpr bool kTbPrefetchMeta = true;
 // FULL tiles: while a phase computes, two dword loads per lane pull the next phase's 16-KB
-// array into L2 (its 128 lines), so the stage that follows finds it there
-constexpr bool kTbTouchNext = true;
+// array into L2 (its 128 lines), so the stage that follows finds it there.  Off: -0.5% time
+// (0.706 vs 0.709-0.711 ms, profiles/r04k/) for FETCH_SIZE +27% (the dword touches are
+// tallied like gathers, so the line's PMC traffic stops meaning HBM bytes, profiles/r04m/).
+constexpr bool kTbTouchNext = false;
 // nontemporal hints on the staged input loads / the flushed output stores (both off: 0.727-0.730
 // ms vs 0.712 for the 1M x 32 line, profiles/r04j/)
 constexpr bool kTbNtLoad = true;

@@ -67,7 +67,7 @@ VARIANTS = {
     "tbnont": [("tiebreak.hip", "constexpr bool kTbNtLoad = true;", "constexpr bool kTbNtLoad = false;"),
                ("tiebreak.hip", "constexpr bool kTbNtStore = true;", "constexpr bool kTbNtStore = false;")],
     "tbnopre": [("tiebreak.hip", "constexpr bool kTbPrefetchMeta = true;", "constexpr bool kTbPrefetchMeta = false;")],
-    "tbnotouch": [("tiebreak.hip", "constexpr bool kTbTouchNext = true;", "constexpr bool kTbTouchNext = false;")],
+    "tbtouch": [("tiebreak.hip", "constexpr bool kTbTouchNext = false;", "constexpr bool kTbTouchNext = true;")],
     "tbkvsort": [("tiebreak.hip", "constexpr bool kTbFullKeysInLds = true;", "constexpr bool kTbFullKeysInLds = false;")],
     "tbnofull": [("tiebreak.hip", "const bool split = kTbStageMode != 2 && !EXOTIC && a.rmode == 0 && al16(a.pred)",
                   "const bool split = false && al16(a.pred)")],
