@@ -49,7 +49,7 @@ struct DevCtx {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int* queue = nullptr;               // kQueueSlots pairs of team-kernel queue words
   std::atomic<unsigned> queue_next{0};
-  int* split = nullptr;               // kQueueSlots tie-break FULL/rest ticket words
+  int* split = nullptr;               // kQueueSlots blocks of kSplitWords tie-break ticket words
   std::atomic<unsigned> split_next{0};
 };
 constexpr int kQueueSlots = 64;
@@ -73,8 +73,8 @@ DevCtx* dev_ctx() {
     if (e == hipSuccess) e = hipMemset(qw, 0, 2 * kQueueSlots * sizeof(int));
     if (e == hipSuccess) c->queue = qw;
     int* sw = nullptr;
-    if (e == hipSuccess) e = hipMalloc((void**)&sw, kQueueSlots * sizeof(int));
-    if (e == hipSuccess) e = hipMemset(sw, 0, kQueueSlots * sizeof(int));
+    if (e == hipSuccess) e = hipMalloc((void**)&sw, (size_t)kQueueSlots * kSplitWords * sizeof(int));
+    if (e == hipSuccess) e = hipMemset(sw, 0, (size_t)kQueueSlots * kSplitWords * sizeof(int));
     if (e == hipSuccess) c->split = sw;
     c->init_err = e;
     if (e == hipSuccess) c->fault = p;
@@ -112,7 +112,7 @@ int* split_slot() {
   DevCtx* c = dev_ctx();
   if (!c || !c->split) return nullptr;
   // tickets make reuse safe: a launch pair only reacts to its own ticket
-  return c->split + (c->split_next.fetch_add(1) % kQueueSlots);
+  return c->split + (size_t)(c->split_next.fetch_add(1) % kQueueSlots) * kSplitWords;
 }
 
 int* fault_word() {

@@ -177,7 +177,9 @@ int launch_wide_team(const ConsArgs& a, const int64_t* bin_start_host, hipStream
 // Two zeroed device ints for one team-kernel launch (a ring of slots per device; the kernel
 // leaves its pair zeroed when it finishes).
 int* team_queue_slot();
-// one word for a tie-break FULL/rest launch pair (tiebreak.hip; written with a per-launch ticket)
+// kSplitWords words (one per wave of the grid) for a tie-break FULL/rest launch pair
+// (tiebreak.hip; written with a per-launch ticket)
+constexpr int kSplitWords = 4096;
 int* split_slot();
 
 }  // namespace bce

@@ -45,7 +45,8 @@ struct TbArgs {
                    // 4: big-integer path 23 <= nd <= 323, 5: big-integer path -308 <= nd <= -16
   int rnd;         // ndigits (modes 4, 5)
   int* fault;      // device fault word: kFaultRoundOverflow (CPython's OverflowError)
-  int* split;      // PART 1/2 launches: PART 1 writes `ticket` here when it leaves a tile to PART 2
+  int* split;      // PART 1/2 launches: one word per wave of the (shared) grid; a PART 1 wave
+                   // that leaves a tile to PART 2 writes `ticket` into its word
   int ticket;      // this launch pair's number (host counter, never 0): no reset needed
 };
 
@@ -320,8 +321,9 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
   __shared__ double sBuf[STAGED ? kTbLpmWaves : 1][DB ? 2 : 1][STAGED ? kTbStage + kTbDump : 1];
   // FULL tiles: RN(1 / c) for group sizes c = 1..32 (tb_div_small)
   constexpr bool kFullBody = PART == 1;
-  __shared__ double sRc[kFullBody ? kTbLpmMax + 1 : 1];
-  if constexpr (kFullBody) {
+  constexpr bool kRcTab = STAGED && !DB;  // group means via the reciprocal table
+  __shared__ double sRc[kRcTab ? kTbLpmMax + 1 : 1];
+  if constexpr (kRcTab) {
     if (threadIdx.x <= (unsigned)kTbLpmMax) sRc[threadIdx.x] = 1.0 / (double)(threadIdx.x ? threadIdx.x : 1);
     __syncthreads();
   }
@@ -419,7 +421,10 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
   // it then only counts itself out
   bool run = true;
   int pfsink = 0;  // kTbTouchNext: consumes the touch loads
-  if constexpr (PART == 2) run = __hip_atomic_load(a.split, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.ticket;
+  // (one word per wave: a single flag word took every skipping wave's store through the
+  // device-coherent path to one address -- 0.55 ms of serialised stores on a ragged batch)
+  if constexpr (PART == 2) run = a.split[wave] == a.ticket;
+  bool left = false;  // PART 1: this wave left a tile to PART 2
   for (int64_t tile = wave; run && tile * 64 < n_list; tile += nwaves) {
     Meta nxt{};
     if constexpr (DB) {
@@ -430,7 +435,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     }
     if constexpr (PART == 1) {
       if (!cur.full) {  // (skipped tiles are never full)
-        if (lane == 0) __hip_atomic_store(a.split, a.ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        left = true;
         continue;
       }
     } else if constexpr (PART == 2) {
@@ -567,13 +572,12 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
       if constexpr (STAGED) ibuf[tb_pad(lrow + g)] = v;
       else dst[off + g] = v;
     };
-    auto run_start = [&](const unsigned (&u)[kTbLpmMax], int p) {
-      return (p == 0) || ((u[p] >> 5) != (u[p > 0 ? p - 1 : 0] >> 5));
-    };
-    auto run_end = [&](const unsigned (&u)[kTbLpmMax], int p) {
-      return (p + 1 >= n) || ((u[p] >> 5) != (u[p + 1 < kTbLpmMax ? p + 1 : p] >> 5));
-    };
     const double nd = (double)(n > 0 ? n : 1);
+    // a group mean: the reciprocal-table quotient where the table exists, else IEEE division
+    auto tb_div_cnt = [&](double x, int c, const double* tab) -> double {
+      if constexpr (kRcTab) return tb_div_small(x, c, tab);
+      else return x / (double)c;
+    };
 
     // ---- FULL tile: 64 markets of exactly kTbLpmMax agents, lane L's row at 33 L ------------
     // The same four phases as below with n a compile-time 32: no per-position validity masks,
@@ -795,9 +799,18 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     }
 
     // ---- 1. keys, group ordinals (first-seen order), sort with the key as payload ---------
+    // Per-lane validity is the bit set vm (bit t: t < n) and run boundaries are stm / enm
+    // (bit p: a run starts / ends at sorted position p), each re-derived per phase through an
+    // empty asm: kept as 32 lane masks they held 64 SGPRs through the tile and spilled.
     unsigned u[kTbLpmMax];
     double kp[kTbLpmMax];
     int ng = 0;
+    const unsigned vm = (n >= kTbLpmMax) ? ~0u : ((1u << (n > 0 ? n : 0)) - 1u);
+    auto vbit = [](unsigned bits, int p) { return ((bits >> p) & 1u) != 0u; };
+    auto refresh_ug = [&]() {
+#pragma unroll
+      for (int p = 0; p < kTbLpmMax; ++p) u[p] = tb_bits(u[p]);
+    };
     if constexpr (DB) {
       dma_arr(a.weight, 1, cur);  // streams in under phase 1
       tb_wait_dma_but_next();     // the predictions are in buffer 0
@@ -807,55 +820,74 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     }
     const double praw0 = at(a.pred, 0);  // a single agent keeps its raw prediction (tiebreak.py:89-96)
     {
+      if (!EXOTIC && a.rmode == 0) {  // the common precisions: rint fast path, exact redo if flagged
 #pragma unroll
-      for (int t = 0; t < kTbLpmMax; ++t) kp[t] = tb_round<EXOTIC>(at(a.pred, min(t, last)), a);
+        for (int t = 0; t < kTbLpmMax; ++t) {
+          const double x = at(a.pred, min(t, last));
+          bool slow;
+          kp[t] = py_round_nd_fast(x, a.rscale, a.rinv, a.rthresh, slow);
+          if (ballot(slow)) kp[t] = slow ? py_round_nd_sel(x, a.rscale, a.rinv, a.rthresh) : kp[t];
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < kTbLpmMax; ++t) kp[t] = tb_round<EXOTIC>(at(a.pred, min(t, last)), a);
+      }
+      const unsigned vm1 = tb_bits(vm);
       int go[kTbLpmMax];
 #pragma unroll
       for (int t = 0; t < kTbLpmMax; ++t) {
         int g = -1;
 #pragma unroll
         for (int s2 = 0; s2 < t; ++s2) g = key_eq(kp[s2], kp[t]) ? go[s2] : g;  // earlier equal key: its group
-        const bool fresh = (t < n) && g < 0;
+        const bool fresh = vbit(vm1, t) && g < 0;
         go[t] = fresh ? ng : g;
         ng += fresh ? 1 : 0;
-        u[t] = (t < n) ? (((unsigned)go[t] << 5) | (unsigned)t) : 0xFFFFFFFFu;
+        u[t] = vbit(vm1, t) ? (((unsigned)go[t] << 5) | (unsigned)t) : 0xFFFFFFFFu;
       }
       if (a.g_of) {  // agent t's prediction (slot t) is consumed: the ordinals go in place
         if constexpr (STAGED) wave_sync_lds();
+        const unsigned vm2 = tb_bits(vm);
 #pragma unroll
         for (int t = 0; t < kTbLpmMax; ++t)
-          if (t < n) put_i32(a.g_of, t, go[t]);
+          if (vbit(vm2, t)) put_i32(a.g_of, t, go[t]);
         if constexpr (STAGED) flush_i32(a.g_of);
       }
     }
     oem_sort_kv(u, kp);
+    // run boundaries from the sorted keys alone (invalid positions hold 0xFFFFFFFF, sorted
+    // last: the last valid position ends its run, no invalid position ends one)
+    unsigned stm = 1u, enm = (u[kTbLpmMax - 1] != 0xFFFFFFFFu) ? (1u << (kTbLpmMax - 1)) : 0u;
+#pragma unroll
+    for (int p = 1; p < kTbLpmMax; ++p) {
+      const unsigned d = ((u[p] >> 5) != (u[p - 1] >> 5)) ? 1u : 0u;
+      stm |= d << p;
+      enm |= d << (p - 1);
+    }
+    enm &= vm;
     // every member carries its run head's key: a group's dict key is its FIRST member's
     // rounded prediction (tiebreak.py:54-55), and -0.0 / 0.0 share a group with different bits
 #pragma unroll
-    for (int p = 1; p < kTbLpmMax; ++p) kp[p] = run_start(u, p) ? kp[p] : kp[p - 1];
+    for (int p = 1; p < kTbLpmMax; ++p) kp[p] = vbit(stm, p) ? kp[p] : kp[p - 1];
 
     // ---- 2. group keys and counts (registers only) ------------------------------------------
     if (a.g_key || a.g_count) {
-      int cnt = 0;
+      if (a.g_key) {
+        const unsigned en_ = tb_bits(enm);
+        refresh_ug();
 #pragma unroll
-      for (int p = 0; p < kTbLpmMax; ++p) {
-        if (p < n) {
-          cnt = (run_start(u, p) ? 0 : cnt) + 1;
-          if (run_end(u, p) && a.g_key) put(a.g_key, (int)(u[p] >> 5), (n == 1) ? praw0 : kp[p]);
-        }
-      }
-      if constexpr (STAGED) {
-        if (a.g_key) flush(a.g_key);
+        for (int p = 0; p < kTbLpmMax; ++p)
+          if (vbit(en_, p)) put(a.g_key, (int)(u[p] >> 5), (n == 1) ? praw0 : kp[p]);
+        if constexpr (STAGED) flush(a.g_key);
       }
       if (a.g_count) {
         if constexpr (STAGED) wave_sync_lds();
-        cnt = 0;
+        const unsigned st_ = tb_bits(stm), en_ = tb_bits(enm);
+        refresh_ug();
+        int cnt = 0;
 #pragma unroll
         for (int p = 0; p < kTbLpmMax; ++p) {
-          if (p < n) {
-            cnt = (run_start(u, p) ? 0 : cnt) + 1;
-            if (run_end(u, p)) put_i32(a.g_count, (int)(u[p] >> 5), cnt);
-          }
+          cnt = (vbit(st_, p) ? 0 : cnt) + 1;
+          if (vbit(en_, p)) put_i32(a.g_count, (int)(u[p] >> 5), cnt);
         }
         if constexpr (STAGED) flush_i32(a.g_count);
       }
@@ -864,6 +896,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     // ---- 3. weights: group densities, kept per run end for the winner -----------------------
     // A group's outputs overwrite slot g of its market's row in place: group g ends only after
     // every group <= g, and agent g (ordinal <= g) belongs to one of those -- consumed.
+    // (Positions past n read slot min(31, ...) of the lane's row or the tile's slack: never used.)
     double densp[kTbLpmMax];
     if constexpr (DB) {
       dma_arr(a.rel, 0, cur);
@@ -873,19 +906,18 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
       stage(a.weight);
     }
     {
+      const unsigned st_ = tb_bits(stm), en_ = tb_bits(enm);
+      refresh_ug();
       double tot = 0.0;
       int cnt = 0;
 #pragma unroll
       for (int p = 0; p < kTbLpmMax; ++p) {
-        densp[p] = 0.0;
-        if (p < n) {
-          const int t = (int)(u[p] & 31u);
-          const bool st = run_start(u, p);
-          tot = (st ? 0.0 : tot) + at(a.weight, t);  // tiebreak.py:60, sum from int 0
-          cnt = (st ? 0 : cnt) + 1;
-          densp[p] = tot / (double)cnt;
-          if (run_end(u, p) && a.g_density) put(a.g_density, (int)(u[p] >> 5), densp[p]);
-        }
+        const int t = min((int)(u[p] & 31u), last);
+        const bool st = vbit(st_, p);
+        tot = (st ? 0.0 : tot) + at(a.weight, t);  // tiebreak.py:60, sum from int 0
+        cnt = (st ? 0 : cnt) + 1;
+        densp[p] = tb_div_cnt(tot, cnt, sRc);
+        if (vbit(en_, p) && a.g_density) put(a.g_density, (int)(u[p] >> 5), densp[p]);
       }
       if constexpr (STAGED) {
         if (a.g_density) flush(a.g_density);
@@ -903,24 +935,24 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
       stage(a.rel);
     }
     {
+      const unsigned st_ = tb_bits(stm), en_ = tb_bits(enm);
+      refresh_ug();
       double mx = 0.0;
 #pragma unroll
       for (int p = 0; p < kTbLpmMax; ++p) {
-        if (p < n) {
-          const int t = (int)(u[p] & 31u);
-          const unsigned g = u[p] >> 5;
-          const double r = at(a.rel, t);
-          mx = run_start(u, p) ? r : ((r > mx) ? r : mx);  // tiebreak.py:62
-          if (run_end(u, p)) {
-            if (a.g_maxrel) put(a.g_maxrel, (int)g, mx);
-            const double key = (n == 1) ? praw0 : kp[p], dens = densp[p];
-            const bool same = (dens == bd) && (mx == bm);
-            if (g == 0 || tb_better(dens, mx, key, bd, bm, bk)) {  // tiebreak.py:113-117
-              tie = (g != 0) && same;
-              bd = dens; bm = mx; bk = key;
-            } else {
-              tie = tie || same;  // tiebreak.py:123-133: does another group tie the winner?
-            }
+        const int t = min((int)(u[p] & 31u), last);
+        const unsigned g = u[p] >> 5;
+        const double r = at(a.rel, t);
+        mx = vbit(st_, p) ? r : ((r > mx) ? r : mx);  // tiebreak.py:62
+        if (vbit(en_, p)) {
+          if (a.g_maxrel) put(a.g_maxrel, (int)g, mx);
+          const double key = (n == 1) ? praw0 : kp[p], dens = densp[p];
+          const bool same = (dens == bd) && (mx == bm);
+          if (g == 0 || tb_better(dens, mx, key, bd, bm, bk)) {  // tiebreak.py:113-117
+            tie = (g != 0) && same;
+            bd = dens; bm = mx; bk = key;
+          } else {
+            tie = tie || same;  // tiebreak.py:123-133: does another group tie the winner?
           }
         }
       }
@@ -943,44 +975,47 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     }
     double variance;
     {
+      const unsigned vm5 = tb_bits(vm);
       double cs = 0.0;
 #pragma unroll
-      for (int t = 0; t < kTbLpmMax; ++t) cs += (t < n) ? at(a.conf, t < n ? t : last) : 0.0;
+      for (int t = 0; t < kTbLpmMax; ++t) cs += vbit(vm5, t) ? at(a.conf, min(t, last)) : 0.0;
       const double mean = cs / nd;
-      // squares: pow(d, 2.0) restated (glibc_pow.hpp); the exact fast path first, the few
-      // near-midpoint squares (a bit in `slow`) redone one per lane per round afterwards
-      double sq[kTbLpmMax];
+      // squares: pow(d, 2.0) restated (glibc_pow.hpp), summed as they come; a lane with a
+      // near-midpoint square (a bit in `slow`) redoes its ordered sum with the exact ones
+      if constexpr (STAGED) wave_sync_lds();  // re-read the confidences instead of holding them
+      const unsigned vm6 = tb_bits(vm);
+      double vs = 0.0;
       unsigned slow = 0;
 #pragma unroll
       for (int t = 0; t < kTbLpmMax; ++t) {
-        const double d = at(a.conf, t < n ? t : last) - mean;
         bool ok;
-        sq[t] = bce_pow::pow2_fast(d, ok);
-        slow |= ((t < n) && !ok) ? (1u << t) : 0u;
+        const double q = bce_pow::pow2_fast(at(a.conf, min(t, last)) - mean, ok);
+        vs += vbit(vm6, t) ? q : 0.0;
+        slow |= (vbit(vm6, t) && !ok) ? (1u << t) : 0u;
       }
-      while (ballot(slow != 0u)) {
-        const int t1 = slow ? (int)__builtin_ctz(slow) : 0;
-        slow &= slow - 1u;
-        const double v = bce_pow::pow2_full(at(a.conf, t1) - mean);
-#pragma unroll
-        for (int t = 0; t < kTbLpmMax; ++t) sq[t] = (t == t1) ? v : sq[t];
+      if (slow) {
+        vs = 0.0;
+#pragma unroll 1
+        for (int t = 0; t < n; ++t) {
+          const double d = at(a.conf, t) - mean;
+          bool ok;
+          const double q = bce_pow::pow2_fast(d, ok);
+          vs += ((slow >> t) & 1u) ? tb_pow2_full(d) : q;
+        }
       }
-      double vs = 0.0;
-#pragma unroll
-      for (int t = 0; t < kTbLpmMax; ++t) vs += (t < n) ? sq[t] : 0.0;
       variance = vs / nd;
     }
     if (a.g_avgconf) {
+      const unsigned st_ = tb_bits(stm), en_ = tb_bits(enm);
+      refresh_ug();
       double gcs = 0.0;
       int cnt = 0;
 #pragma unroll
       for (int p = 0; p < kTbLpmMax; ++p) {
-        if (p < n) {
-          const bool st = run_start(u, p);
-          gcs = (st ? 0.0 : gcs) + at(a.conf, (int)(u[p] & 31u));  // tiebreak.py:61
-          cnt = (st ? 0 : cnt) + 1;
-          if (run_end(u, p)) put(a.g_avgconf, (int)(u[p] >> 5), gcs / (double)cnt);
-        }
+        const bool st = vbit(st_, p);
+        gcs = (st ? 0.0 : gcs) + at(a.conf, min((int)(u[p] & 31u), last));  // tiebreak.py:61
+        cnt = (st ? 0 : cnt) + 1;
+        if (vbit(en_, p)) put(a.g_avgconf, (int)(u[p] >> 5), tb_div_cnt(gcs, cnt, sRc));
       }
       if constexpr (STAGED) flush(a.g_avgconf);
     }
@@ -1000,6 +1035,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
   }
   if constexpr (DB) tb_wait_dma_all();  // no DMA outlives the wave
   if (PART == 1 && pfsink == 0x5bd1e995 && n_list < 0) a.label[0] = pfsink;  // never: keeps the touches
+  if (PART == 1 && left && lane == 0) a.split[wave] = a.ticket;
 }
 
 // n > 64: one workgroup per market.  (rounded key, index) pairs are bitonic-sorted in
@@ -1232,14 +1268,15 @@ static int launch_tb_short(const TbArgs& a, const int32_t* market_list, int64_t 
     // run a kernel specialised for them, then a second launch takes every other tile (each
     // launch only reads the offsets of the tiles it leaves to the other)
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-    const bool split = kTbStageMode != 2 && !EXOTIC && a.rmode == 0 && al16(a.pred) && al16(a.conf) &&
-                       al16(a.weight) && al16(a.rel);
+    bool split = kTbStageMode != 2 && !EXOTIC && a.rmode == 0 && al16(a.pred) && al16(a.conf) &&
+                 al16(a.weight) && al16(a.rel);
     const void* fn = market_list ? reinterpret_cast<const void*>(&tiebreak_lpm_kernel<false, EXOTIC>)
                      : split     ? reinterpret_cast<const void*>(&tiebreak_lpm_kernel<true, false, 1>)
                                  : reinterpret_cast<const void*>(&tiebreak_lpm_kernel<true, EXOTIC>);
     const int per_cu = blocks_per_cu(fn, 64 * kTbLpmWaves, 0, 1, "tiebreak_lpm_kernel");
     const int64_t cap = (int64_t)cu_count() * per_cu;
     if (blocks > cap) blocks = cap;
+    split = split && blocks * kTbLpmWaves <= kSplitWords;  // one split word per wave of the grid
     hipStream_t st = as_stream(stream);
     const dim3 grid((int)blocks), block(64 * kTbLpmWaves);
     if (market_list) {

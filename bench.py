@@ -61,6 +61,7 @@ def parse(argv=None):
     p.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5", "ns", "agg", "tb"])
     p.add_argument("--markets", type=int, default=1_000_000)
     p.add_argument("--len", type=int, default=32)
+    p.add_argument("--ragged", action="store_true", help="tb: market lengths uniform on 1..--len")
     p.add_argument("--sources", type=int, default=10_000)
     p.add_argument("--mode", default=None, choices=["exact", "fast"],
                    help="consensus summation mode (default: exact for c2, where it costs nothing; fast -- "

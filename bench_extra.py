@@ -800,6 +800,12 @@ def _tb(args, world, rank, barrier, max_over, sum_over):
 
     M, L, S = args.markets, args.len, args.sources
     off, sid, prob, rel_t, conf_t, present = make_c2(M, L, S, seed=2 + rank)
+    ragged = bool(getattr(args, "ragged", False))
+    if ragged:  # lengths uniform on 1..L: the general (non-FULL) lane kernel takes every tile
+        lens = np.random.default_rng(20 + rank).integers(1, L + 1, M).astype(np.int64)
+        off = np.zeros(M + 1, np.int64)
+        off[1:] = np.cumsum(lens)
+        sid, prob = sid[:off[-1]], prob[:off[-1]]
     pred, conf, rel = prob, conf_t[sid], rel_t[sid]
     weight = rel
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -811,7 +817,7 @@ def _tb(args, world, rank, barrier, max_over, sum_over):
         batch.tiebreak(*d, offsets_host=off, out=res, max_len=L)
 
     wall, per = _timed(step, args, world, torch.cuda.current_stream(dev), barrier, max_over)
-    n = M * L
+    n = int(off[-1])
     ng = res.n_groups.cpu().numpy().astype(np.int64)
     sum_g = int(ng.sum())
     # in: pred, conf, weight, rel (32 B per agent) + offsets; out per market: winner,
@@ -839,14 +845,16 @@ def _tb(args, world, rank, barrier, max_over, sum_over):
     N.check_faults(dev, "tb timed steps")
     tot = sum_over(float(n * args.steps), world)
     return {
-        "metric": "signals tie-broken/sec (node), DeterministicTieBreaker.resolve over 1M markets x 32 agents",
+        "metric": ("signals tie-broken/sec (node), DeterministicTieBreaker.resolve over 1M ragged markets"
+                   if ragged else "signals tie-broken/sec (node), DeterministicTieBreaker.resolve over 1M markets x 32 agents"),
         "value": tot / wall, "unit": "signals/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f64", "data": "synthetic (the c2 batch; 10% grid markets force ties)",
-        "config": {"workload": f"tb: {M} markets x {L} agents, precision 6", "groups_per_market_mean": sum_g / M,
+        "config": {"workload": (f"tb: {M} markets x 1..{L} agents (ragged), precision 6" if ragged else
+                                f"tb: {M} markets x {L} agents, precision 6"), "groups_per_market_mean": sum_g / M,
                    "parallelism": f"markets sharded over {world} rank(s), no collective"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc("pmc_tb.json", markets=M),
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None if ragged else _pmc("pmc_tb.json", markets=M),
                      "kernel": "tiebreak_lpm_kernel" if L <= 32 else "tiebreak_wave_kernel", "bytes_per_launch": bytes_step, "avg_launch_ms": per * 1e3},
         "cpu_baseline": cpu_line,
         "parity_vs_oracle": parity,

@@ -912,3 +912,38 @@ def test_tiebreak_max_len_skips_host_scan():
     batch.tiebreak(T(off), T(pred), T(conf), T(weight), T(rel), max_len=32)
     with pytest.raises(N.BCEError, match="longer than"):
         N.check_faults(torch.device("cuda", 0), "max_len too small")
+
+
+@pytest.mark.parametrize("precision", [6, 0, -2, 30])
+def test_tiebreak_ragged_lane_kernel_vs_oracle(precision):
+    """Markets of 0..32 agents (every tile ragged: the general lane-per-market body, PART 2 of
+    the split launch or the only launch for the exotic precisions) with adversarial values:
+    every output bit-exact against the oracle fed Python's own round() keys."""
+    import torch
+    from bayesian_engine import batch
+    from oracle import oracle as orc
+    rng = np.random.default_rng(1200 + precision)
+    lens = rng.integers(0, 33, 64 * 24).astype(np.int64)
+    off, pred, conf, weight, rel = _tb_inputs(lens, 1300 + precision)
+    n = len(pred)
+    pred = np.where(rng.random(n) < 0.1, (rng.integers(-500, 500, n) + 0.5) * 10.0 ** -max(precision, 0), pred)
+    pred[rng.random(n) < 0.005] = np.nan
+    weight[rng.random(n) < 0.01] = 0.0
+    keys = np.array([round(float(x), precision) for x in pred], np.float64)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    r = batch.tiebreak(T(off), T(pred), T(conf), T(weight), T(rel), precision=precision, max_len=32)
+    torch.cuda.synchronize()
+    exp = orc.tiebreak_csr(off, pred, conf, weight, rel, keys=keys)
+    for k in ("winner", "label", "n_groups", "variance"):
+        got = getattr(r, k).cpu().numpy()
+        assert got.tobytes() == exp[k].astype(got.dtype).tobytes(), k
+    gk, gc, ga, gm = (x.cpu().numpy() for x in (r.g_key, r.g_count, r.g_avgconf, r.g_maxrel))
+    for m in range(len(lens)):
+        a, g = int(off[m]), int(exp["n_groups"][m])
+        if lens[m] == 0:
+            continue
+        sl = slice(a, a + g)
+        assert gk[sl].tobytes() == exp["g_key"][sl].tobytes(), m
+        assert np.array_equal(gc[sl], exp["g_count"][sl]), m
+        assert ga[sl].tobytes() == exp["g_avgconf"][sl].tobytes(), m
+        assert gm[sl].tobytes() == exp["g_maxrel"][sl].tobytes(), m
