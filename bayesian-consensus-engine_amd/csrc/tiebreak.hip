@@ -265,9 +265,11 @@ constexpr bool kTbDMA = kTbStageMode == 2;
 __device__ __forceinline__ int tb_pad(int i) { return i + (i >> 5); }
 constexpr bool kTbFullKeysInLds = true;  // FULL tiles: sort (ordinal, agent) alone, keys via LDS
 constexpr int kTbDump = 64;
-// FULL tiles: 16-B loads per lane in flight while staging the predictions / confidences (few
-// registers live then; the weights / reliabilities, with keys and densities live, use stage())
+// FULL tiles: 16-B loads per lane in flight while staging the predictions / confidences and the
+// weights / reliabilities (8 for the latter spills ~10 VGPRs around those stages and still
+// wins: 0.662 vs 0.688 ms with stage()'s 4, profiles/r04q/)
 constexpr int kTbFullBatchPC = 8;
+constexpr int kTbFullBatchWR = 8;
 constexpr bool kTbPrefetchMeta = true;
 // FULL tiles: while a phase computes, two dword loads per lane pull the next phase's 16-KB
 // array into L2 (its 128 lines), so the stage that follows finds it there.  Off: -0.5% time
@@ -698,7 +700,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
         // 3. densities
         double densp[N];
         settle();
-        stage(a.weight);
+        stage_full(a.weight, std::integral_constant<int, kTbFullBatchWR>{});
         touch(a.rel);
         {
           const unsigned st_ = tb_bits(stm), en_ = tb_bits(enm);
@@ -719,7 +721,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
         double bd = 0.0, bm = 0.0, bk = 0.0;
         bool tie = false;
         settle();
-        stage(a.rel);
+        stage_full(a.rel, std::integral_constant<int, kTbFullBatchWR>{});
         touch(a.conf);
         {
           const unsigned st_ = tb_bits(stm), en_ = tb_bits(enm);

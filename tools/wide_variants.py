@@ -68,6 +68,11 @@ VARIANTS = {
                ("tiebreak.hip", "constexpr bool kTbNtStore = true;", "constexpr bool kTbNtStore = false;")],
     "tbnopre": [("tiebreak.hip", "constexpr bool kTbPrefetchMeta = true;", "constexpr bool kTbPrefetchMeta = false;")],
     "tbtouch": [("tiebreak.hip", "constexpr bool kTbTouchNext = false;", "constexpr bool kTbTouchNext = true;")],
+    # FULL tiles: staging batches (shipped: 8 and 8)
+    "tbwr4": [("tiebreak.hip", "constexpr int kTbFullBatchWR = 8;", "constexpr int kTbFullBatchWR = 4;")],
+    "tbwr16": [("tiebreak.hip", "constexpr int kTbFullBatchWR = 8;", "constexpr int kTbFullBatchWR = 16;")],
+    "tbpc16wr16": [("tiebreak.hip", "constexpr int kTbFullBatchWR = 8;", "constexpr int kTbFullBatchWR = 16;"),
+                   ("tiebreak.hip", "constexpr int kTbFullBatchPC = 8;", "constexpr int kTbFullBatchPC = 16;")],
     "tbkvsort": [("tiebreak.hip", "constexpr bool kTbFullKeysInLds = true;", "constexpr bool kTbFullKeysInLds = false;")],
     "tbnofull": [("tiebreak.hip", "const bool split = kTbStageMode != 2 && !EXOTIC && a.rmode == 0 && al16(a.pred)",
                   "const bool split = false && al16(a.pred)")],
