@@ -14,4 +14,5 @@ bash tools/gpu_profile.sh tb "tiebreak_lpm_kernel<true, false, 1>" markets=10000
 bash tools/gpu_profile.sh c5 reestimate_consensus_votes_kernel markets_this_rank=1000000 mode=exact -- --config c5 --steps 2 --warmup 1 --single-mode && \
 python3 tools/pmc_summary.py stats gpurun_out/prof_c5/stats reestimate_agreement_votes_kernel > gpurun_out/prof_c5/stats_agreement.json && \
 python3 tools/pmc_summary.py pmc gpurun_out/prof_c5/fetch gpurun_out/prof_c5/write reestimate_agreement_votes_kernel \
-  gpurun_out/prof_c5/pmc_agreement.json markets_this_rank=1000000
+  gpurun_out/prof_c5/pmc_agreement.json markets_this_rank=1000000 && \
+python3 tools/roofline_check.py gpurun_out > gpurun_out/roofline_check.txt
