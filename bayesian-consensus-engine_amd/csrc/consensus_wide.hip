@@ -367,9 +367,14 @@ __device__ __forceinline__ int sq_addr(int q) {
   else return q;
 }
 
+// FAST: run averages and normalizedWeight by reciprocal products instead of IEEE divisions
+// (a few ulps; FAST's contract is 1e-9 relative)
+constexpr bool kWideFastRecip = true;
+
 // builtin sum() from 0 over a run of len sorted probabilities in input order (core.py:116);
 // terms past the run add +0.0, exact since the sum starts at +0.0 and is never -0.0.
-template <int R>
+// APPROX (FAST): the average as sum * (1/len) -- v_rcp_f64 refined by one Newton step.
+template <int R, bool APPROX = false>
 __device__ __forceinline__ double run_sum(const double* sA, int q0, int len) {
   double x[4];
 #pragma unroll
@@ -394,7 +399,14 @@ __device__ __forceinline__ double run_sum(const double* sA, int q0, int len) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) sum += (e0 + e < len) ? xa[e] : 0.0;
   }
-  return (len > 1) ? sum / (double)len : sum;
+  if constexpr (APPROX) {
+    const double c = (double)len;
+    double y = __builtin_amdgcn_rcp(c);
+    y = __builtin_fma(__builtin_fma(-c, y, 1.0), y, y);
+    return (len > 1) ? sum * y : sum;
+  } else {
+    return (len > 1) ? sum / (double)len : sum;
+  }
 }
 
 // acc += src[0] + src[1] + ... + src[ce-1], left to right (the reference's chains,
@@ -765,7 +777,7 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
       if constexpr (FAST) {
         // runs longer than kWaveRun (hot sources) are summed by the whole wave in a fixed
         // order instead of by their own lane, so one hot source does not hold the wave
-        avg = (jj < u && len <= kWaveRun) ? run_sum<R>(sA, q0s[i], len) : 0.0;
+        avg = (jj < u && len <= kWaveRun) ? run_sum<R, kWideFastRecip>(sA, q0s[i], len) : 0.0;
         unsigned long long lm = ballot(jj < u && len > kWaveRun);
         while (lm) {
           const int LL = __builtin_ctzll(lm);
@@ -886,6 +898,7 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
       }
     } else {
       constexpr int NB = (kWideNWBF < R) ? kWideNWBF : R;  // read-backs per batch
+      const double rtw = (tw > 0.0) ? 1.0 / tw : 0.0;
       for (int j0 = t; j0 < u; j0 += NB * NT) {
         double wj[NB];
 #pragma unroll
@@ -896,7 +909,8 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
 #pragma unroll
         for (int k = 0; k < NB; ++k) {
           const int jj = j0 + NT * k;
-          if (jj < u) __builtin_nontemporal_store((tw > 0.0) ? wj[k] / tw : 0.0, &a.nweight[off + jj]);
+          const double nw = kWideFastRecip ? ((tw > 0.0) ? wj[k] * rtw : 0.0) : ((tw > 0.0) ? wj[k] / tw : 0.0);
+          if (jj < u) __builtin_nontemporal_store(nw, &a.nweight[off + jj]);
         }
       }
     }

@@ -73,6 +73,7 @@ VARIANTS = {
     "tbwr16": [("tiebreak.hip", "constexpr int kTbFullBatchWR = 8;", "constexpr int kTbFullBatchWR = 16;")],
     "tbpc16wr16": [("tiebreak.hip", "constexpr int kTbFullBatchWR = 8;", "constexpr int kTbFullBatchWR = 16;"),
                    ("tiebreak.hip", "constexpr int kTbFullBatchPC = 8;", "constexpr int kTbFullBatchPC = 16;")],
+    "wdiv": [("consensus_wide.hip", "constexpr bool kWideFastRecip = true;", "constexpr bool kWideFastRecip = false;")],
     "tbkvsort": [("tiebreak.hip", "constexpr bool kTbFullKeysInLds = true;", "constexpr bool kTbFullKeysInLds = false;")],
     "tbnofull": [("tiebreak.hip", "const bool split = kTbStageMode != 2 && !EXOTIC && a.rmode == 0 && al16(a.pred)",
                   "const bool split = false && al16(a.pred)")],
