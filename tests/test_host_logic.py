@@ -256,3 +256,21 @@ def test_big_integer_round_matches_cpython(nd):
         if not same:
             bad.append((x, got, exp))
     assert not bad, bad[:5]
+
+
+def test_markstein_quotients_match_ieee_division(tmp_path):
+    """The tie-break FULL kernel's divisions without a divide (tiebreak.hip tb_div_small,
+    bce_device.hpp py_round_nd_sel): RN(x * RN(1/c)) with one FMA correction equals the IEEE
+    quotient -- for k / 10^nd (integer k < 2^53, nd 0..22) and for x / c (c = 1..32, |x| in
+    [2^-1000, 2^1000]).  tools/check_markstein.c at 1/100 of its full sample (the full run,
+    3.1e9 quotients, is recorded in DESIGN.md §4.9)."""
+    import shutil
+    import subprocess
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no C compiler")
+    exe = tmp_path / "check_markstein"
+    src = os.path.join(os.path.dirname(__file__), "..", "tools", "check_markstein.c")
+    subprocess.run([cc, "-O2", "-ffp-contract=off", "-o", str(exe), src, "-lm"], check=True)
+    out = subprocess.run([str(exe), "100"], check=True, capture_output=True, text=True).stdout
+    assert out.strip().startswith("0 of "), out

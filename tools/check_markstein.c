@@ -5,9 +5,12 @@
 // a log-uniform magnitude up to 2^53 (plus k near 2^53 and near multiples of 10^nd); and the
 // group means a / c, c in 1..32, the same way with rinv = RN(1 / c).
 //   gcc -O2 -ffp-contract=off -o /tmp/check_markstein tools/check_markstein.c -lm && /tmp/check_markstein
+// An optional argument scales the random sample counts down (tests/test_host_logic.py runs
+// it with 100: ~31M quotients in a few seconds).
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 static uint64_t rng = 0x9E3779B97F4A7C15ull;
 static uint64_t next(void) {
@@ -29,7 +32,8 @@ static void one(double k, double s, double rinv) {
   }
 }
 
-int main(void) {
+int main(int argc, char** argv) {
+  const long scale = argc > 1 ? atol(argv[1]) : 1;
   for (int nd = 0; nd <= 22; ++nd) {
     double s = 1.0;
     for (int i = 0; i < nd; ++i) s *= 10.0;
@@ -38,12 +42,12 @@ int main(void) {
       one((double)k, s, rinv);
       one(-(double)k, s, rinv);
     }
-    for (int i = 0; i < 20000000; ++i) {
+    for (long i = 0; i < 20000000 / scale; ++i) {
       const int bits = 1 + (int)(next() % 53);
       const uint64_t k = next() >> (64 - bits);
       one((double)k, s, rinv);
     }
-    for (int64_t j = 0; j < 100000; ++j) {
+    for (int64_t j = 0; j < 100000 / scale; ++j) {
       one(9007199254740991.0 - (double)j, s, rinv);
       const double m = floor((double)(next() >> 11) / s) * s;  // a multiple of 10^nd below 2^53
       if (m + 1 < 9007199254740992.0) {
@@ -57,7 +61,7 @@ int main(void) {
   // kernel divides outside that range), rinv = RN(1 / c)
   for (int c = 1; c <= 32; ++c) {
     const double b = (double)c, rinv = 1.0 / b;
-    for (int i = 0; i < 20000000; ++i) {
+    for (long i = 0; i < 20000000 / scale; ++i) {
       const uint64_t r = next();
       const int e = (int)(r % 2000) - 1000;                              // exponent in [-1000, 1000)
       const double m = 1.0 + (double)(next() >> 12) * 0x1p-52;          // random significand
