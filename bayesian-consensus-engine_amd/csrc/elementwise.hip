@@ -212,6 +212,16 @@ struct NsArgs {
   uint8_t* scope;
 };
 
+// nontemporal hints on the namespace pass (every byte is read / written once): both on 0.1665
+// ms, off 0.1752 (10M sources x 3 scopes, profiles/r04t/)
+constexpr bool kNsNtLoad = true;
+constexpr bool kNsNtStore = true;
+template <typename T>
+__device__ __forceinline__ T ns_ld(const T* p) {
+  if constexpr (kNsNtLoad) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+
 __global__ __launch_bounds__(256) void namespace_resolve_kernel(int64_t n, NsArgs a) {
   __shared__ unsigned long long sExp[256];  // the exp table in LDS (see replay_step_kernel)
   sExp[threadIdx.x] = kExpTab[threadIdx.x];
@@ -227,20 +237,29 @@ __global__ __launch_bounds__(256) void namespace_resolve_kernel(int64_t n, NsArg
       uint8_t h[3] = {0, 0, 0};
 #pragma unroll
       for (int q = 0; q < 3; ++q)
-        if (q < a.n_scopes) h[q] = a.sc[q].has[s];
+        if (q < a.n_scopes) h[q] = ns_ld(a.sc[q].has + s);
       int pick = -1;
 #pragma unroll
       for (int q = 2; q >= 0; --q)
         if (q < a.n_scopes && h[q]) pick = q;
       if (pick >= 0) {
         const NsScope& sc = a.sc[pick];
-        r = sc.rel[s];
-        c = sc.conf[s];
-        if (a.apply_decay) r = decayed(r, sc.t_us[s], a.k, sExp);
+        r = ns_ld(sc.rel + s);
+        c = ns_ld(sc.conf + s);
+        if (a.apply_decay) r = decayed(r, ns_ld(sc.t_us + s), a.k, sExp);
         code = a.scope_code[pick];
       }
-      if (a.relconf) a.relconf[s] = make_double2(r, c);
-      if (a.scope) a.scope[s] = (uint8_t)code;
+      if constexpr (kNsNtStore) {
+        typedef double d2v __attribute__((ext_vector_type(2)));
+        d2v v;
+        v.x = r;
+        v.y = c;
+        if (a.relconf) __builtin_nontemporal_store(v, reinterpret_cast<d2v*>(a.relconf + s));
+        if (a.scope) __builtin_nontemporal_store((uint8_t)code, a.scope + s);
+      } else {
+        if (a.relconf) a.relconf[s] = make_double2(r, c);
+        if (a.scope) a.scope[s] = (uint8_t)code;
+      }
     }
     if (a.bits) {
       const unsigned long long m = __ballot(in && (!a.mark_cold || code != 3));
