@@ -26,7 +26,7 @@ def last_json(path):
 def main():
     root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
     rows, worst = [], 0.0
-    for line in ("c2", "c3", "c4", "c5", "tb"):
+    for line in ("c2", "c3", "c4", "c5", "tb", "ns", "agg"):
         d = os.path.join(root, f"prof_{line}")
         if not os.path.isdir(d):
             continue
