@@ -718,7 +718,9 @@ def _agg(args, world, rank, barrier, max_over, sum_over):
                                        N.ptr(nin), C.c_void_p(st.cuda_stream)), "bce_aggregate_groups")
 
     wall, per = _timed(lambda: launch(False), args, world, st, barrier, max_over)
-    _, per_med = _timed(lambda: launch(True), args, world, st, barrier, max_over)
+    per_med = float("nan")
+    if not getattr(args, "single_mode", False):  # (--single-mode: the line's launches only, for rocprof)
+        _, per_med = _timed(lambda: launch(True), args, world, st, barrier, max_over)
     cpu_line, parity = (_cpu_agg(goff, members, cons, conf, has, (wavg, med, maj, mc, nin), args)
                         if rank == 0 and world == 1 else (None, None))
     # per-group latency chain (the kernel is not HBM-bound): one workgroup
