@@ -327,8 +327,9 @@ def tiebreak(offsets: torch.Tensor, pred: torch.Tensor, conf: torch.Tensor, weig
     round() does (precision <= -16 only, checked with one stream synchronisation).
 
     ``max_len`` (optional, <= 64): the caller's bound on every market's length; the host then
-    skips its length scan of the offsets (a market longer than the bound fails the call with
-    a device fault, as the C ABI does)."""
+    skips its length scan of the offsets and does not synchronise.  A market longer than the
+    bound is left unprocessed and recorded in the device fault word, as the C ABI does --
+    ``_native.check_faults`` raises it (the bench and tests call it after their steps)."""
     L = N.require_gpu()
     M = offsets.numel() - 1
     Nsig = pred.numel()
