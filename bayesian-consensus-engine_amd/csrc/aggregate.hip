@@ -49,11 +49,17 @@ __device__ __forceinline__ double key_f64(uint64_t k) {
 }
 
 // One workgroup per group (no per-CU cap): -15% against 8 looping workgroups per CU.
+// kAggWpe: minimum waves per SIMD the VGPR budget must allow.  The compiler's own choice, 90
+// VGPRs, holds five groups per CU; 6 (78 VGPRs, 2 spilled) holds six -- as many as the 25.7 KB
+// of LDS allows: 0.0860 vs 0.0943 ms (+median 0.173 vs 0.193, profiles/r04w/).  Dropping the
+// cons*conf LDS array so more groups fit (the product formed in the chain) ran 2x slower
+// (0.19-0.22 ms, profiles/r04v/; code reverted): the chains' loop is the critical path.
+constexpr int kAggWpe = 6;
 constexpr int kAggT = 256;
 constexpr int kAggPer = 4;                  // members per thread per chunk
 constexpr int kAggCh = kAggT * kAggPer;     // chunk = 1024 members, list order r-major
 
-__global__ __launch_bounds__(kAggT) void aggregate_kernel(AggArgs a) {
+__global__ __launch_bounds__(kAggT) __attribute__((amdgpu_waves_per_eu(kAggWpe, 8))) void aggregate_kernel(AggArgs a) {
   __shared__ double sV[3][kAggCh];  // conf, cons, cons*conf of the chunk's valid members
   __shared__ int sWave[kAggPer][kAggT / 64];
   __shared__ int sHist[256];
