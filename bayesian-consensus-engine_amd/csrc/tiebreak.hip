@@ -271,6 +271,10 @@ constexpr int kTbDump = 64;
 constexpr int kTbFullBatchPC = 8;
 constexpr int kTbFullBatchWR = 8;
 constexpr bool kTbPrefetchMeta = true;
+// FULL tiles: the next array's first batch issued before the phase's output flushes (the
+// stage then waits for loads, not for the flushes' stores): 36 spilled VGPRs, 0.712-0.716 vs
+// 0.664 ms (profiles/r04aa/) -- off
+constexpr bool kTbPreBatch = false;
 // FULL tiles: while a phase computes, two dword loads per lane pull the next phase's 16-KB
 // array into L2 (its 128 lines), so the stage that follows finds it there.  Off: -0.5% time
 // (0.706 vs 0.709-0.711 ms, profiles/r04k/) for FETCH_SIZE +27% (the dword touches are
@@ -516,11 +520,30 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
       wave_sync_lds();
     };
     // FULL tiles (2048 agents): no bounds checks, NB 16-B loads per lane in flight
-    auto stage_full = [&](const double* src, auto nb) {
+    // kTbPreBatch: the next array's first NB loads are issued before the phase's output
+    // flushes, so the stage that follows waits for loads only, not for the flushes' stores
+    // (vmcnt counts both, in order)
+    double2 pv[kTbFullBatchPC];
+    auto pre_issue = [&](const double* src) {
+#pragma unroll
+      for (int k = 0; k < kTbFullBatchPC; ++k) pv[k] = tb_ld2(src + B + 2 * lane + 128 * k);
+    };
+    auto stage_full = [&](const double* src, auto nb, bool pre = false) {
       constexpr int NB = decltype(nb)::value;  // (src + B is 16-B aligned: see Meta::full)
+      static_assert(NB == kTbFullBatchPC, "the preloaded batch is one staging batch");
       wave_sync_lds();
+      int k0 = 0;
+      if (pre) {
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+          const int e = 2 * lane + 128 * k;
+          buf[tb_pad(e)] = pv[k].x;
+          buf[tb_pad(e + 1)] = pv[k].y;
+        }
+        k0 = NB;
+      }
 #pragma unroll 1
-      for (int k0 = 0; k0 < kTbStageIt; k0 += NB) {
+      for (; k0 < kTbStageIt; k0 += NB) {
         double2 v[NB];
 #pragma unroll
         for (int k = 0; k < NB; ++k) v[k] = tb_ld2(src + B + 2 * lane + 128 * (k0 + k));
@@ -636,6 +659,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
             ngf += g < 0 ? 1 : 0;
             u[t] = ((unsigned)go[t] << 5) | (unsigned)t;
           }
+          if constexpr (kTbPreBatch) pre_issue(a.weight);
           if (a.g_of) {
             wave_sync_lds();
 #pragma unroll
@@ -700,7 +724,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
         // 3. densities
         double densp[N];
         settle();
-        stage_full(a.weight, std::integral_constant<int, kTbFullBatchWR>{});
+        stage_full(a.weight, std::integral_constant<int, kTbFullBatchWR>{}, kTbPreBatch);
         touch(a.rel);
         {
           const unsigned st_ = tb_bits(stm), en_ = tb_bits(enm);
@@ -715,13 +739,14 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
             densp[p] = tb_div_small(tot, cnt, sRc);
             put_sel(en_, p, u[p] >> 5, densp[p]);
           }
+          if constexpr (kTbPreBatch) pre_issue(a.rel);
           if (a.g_density) flush(a.g_density);
         }
         // 4. max reliability per group, the winner and the tie flag
         double bd = 0.0, bm = 0.0, bk = 0.0;
         bool tie = false;
         settle();
-        stage_full(a.rel, std::integral_constant<int, kTbFullBatchWR>{});
+        stage_full(a.rel, std::integral_constant<int, kTbFullBatchWR>{}, kTbPreBatch);
         touch(a.conf);
         {
           const unsigned st_ = tb_bits(stm), en_ = tb_bits(enm);
@@ -743,11 +768,12 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
             bm = upd ? mx : bm;
             bk = upd ? kp[p] : bk;
           }
+          if constexpr (kTbPreBatch) pre_issue(a.conf);
           if (a.g_maxrel) flush(a.g_maxrel);
         }
         // 5. variance (input order), per-group mean confidences
         settle();
-        stage_full(a.conf, std::integral_constant<int, kTbFullBatchPC>{});
+        stage_full(a.conf, std::integral_constant<int, kTbFullBatchPC>{}, kTbPreBatch);
         if (kTbPrefetchMeta && (tile + nwaves) * 64 < n_list) meta_pre(tile + nwaves);
         double variance;
         {

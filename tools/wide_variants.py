@@ -78,6 +78,7 @@ VARIANTS = {
     "nsnont": [("elementwise.hip", "constexpr bool kNsNtLoad = true;", "constexpr bool kNsNtLoad = false;"),
                ("elementwise.hip", "constexpr bool kNsNtStore = true;", "constexpr bool kNsNtStore = false;")],
     "aggw1": [("aggregate.hip", "constexpr int kAggWpe = 6;", "constexpr int kAggWpe = 1;")],
+    "tbprebatch": [("tiebreak.hip", "constexpr bool kTbPreBatch = false;", "constexpr bool kTbPreBatch = true;")],
     "tbkvsort": [("tiebreak.hip", "constexpr bool kTbFullKeysInLds = true;", "constexpr bool kTbFullKeysInLds = false;")],
     "tbnofull": [("tiebreak.hip", "const bool split = kTbStageMode != 2 && !EXOTIC && a.rmode == 0 && al16(a.pred)",
                   "const bool split = false && al16(a.pred)")],
