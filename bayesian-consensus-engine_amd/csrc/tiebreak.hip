@@ -530,7 +530,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     };
     auto stage_full = [&](const double* src, auto nb, bool pre = false) {
       constexpr int NB = decltype(nb)::value;  // (src + B is 16-B aligned: see Meta::full)
-      static_assert(NB == kTbFullBatchPC, "the preloaded batch is one staging batch");
+      static_assert(!kTbPreBatch || NB == kTbFullBatchPC, "the preloaded batch is one staging batch");
       wave_sync_lds();
       int k0 = 0;
       if (pre) {
