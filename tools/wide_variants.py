@@ -79,6 +79,7 @@ VARIANTS = {
                ("elementwise.hip", "constexpr bool kNsNtStore = true;", "constexpr bool kNsNtStore = false;")],
     "aggw1": [("aggregate.hip", "constexpr int kAggWpe = 6;", "constexpr int kAggWpe = 1;")],
     "tbprebatch": [("tiebreak.hip", "constexpr bool kTbPreBatch = false;", "constexpr bool kTbPreBatch = true;")],
+    "tab4w": [("consensus_tab.hip", "constexpr int kTabWaves = 8;", "constexpr int kTabWaves = 4;")],
     "tbkvsort": [("tiebreak.hip", "constexpr bool kTbFullKeysInLds = true;", "constexpr bool kTbFullKeysInLds = false;")],
     "tbnofull": [("tiebreak.hip", "const bool split = kTbStageMode != 2 && !EXOTIC && a.rmode == 0 && al16(a.pred)",
                   "const bool split = false && al16(a.pred)")],
