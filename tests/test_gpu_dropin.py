@@ -947,3 +947,49 @@ def test_tiebreak_ragged_lane_kernel_vs_oracle(precision):
         assert np.array_equal(gc[sl], exp["g_count"][sl]), m
         assert ga[sl].tobytes() == exp["g_avgconf"][sl].tobytes(), m
         assert gm[sl].tobytes() == exp["g_maxrel"][sl].tobytes(), m
+
+
+@pytest.mark.parametrize("precision", [0, 1, 6, 15, 22])
+def test_tiebreak_full_tiles_round_edges(precision):
+    """The FULL kernel's round(): rint of x * 10^p, an exact redo only for flagged halves, and
+    k / 10^p as a reciprocal product with one FMA correction.  Full tiles of predictions at the
+    edges -- exact decimal halves, values one ulp either side of them, magnitudes around the
+    threshold past which round() returns x itself, subnormals, +-0.0 -- give the group keys
+    Python's round() gives, bit for bit."""
+    import math
+    import torch
+    from bayesian_engine import batch
+    from oracle import oracle as orc
+    rng = np.random.default_rng(700 + precision)
+    M = 64 * 12
+    n = M * 32
+    scale = 10.0 ** precision
+    k = rng.integers(-10**6, 10**6, n).astype(np.float64)
+    halves = (k + 0.5) / scale
+    pred = halves.copy()
+    sel = rng.random(n)
+    pred = np.where(sel < 0.2, np.nextafter(halves, np.inf), pred)
+    pred = np.where((sel >= 0.2) & (sel < 0.4), np.nextafter(halves, -np.inf), pred)
+    E = math.floor(52.0 - precision * 3.321928094887362) + 1  # the restatement's threshold 2^E
+    big = np.ldexp(1.0, E) * rng.uniform(0.5, 2.0, n) * np.where(rng.random(n) < 0.5, -1.0, 1.0)
+    pred = np.where((sel >= 0.4) & (sel < 0.55), big, pred)
+    pred = np.where((sel >= 0.55) & (sel < 0.6), rng.random(n) * 1e-310, pred)     # subnormal
+    pred = np.where((sel >= 0.6) & (sel < 0.63), -0.0, pred)
+    pred = np.where((sel >= 0.63) & (sel < 0.7), rng.random(n), pred)
+    # repeat some values inside markets so groups form
+    dup = rng.random(n) < 0.25
+    pred[dup] = pred[np.maximum(np.nonzero(dup)[0] - 1, 0)]
+    off = np.arange(0, n + 1, 32, dtype=np.int64)
+    conf, weight, rel = rng.random(n), rng.random(n), rng.random(n)
+    keys = np.array([round(float(x), precision) for x in pred], np.float64)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    r = batch.tiebreak(T(off), T(pred), T(conf), T(weight), T(rel), precision=precision, max_len=32)
+    torch.cuda.synchronize()
+    exp = orc.tiebreak_csr(off, pred, conf, weight, rel, keys=keys)
+    for key in ("winner", "label", "n_groups", "variance"):
+        got = getattr(r, key).cpu().numpy()
+        assert got.tobytes() == exp[key].astype(got.dtype).tobytes(), key
+    gk = r.g_key.cpu().numpy()
+    for m in range(M):
+        a, g = int(off[m]), int(exp["n_groups"][m])
+        assert gk[a:a + g].tobytes() == exp["g_key"][a:a + g].tobytes(), m
