@@ -50,7 +50,6 @@ _SIGS = {
     "bce_debug_set_spin_cap": (C.c_int, [C.c_int]),
     "bce_debug_lane_selftest": (C.c_int, [_vp, _vp]),
     "bce_debug_py_round": (_f64, [_f64, _i32, _vp]),
-    "bce_debug_set_wide_team": (C.c_int, [C.c_int]),
     "bce_jsonl_parse": (C.c_int, [_vp, _i64, _i32, _vp]),
     "bce_jsonl_counts": (C.c_int, [_vp, _vp]),
     "bce_jsonl_arrays": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),

@@ -92,18 +92,27 @@ def _consensus_batch(args: argparse.Namespace) -> None:
             run.append(text)
             continue
         if run:
-            sys.stdout.flush()
-            sys.stdout.buffer.write(b"\n".join(run) + b"\n")
-            sys.stdout.buffer.flush()
+            _write_out(run)
             run = []
         print(text.decode("utf-8", "surrogatepass"), file=sys.stderr)
         failed = True
     if run:
-        sys.stdout.flush()
-        sys.stdout.buffer.write(b"\n".join(run) + b"\n")
-        sys.stdout.buffer.flush()
+        _write_out(run)
     if failed:
         raise SystemExit(1)
+
+
+def _write_out(texts: list) -> None:
+    """The rendered results (ASCII bytes) to stdout: its byte buffer when it has one, else as
+    text (a redirect_stdout(StringIO()) or an embedding host)."""
+    data = b"\n".join(texts) + b"\n"
+    out = sys.stdout
+    if hasattr(out, "buffer"):
+        out.flush()
+        out.buffer.write(data)
+        out.buffer.flush()
+    else:
+        out.write(data.decode("ascii"))
 
 
 def _with_store(command: str, body: Callable[[argparse.Namespace, SQLiteReliabilityStore], Any]):

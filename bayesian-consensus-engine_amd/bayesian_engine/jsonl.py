@@ -285,6 +285,10 @@ def _weight_texts(nb: "_NativeBatch", sr: dict, used: np.ndarray):
     usedset = set(used.tolist())
     for i, n in enumerate(names):
         d = sr.get(n, {})
+        if i not in usedset and not isinstance(d, dict):
+            # a name only failed lines use: the reference never looks it up (core.py:110 runs
+            # for computed payloads only), so its entry's shape cannot raise
+            d = {}
         r = d.get("reliability", DEFAULT_RELIABILITY)
         c = d.get("confidence", DEFAULT_CONFIDENCE)
         if i in usedset:

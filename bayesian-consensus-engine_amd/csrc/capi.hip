@@ -47,8 +47,6 @@ struct DevCtx {
   std::mutex side_mu;  // held from the plan's fork to its join (bce_consensus_planned)
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  int* queue = nullptr;               // kQueueSlots pairs of team-kernel queue words
-  std::atomic<unsigned> queue_next{0};
   int* split = nullptr;               // kQueueSlots blocks of kSplitWords tie-break ticket words
   std::atomic<unsigned> split_next{0};
 };
@@ -68,10 +66,6 @@ DevCtx* dev_ctx() {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
-    int* qw = nullptr;
-    if (e == hipSuccess) e = hipMalloc((void**)&qw, 2 * kQueueSlots * sizeof(int));
-    if (e == hipSuccess) e = hipMemset(qw, 0, 2 * kQueueSlots * sizeof(int));
-    if (e == hipSuccess) c->queue = qw;
     int* sw = nullptr;
     if (e == hipSuccess) e = hipMalloc((void**)&sw, (size_t)kQueueSlots * kSplitWords * sizeof(int));
     if (e == hipSuccess) e = hipMemset(sw, 0, (size_t)kQueueSlots * kSplitWords * sizeof(int));
@@ -101,17 +95,11 @@ int cu_count() {
   return c ? c->cus : 256;
 }
 
-int* team_queue_slot() {
-  DevCtx* c = dev_ctx();
-  if (!c || !c->queue) return nullptr;
-  // a slot is reused after kQueueSlots launches; each launch zeroes its pair when it ends
-  return c->queue + 2 * (c->queue_next.fetch_add(1) % kQueueSlots);
-}
-
 int* split_slot() {
   DevCtx* c = dev_ctx();
   if (!c || !c->split) return nullptr;
-  // tickets make reuse safe: a launch pair only reacts to its own ticket
+  // tickets make reuse safe, on any stream: PART 1 raises a word to its ticket (atomicMax) and
+  // PART 2 runs whenever the word holds its own or a newer pair's ticket (tiebreak.hip)
   return c->split + (size_t)(c->split_next.fetch_add(1) % kQueueSlots) * kSplitWords;
 }
 

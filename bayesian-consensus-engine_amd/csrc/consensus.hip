@@ -1725,23 +1725,6 @@ extern "C" int64_t bce_consensus_scratch_bytes(const int64_t* offsets_host, cons
   return (int64_t)grid * 4 * next_pow2(mx) * 8;
 }
 
-// BCE_WIDE_TEAM=1 in the environment, or bce_debug_set_wide_team(1), selects the all-bins
-// team kernel instead of one launch per wide bin (the default: C3 fast 1.314 vs 1.393 ms on
-// one GPU, profiles/r04c/ab_*.txt).
-static int g_wide_team = -1;
-static bool wide_team_enabled() {
-  if (g_wide_team < 0) {
-    const char* e = getenv("BCE_WIDE_TEAM");
-    g_wide_team = (e && e[0] == '1') ? 1 : 0;  // default: one launch per bin (faster on one GPU)
-  }
-  return g_wide_team != 0;
-}
-extern "C" int bce_debug_set_wide_team(int on) {
-  const int prev = wide_team_enabled() ? 1 : 0;
-  g_wide_team = on ? 1 : 0;
-  return prev;
-}
-
 extern "C" int bce_consensus_planned(const int64_t* offsets, int64_t n_markets, const int32_t* sid,
                                      const double* prob, int64_t n_signals, const double* relconf,
                                      const uint32_t* present_bits, int32_t n_sources,
@@ -1780,31 +1763,6 @@ extern "C" int bce_consensus_planned(const int64_t* offsets, int64_t n_markets, 
   // kernel's LDS chain buffers allow two workgroups per CU at 3/6 waves as at 4/8, so the
   // smaller workgroup only loses latency hiding, and a separate launch adds a tail.
   const bool merge_np2 = mode == BCE_MODE_EXACT;
-  // All wide bins (65..4096) in ONE persistent launch of the team kernel (consensus_wide.hip):
-  // needs the weight output (its lockstep teams read w back instead of parking it behind
-  // barriers) and keys of 20 + 12 bits.  The short bins go to the side stream first, so
-  // their workgroups are dispatched before the team kernel's fill the rest of the chip.
-  // Off by default (bce_debug_set_wide_team / BCE_WIDE_TEAM=1 turn it on).
-  const bool team_env = wide_team_enabled();
-  int64_t wide_markets = 0;
-  for (int b = kPlanSideLast + 1; b <= BCE_NBINS - 2; ++b) wide_markets += bin_start_host[b + 1] - bin_start_host[b];
-  const bool team = team_env && weight != nullptr && n_sources <= (1 << 20) && wide_markets > 0;
-  if (team) {
-    for (int b = 0; b <= side_last && !rc; ++b) {
-      ConsArgs a = base;
-      a.list = order + bin_start_host[b];
-      a.n_list = bin_start_host[b + 1] - bin_start_host[b];
-      if (a.n_list == 0) continue;
-      static const int lens[4] = {8, 16, 32, 64};
-      rc = seg_ok ? launch_seg_for_len(lens[b], a, side) : launch_long_lds(a, side);
-    }
-    if (!rc) {
-      ConsArgs a = base;
-      a.list = order;
-      a.n_list = bin_start_host[BCE_NBINS - 1] - bin_start_host[kPlanSideLast + 1];
-      rc = launch_wide_team(a, bin_start_host, st);
-    }
-  }
   // Longest bins first, except that the 2049..3072 bin precedes the 3073..4096 one: its
   // 6-wave workgroups leave 4 of a CU's 16 wave slots free (two per CU at 128 VGPRs), which
   // the side stream's short-market kernels then fill (C3 fast -1.3%,
@@ -1812,7 +1770,6 @@ extern "C" int bce_consensus_planned(const int64_t* offsets, int64_t n_markets, 
   static const int kOrder[BCE_NBINS] = {12, 10, 11, 9, 8, 7, 6, 5, 4, 3, 2, 1, 0};
   for (int oi = 0; oi < BCE_NBINS && !rc; ++oi) {
     const int b = kOrder[oi];
-    if (team && b != BCE_NBINS - 1) continue;  // launched above; the > 4096 bin still runs here
     if (merge_np2 && (b == kBinNp2Lo || b == kBinNp2Hi)) continue;
     const int b0 = (merge_np2 && (b == kBinNp2Lo + 1 || b == kBinNp2Hi + 1)) ? b - 1 : b;
     ConsArgs a = base;

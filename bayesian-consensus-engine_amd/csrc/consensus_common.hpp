@@ -171,12 +171,6 @@ int launch_tab32(const ConsArgs& a, hipStream_t st);
 // index field (7..12, wide_key_bits(max_len)); needs n_sources <= 2^(32 - ib).
 int wide_key_bits(int64_t max_len);
 int launch_wide_len(int64_t max_len, const ConsArgs& a, hipStream_t st);
-// All wide bins (65..4096) of a plan in one persistent launch (needs the weight output and
-// n_sources <= 2^20); the queue words come from team_queue_slot().
-int launch_wide_team(const ConsArgs& a, const int64_t* bin_start_host, hipStream_t st);
-// Two zeroed device ints for one team-kernel launch (a ring of slots per device; the kernel
-// leaves its pair zeroed when it finishes).
-int* team_queue_slot();
 // kSplitWords words (one per wave of the grid) for a tie-break FULL/rest launch pair
 // (tiebreak.hip; written with a per-launch ticket)
 constexpr int kSplitWords = 4096;

@@ -40,11 +40,6 @@
 constexpr int kWideHR = 1;       // rounds of NT uniques whose gathers are in flight together (2: C3 fast +6%)
 constexpr int kWideWPE = 4;      // min waves per SIMD (register budget; 4 vs 2: exact -1.3%, fast unchanged)
 constexpr int kWideNWBF = 4;     // FAST nweight read-backs per batch (1: 1.645, 2: 1.634, 4: 1.587 ms C3)
-// Sorted probabilities in region A rotated per thread block (sq_addr below): conflict-free
-// step-3 stores, but the per-element read addresses spill 4-10 VGPRs in the FAST kernels --
-// C3 fast 1.505 vs 1.314 ms per bin, 1.633 vs 1.393 ms in the team kernel, parity green
-// (profiles/r04c/ab_*.txt): kept off.
-constexpr bool kWideSwz = false;
 
 namespace bce {
 namespace {
@@ -354,19 +349,6 @@ __device__ __forceinline__ double wave_sum_fixed(double v) {
   return (readlane_f64(v, 0) + readlane_f64(v, 16)) + (readlane_f64(v, 32) + readlane_f64(v, 48));
 }
 
-// Address of sorted position q in region A.  Thread t holds positions t*R .. t*R + R-1 after
-// the sort; written thread-major they put the R stores of a wave 8R bytes apart per lane (a
-// 4-way bank conflict on every ds_write_b128 at R = 8).  Rotating each thread's block by
-// (t >> log2(32/R)) & (R-1) -- (q >> 5) for every R -- spreads 32 consecutive lanes over all
-// 32 bank pairs for each register, so the R ds_write_b64 of the sorted probabilities are
-// conflict-free; a run of consecutive positions stays inside its blocks.  The map is a
-// bijection on [0, P), so slot j of the parked weights uses it too.
-template <int R>
-__device__ __forceinline__ int sq_addr(int q) {
-  if constexpr (kWideSwz) return (q & ~(R - 1)) | (((q & (R - 1)) + (q >> 5)) & (R - 1));
-  else return q;
-}
-
 // FAST: run averages and normalizedWeight by reciprocal products instead of IEEE divisions
 // (a few ulps; FAST's contract is 1e-9 relative)
 constexpr bool kWideFastRecip = true;
@@ -378,7 +360,7 @@ template <int R, bool APPROX = false>
 __device__ __forceinline__ double run_sum(const double* sA, int q0, int len) {
   double x[4];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) x[e] = sA[sq_addr<R>(q0 + e)];
+  for (int e = 0; e < 4; ++e) x[e] = sA[q0 + e];
   double sum = 0.0;
 #pragma unroll
   for (int e = 0; e < 4; ++e) sum += (e < len) ? x[e] : 0.0;
@@ -386,11 +368,11 @@ __device__ __forceinline__ double run_sum(const double* sA, int q0, int len) {
     int e0 = 4;
     double xa[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) xa[e] = sA[sq_addr<R>(q0 + e0 + e)];
+    for (int e = 0; e < 8; ++e) xa[e] = sA[q0 + e0 + e];
     for (; e0 + 8 <= len; e0 += 8) {
       double xb[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) xb[e] = sA[sq_addr<R>(q0 + e0 + 8 + e)];
+      for (int e = 0; e < 8; ++e) xb[e] = sA[q0 + e0 + 8 + e];
 #pragma unroll
       for (int e = 0; e < 8; ++e) sum += xa[e];
 #pragma unroll
@@ -461,9 +443,7 @@ __device__ __forceinline__ void chain_add(double& acc, const double* src, int ce
   }
 }
 
-// LDS of one market's team of NW waves, carved from a byte buffer: the per-bin kernel gives
-// each workgroup one team, the all-bins team kernel (below) lays 8/NW teams -- and over time
-// several configurations -- over one allocation.
+// LDS of one market's workgroup of NW waves, carved from a byte buffer.
 //   region A  P doubles (+ read-ahead pad): input-order probs, then sorted probs in place
 //   region B  sort exchange rows, then leaders [P] (+ exact: chain buffers [2][3][NT])
 //   small     per-wave last keys / counts, totals, error index, exact hand-off counters
@@ -496,17 +476,7 @@ struct WideLds {
         sDone(reinterpret_cast<int*>(base + MISC_OFF + 12)) {}
 };
 
-// The barrier a market's phases need: the whole workgroup, except for a one-wave team inside
-// the team kernel, whose LDS hand-offs stay inside its wave (in-order LDS + lgkmcnt drain).
-// Teams of >= 2 waves in the team kernel run in lockstep: every team executes the same
-// barrier sequence per market (the bin fixes it), dummy teams included.
-template <int NW, bool TEAM>
-__device__ __forceinline__ void team_sync() {
-  if constexpr (TEAM && NW == 1) wave_sync_lds();
-  else __syncthreads();
-}
-
-// Market metadata (m = order entry; n = 0 for a dummy team) and the buffer loads of its sids
+// The buffer loads of a market's sids
 // and probabilities into registers (records = n signals, so i >= n reads 0).
 template <int NW, int R>
 __device__ __forceinline__ void wide_load(const ConsArgs& a, int64_t off, int n, int t, unsigned (&ps)[R],
@@ -522,11 +492,10 @@ __device__ __forceinline__ void wide_load(const ConsArgs& a, int64_t off, int n,
     pp[c] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rp, t * 8, c * NT * 8, 0));
 }
 
-// One market (m, off, n) on a team of NW waves; t = thread within the team.  ps / pp hold
+// One market (m, off, n) on a workgroup of NW waves; t = thread.  ps / pp hold
 // its sids and probabilities (loaded by the caller); issue_next() is called once the keys are
-// built, to start the team's next market's loads into ps / pp.  m < 0: a dummy market (team
-// kernel, an item with fewer markets than teams) -- every barrier, no output.
-template <int NW, int R, bool FAST, int NN, bool TEAM, class NextFn>
+// built, to start the workgroup's next market's loads into ps / pp.
+template <int NW, int R, bool FAST, int NN, class NextFn>
 __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW, R, FAST, NN>& L, const int t,
                                             const int32_t m, const int64_t off, int n, unsigned (&ps)[R],
                                             double (&pp)[R], NextFn&& issue_next) {
@@ -550,7 +519,7 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
   double* const sW = reinterpret_cast<double*>(sB + P);
 
   const int lane = lane_id();
-  const int wv = __builtin_amdgcn_readfirstlane(t >> 6);  // wave within the team (uniform)
+  const int wv = __builtin_amdgcn_readfirstlane(t >> 6);  // wave within the workgroup (uniform)
   const unsigned smax = (unsigned)(a.n_sources > 0 ? a.n_sources - 1 : 0);
   // normalizedWeight reads w[j] back from the weight output (this thread's own stores)
   // in workgroups of several waves (it saves their barriers); a single wave parks w[j] in
@@ -572,7 +541,7 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
   // input-order probs into region A before the next loads; region A's last readers are
   // the previous market's run sums (before its final barrier) unless normalizedWeight
   // reads w[j] from it
-  if (NW > 1 && !wback) team_sync<NW, TEAM>();
+  if (NW > 1 && !wback) __syncthreads();
 #pragma unroll
   for (int c = 0; c < R; ++c) {
     const int i = c * NT + t;
@@ -583,8 +552,7 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
   issue_next();
   if (n > P) {  // longer than this launch's max_len: left unprocessed, reported
     raise_fault(a.fault, kFaultTooLong);
-    if constexpr (!TEAM) return;  // uniform over the workgroup
-    n = 0;                        // lockstep teams: a dummy market (every barrier, no output)
+    return;  // uniform over the workgroup
   }
   if (t == 0) *L.sErr = kNoErr;
 
@@ -593,7 +561,7 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
 
   // ---- 3. input-order probs + range check, sorted probs in place, leaders ----------
   if (lane == 63) L.sLast[wv] = key[R - 1];
-  team_sync<NW, TEAM>();  // (a) input-order probs + sLast visible; exchange rows dead
+  __syncthreads();  // (a) input-order probs + sLast visible; exchange rows dead
   if (myerr != kNoErr) atomicMin(L.sErr, myerr);
   double x[R];
 #pragma unroll
@@ -614,15 +582,9 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
   const int cnt = __popc(lead);
   const int incl = wave_incl_scan(cnt);
   if (lane == 63) L.sCnt[wv] = incl;
-  team_sync<NW, TEAM>();  // (b) every read of the input-order probs done; counts visible
-  if constexpr (kWideSwz) {
+  __syncthreads();  // (b) every read of the input-order probs done; counts visible
 #pragma unroll
-    for (int r = 0; r < R; ++r) sA[sq_addr<R>(t * R + r)] = x[r];
-  } else {
-#pragma unroll
-    for (int r = 0; r < R; r += 2)
-      *reinterpret_cast<double2*>(sA + t * R + r) = make_double2(x[r], x[r + 1]);
-  }
+  for (int r = 0; r < R; r += 2) *reinterpret_cast<double2*>(sA + t * R + r) = make_double2(x[r], x[r + 1]);
   int base = incl - cnt, u = 0;
 #pragma unroll
   for (int w = 0; w < NW; ++w) {
@@ -641,7 +603,7 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
     L.sRdy[0] = L.sRdy[1] = 0;
     *L.sDone = 0;
   }
-  team_sync<NW, TEAM>();  // (c) sorted probs + leaders visible
+  __syncthreads();  // (c) sorted probs + leaders visible
 
   // ---- 4. per-unique products --------------------------------------------------------
   double acc = 0.0;                     // exact: wave 0 lanes 0..2 carry the chains
@@ -784,7 +746,7 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
           lm &= lm - 1;
           const int lq0 = __builtin_amdgcn_readlane(q0s[i], LL), llen = __builtin_amdgcn_readlane(len, LL);
           double part = 0.0;
-          for (int e = lane; e < llen; e += 64) part += sA[sq_addr<R>(lq0 + e)];
+          for (int e = lane; e < llen; e += 64) part += sA[lq0 + e];
           part = wave_sum_fixed(part);
           if (lane == LL) avg = part / (double)llen;
         }
@@ -807,11 +769,11 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
         pc += vc[i];
       }
       if (!wback) {
-        team_sync<NW, TEAM>();  // every sorted-prob read of this group done
+        __syncthreads();  // every sorted-prob read of this group done
 #pragma unroll
         for (int i = 0; i < HR; ++i) {
           const int jj = (h + i) * NT + t;
-          if (jj < u) sA[sq_addr<R>(jj)] = vw[i];  // later groups read only positions > jj
+          if (jj < u) sA[jj] = vw[i];  // later groups read only positions > jj
         }
       }
     } else {
@@ -822,9 +784,9 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
           buf[t] = vw[i];
           buf[NT + t] = va[i];
           buf[2 * NT + t] = vc[i];
-          team_sync<NW, TEAM>();  // round staged; every sorted-prob read of this group is done
+          __syncthreads();  // round staged; every sorted-prob read of this group is done
           const int jj = (h + i) * NT + t;
-          if (jj < u && !wback) sA[sq_addr<R>(jj)] = vw[i];  // position jj is only read by uniques <= jj
+          if (jj < u && !wback) sA[jj] = vw[i];  // position jj is only read by uniques <= jj
           if (wv == 0) {
             __builtin_amdgcn_s_setprio(2);  // the chain is the critical path
             const int ce = (u - (h + i) * NT < NT) ? u - (h + i) * NT : NT;
@@ -862,7 +824,7 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
   } else {
     if (wv == 0 && lane < 3) L.sTot[lane] = acc;
   }
-  team_sync<NW, TEAM>();  // totals + w[j] visible
+  __syncthreads();  // totals + w[j] visible
   double tw = L.sTot[0], ta = L.sTot[1], tc = L.sTot[2];
   if constexpr (FAST) {
 #pragma unroll
@@ -889,7 +851,7 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
 #pragma unroll
       for (int k = 0; k < R; ++k) {
         const int jj = t + NT * k;
-        wj[k] = (jj < u) ? (wback ? a.weight[off + jj] : sA[sq_addr<R>(jj)]) : 0.0;
+        wj[k] = (jj < u) ? (wback ? a.weight[off + jj] : sA[jj]) : 0.0;
       }
 #pragma unroll
       for (int k = 0; k < R; ++k) {
@@ -904,7 +866,7 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
 #pragma unroll
         for (int k = 0; k < NB; ++k) {
           const int jj = j0 + NT * k;
-          wj[k] = (jj < u) ? (park ? sW[jj] : wback ? a.weight[off + jj] : sA[sq_addr<R>(jj)]) : 0.0;
+          wj[k] = (jj < u) ? (park ? sW[jj] : wback ? a.weight[off + jj] : sA[jj]) : 0.0;
         }
 #pragma unroll
         for (int k = 0; k < NB; ++k) {
@@ -962,158 +924,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
     const int32_t m = nm;
     const int64_t off = noff;
     const int n = nn;
-    wide_market<NW, R, FAST, NN, false>(a, L, t, m, off, n, ps, pp, [&]() {
+    wide_market<NW, R, FAST, NN>(a, L, t, m, off, n, ps, pp, [&]() {
       if (li + G < a.n_list) {
         meta(li + G);
         wide_load<NW, R>(a, noff, nn, t, ps, pp);
       }
     });
-  }
-}
-
-// ---- all wide bins in one persistent launch (planned calls) ---------------------------
-// Workgroups of 8 waves pull items from a device queue: an item is up to 8/NW consecutive
-// markets of one length bin (the plan lists each bin's markets longest first and the bins
-// longest first), one market per team of NW waves.  One launch per step instead of one per
-// bin: a single ramp and a single tail, and a workgroup that finishes its long markets moves
-// on to shorter ones instead of idling at a bin boundary -- what a 1/8 market shard of C3
-// needs.  The queue word pair (next item, finished workgroups) is reset by the
-// last workgroup out, ready for the next launch.
-constexpr int kTeamWaves = 8;
-constexpr int kTeamBins = 8;  // 65..128, ..256, ..512, ..1024, ..1536, ..2048, ..3072, ..4096
-
-struct WideItems {
-  int* queue;                    // [2]: next item, finished workgroups (zero between launches)
-  int32_t n_items;
-  int32_t item_start[kTeamBins + 1];  // items of team bin k: [item_start[k], item_start[k+1])
-  int32_t first[kTeamBins];      // bin k's first position in a.list
-  int32_t end[kTeamBins];        // one past its last
-};
-
-// team bin k in processing order (longest markets first): 0 = 3073..4096, 7 = 65..128
-template <int K> struct TeamBin;
-template <> struct TeamBin<0> { static constexpr int NW = 8, R = 8; };  // 3073..4096
-template <> struct TeamBin<1> { static constexpr int NW = 8, R = 8; };  // 2049..3072
-template <> struct TeamBin<2> { static constexpr int NW = 4, R = 8; };  // 1537..2048
-template <> struct TeamBin<3> { static constexpr int NW = 4, R = 8; };  // 1025..1536
-template <> struct TeamBin<4> { static constexpr int NW = 2, R = 8; };  // 513..1024
-template <> struct TeamBin<5> { static constexpr int NW = 1, R = 8; };  // 257..512
-template <> struct TeamBin<6> { static constexpr int NW = 1, R = 4; };  // 129..256
-template <> struct TeamBin<7> { static constexpr int NW = 1, R = 2; };  // 65..128
-
-template <bool FAST>
-constexpr int team_lds_bytes() {
-  int mx = 0;
-  const int b[5] = {kTeamWaves * WideLds<1, 2, FAST, 1>::BYTES, kTeamWaves * WideLds<1, 4, FAST, 1>::BYTES,
-                    kTeamWaves * WideLds<1, 8, FAST, 1>::BYTES, (kTeamWaves / 2) * WideLds<2, 8, FAST, 2>::BYTES,
-                    (kTeamWaves / 4) * WideLds<4, 8, FAST, 4>::BYTES};
-  for (int i = 0; i < 5; ++i) mx = b[i] > mx ? b[i] : mx;
-  const int b8 = WideLds<8, 8, FAST, 8>::BYTES;
-  return b8 > mx ? b8 : mx;
-}
-
-__device__ __forceinline__ int team_bin_of(const WideItems& q, int item) {
-  int k = 0;
-#pragma unroll
-  for (int i = 1; i < kTeamBins; ++i) k += (item >= q.item_start[i]) ? 1 : 0;
-  return k;
-}
-
-// Items of team bin K while the queue keeps handing this workgroup items of that bin.
-// cur / nxt: the item being started and the one already claimed after it (known to every
-// thread); the claim after that is made by thread 0 during the current item and published at
-// the item's closing barrier (two LDS slots, alternating).
-template <int K, bool FAST>
-__device__ __forceinline__ void team_run(const ConsArgs& a, const WideItems& q, unsigned char* smem, int* sItem,
-                                         int& cur, int& nxt, int& slot, bool& claiming) {
-  constexpr int NW = TeamBin<K>::NW, R = TeamBin<K>::R;
-  constexpr int TEAMS = kTeamWaves / NW;
-  using LD = WideLds<NW, R, FAST, NW>;
-  const int t0 = threadIdx.x;
-  const int team = __builtin_amdgcn_readfirstlane((int)(t0 >> 6)) / NW;  // uniform: LDS bases stay scalar
-  const int t = t0 - team * 64 * NW;
-  const LD L(smem + team * LD::BYTES);
-  unsigned ps[R];
-  double pp[R];
-  // this team's market of item `it` (m < 0: none -- the bin's last item can be short)
-  auto market_of = [&](int it, int32_t& m, int64_t& off, int& n) {
-    const int64_t pos = (int64_t)q.first[K] + (int64_t)(it - q.item_start[K]) * TEAMS + team;
-    m = -1;
-    off = 0;
-    n = 0;
-    if (pos < q.end[K]) {
-      m = a.list[pos];
-      off = a.offsets[m];
-      n = (int)(a.offsets[m + 1] - off);
-    }
-  };
-  int32_t m;
-  int64_t off;
-  int n;
-  market_of(cur, m, off, n);
-  wide_load<NW, R>(a, off, n, t, ps, pp);
-  for (;;) {
-    if (t0 == 0) {  // the claim after nxt (past the end once a claim has landed there)
-      int c = q.n_items;
-      if (claiming) {
-        c = atomicAdd(&q.queue[0], 1);
-        claiming = c < q.n_items;
-      }
-      sItem[slot] = c;
-    }
-    const bool same = nxt < q.n_items && team_bin_of(q, nxt) == K;
-    int32_t m2 = -1;
-    int64_t off2 = 0;
-    int n2 = 0;
-    wide_market<NW, R, FAST, NW, true>(a, L, t, m, off, n, ps, pp, [&]() {
-      if (same) {
-        market_of(nxt, m2, off2, n2);
-        wide_load<NW, R>(a, off2, n2, t, ps, pp);
-      }
-    });
-    __syncthreads();  // the item's LDS is free; the next claim is visible
-    cur = nxt;
-    nxt = sItem[slot];
-    slot ^= 1;
-    if (!same) return;
-    m = m2;
-    off = off2;
-    n = n2;
-  }
-}
-
-template <bool FAST>
-__global__ __launch_bounds__(64 * kTeamWaves) __attribute__((amdgpu_waves_per_eu(4, 8))) void consensus_wide_team_kernel(
-    ConsArgs a, WideItems q) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[team_lds_bytes<FAST>()];
-  __shared__ int sItem[2];
-  if (threadIdx.x == 0) {
-    sItem[0] = atomicAdd(&q.queue[0], 1);
-    sItem[1] = atomicAdd(&q.queue[0], 1);
-  }
-  __syncthreads();
-  int cur = sItem[0], nxt = sItem[1], slot = 0;
-  bool claiming = nxt < q.n_items;  // thread 0's: keep claiming while claims land in range
-  __syncthreads();                   // both slots read before thread 0 reuses one
-  while (cur < q.n_items) {
-    switch (team_bin_of(q, cur)) {
-      case 0: team_run<0, FAST>(a, q, smem, sItem, cur, nxt, slot, claiming); break;
-      case 1: team_run<1, FAST>(a, q, smem, sItem, cur, nxt, slot, claiming); break;
-      case 2: team_run<2, FAST>(a, q, smem, sItem, cur, nxt, slot, claiming); break;
-      case 3: team_run<3, FAST>(a, q, smem, sItem, cur, nxt, slot, claiming); break;
-      case 4: team_run<4, FAST>(a, q, smem, sItem, cur, nxt, slot, claiming); break;
-      case 5: team_run<5, FAST>(a, q, smem, sItem, cur, nxt, slot, claiming); break;
-      case 6: team_run<6, FAST>(a, q, smem, sItem, cur, nxt, slot, claiming); break;
-      default: team_run<7, FAST>(a, q, smem, sItem, cur, nxt, slot, claiming); break;
-    }
-  }
-  // every claim of this workgroup is made: the last workgroup out resets the queue
-  if (threadIdx.x == 0) {
-    __atomic_thread_fence(__ATOMIC_SEQ_CST);
-    if (atomicAdd(&q.queue[1], 1) == (int)gridDim.x - 1) {
-      atomicExch(&q.queue[0], 0);
-      atomicExch(&q.queue[1], 0);
-    }
   }
 }
 
@@ -1176,40 +992,6 @@ extern "C" int bce_debug_lane_selftest(unsigned* out, void* stream) {
 int wide_key_bits(int64_t max_len) {
   return max_len <= 128 ? 7 : max_len <= 256 ? 8 : max_len <= 512 ? 9 : max_len <= 1024 ? 10 : max_len <= 2048 ? 11
                                                                                                                  : 12;
-}
-
-// All wide bins of a plan (bins 4..11 of bce_plan_bins, 65..4096 signals) in one launch of
-// the team kernel.  a.list = the plan's order; bin_start_host = its bin boundaries.
-int launch_wide_team(const ConsArgs& a, const int64_t* bin_start_host, hipStream_t st) {
-  WideItems q{};
-  q.queue = team_queue_slot();
-  if (!q.queue) {
-    set_error("wide team kernel: no queue words on this device");
-    return BCE_EHIP;
-  }
-  int64_t items = 0;
-  for (int k = 0; k < kTeamBins; ++k) {
-    const int b = 11 - k;  // team bin k <-> plan bin 11 - k (longest first)
-    const int teams = kTeamWaves / (k <= 1 ? 8 : k <= 3 ? 4 : k == 4 ? 2 : 1);
-    q.item_start[k] = (int32_t)items;
-    q.first[k] = (int32_t)bin_start_host[b];
-    q.end[k] = (int32_t)bin_start_host[b + 1];
-    items += (bin_start_host[b + 1] - bin_start_host[b] + teams - 1) / teams;
-  }
-  q.item_start[kTeamBins] = (int32_t)items;
-  q.n_items = (int32_t)items;
-  if (items == 0) return BCE_OK;
-  BCE_REQUIRE(items < (1ll << 30), "wide team kernel: too many items");
-  const void* fn = (a.mode == BCE_MODE_FAST) ? reinterpret_cast<const void*>(&consensus_wide_team_kernel<true>)
-                                             : reinterpret_cast<const void*>(&consensus_wide_team_kernel<false>);
-  const int per_cu = blocks_per_cu(fn, 64 * kTeamWaves, 0, 1, "consensus_wide_team_kernel");
-  int64_t grid = (int64_t)cu_count() * per_cu;
-  if (grid > items) grid = items;
-  if (a.mode == BCE_MODE_FAST)
-    hipLaunchKernelGGL((consensus_wide_team_kernel<true>), dim3((int)grid), dim3(64 * kTeamWaves), 0, st, a, q);
-  else
-    hipLaunchKernelGGL((consensus_wide_team_kernel<false>), dim3((int)grid), dim3(64 * kTeamWaves), 0, st, a, q);
-  return check_launch("consensus_wide_team_kernel");
 }
 
 int launch_wide_len(int64_t max_len, const ConsArgs& a, hipStream_t st) {

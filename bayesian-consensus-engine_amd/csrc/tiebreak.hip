@@ -55,13 +55,16 @@ constexpr int kFaultRoundOverflow = 6;  // round(x, nd) too large to represent (
 // round(prediction, precision) of tiebreak.py:54 for every precision CPython accepts (see
 // tb_round_mode on the host).  EXOTIC kernels (modes 4, 5: 10^|nd| not an exact double) run
 // the exact big-integer restatement of py_round_big.hpp; the others never contain it.
+// report: this lane's value is really rounded by the reference -- an agent of a market with
+// >= 2 agents (a single agent keeps its raw prediction, tiebreak.py:89-96, and lanes without a
+// market round a placeholder) -- so its OverflowError is raised.
 template <bool EXOTIC>
-__device__ __forceinline__ double tb_round(double x, const TbArgs& a) {
+__device__ __forceinline__ double tb_round(double x, const TbArgs& a, bool report = true) {
   if constexpr (EXOTIC) {
     if (a.rmode == 4) return bce_round::round_pos(x, a.rnd);
     bool ovf = false;
     const double r = bce_round::round_neg(x, -a.rnd, &ovf);
-    if (ovf && a.fault) atomicCAS(a.fault, 0, kFaultRoundOverflow);
+    if (ovf && report && a.fault) atomicCAS(a.fault, 0, kFaultRoundOverflow);
     return r;
   } else {
     switch (a.rmode) {
@@ -127,7 +130,11 @@ __global__ __launch_bounds__(256) void tiebreak_wave_kernel(TbArgs a, const int3
     const int64_t m = list ? list[li] : li;
     const int64_t off = a.offsets[m];
     const int n = (int)(a.offsets[m + 1] - off);
-    if (n == 0) {  // tiebreak.py:86-87 (ValueError)
+    // n == 0: tiebreak.py:86-87 (ValueError).  n > 64: longer than this kernel's lanes (a
+    // max_len bound the caller got wrong) -- left unprocessed with the empty marker and
+    // reported in the fault word, never computed from wrapped lanes
+    if (n == 0 || n > 64) {
+      if (n > 64) raise_fault(a.fault, kFaultTooLong);
       if (lane == 0) {
         a.winner[m] = 0.0; a.label[m] = -1; a.n_groups[m] = -1; a.variance[m] = 0.0;
       }
@@ -251,16 +258,10 @@ constexpr int kTbLpmWaves = 4;
 constexpr int kTbStage = 64 * kTbLpmMax + 64;  // doubles per wave buffer: a tile's agents + pads
 constexpr int kTbStageIt = 64 * kTbLpmMax / 128;  // 16-B loads per lane for a full tile
 constexpr int kTbStageBatch = 4;                  // of them in flight together (2 x 8 VGPRs each)
-// How a STAGED tile's arrays reach LDS:
-//   0  16-B loads into registers, kTbStageBatch in flight, then ds_writes (two workgroups of
-//      four waves per CU): 0.851 ms for the 1M x 32 tb line;
-//   1  LDS-DMA (global_load_lds_dword, 64 per array) into the one buffer, then vmcnt(0):
-//      1.070 ms (0.849-0.866 for mode 0 on the same box, profiles/r04f/);
-//   2  two buffers per wave filled by LDS-DMA, the next array streaming in under the current
-//      phase -- one workgroup per CU (1 wave per SIMD, 135 KB of LDS): 1.316 ms, VALU active
-//      32% of wave cycles but nothing else issues while that wave waits (profiles/r04e/).
-constexpr int kTbStageMode = 0;
-constexpr bool kTbDMA = kTbStageMode == 2;
+// A STAGED tile's arrays reach LDS as 16-B loads into registers, kTbStageBatch in flight, then
+// ds_writes (two workgroups of four waves per CU).  LDS-DMA staging into the one buffer (1.070 vs
+// 0.849-0.866 ms, profiles/r04f/) and two DMA-filled buffers per wave (one workgroup per CU:
+// 1.316 ms, profiles/r04e/) were measured and removed.
 
 __device__ __forceinline__ int tb_pad(int i) { return i + (i >> 5); }
 constexpr bool kTbFullKeysInLds = true;  // FULL tiles: sort (ordinal, agent) alone, keys via LDS
@@ -271,15 +272,9 @@ constexpr int kTbDump = 64;
 constexpr int kTbFullBatchPC = 8;
 constexpr int kTbFullBatchWR = 8;
 constexpr bool kTbPrefetchMeta = true;
-// FULL tiles: the next array's first batch issued before the phase's output flushes (the
-// stage then waits for loads, not for the flushes' stores): 36 spilled VGPRs, 0.712-0.716 vs
-// 0.664 ms (profiles/r04aa/) -- off
-constexpr bool kTbPreBatch = false;
-// FULL tiles: while a phase computes, two dword loads per lane pull the next phase's 16-KB
-// array into L2 (its 128 lines), so the stage that follows finds it there.  Off: -0.5% time
-// (0.706 vs 0.709-0.711 ms, profiles/r04k/) for FETCH_SIZE +27% (the dword touches are
-// tallied like gathers, so the line's PMC traffic stops meaning HBM bytes, profiles/r04m/).
-constexpr bool kTbTouchNext = false;
+// (FULL tiles, measured and removed: the next array's first batch issued before the phase's
+// output flushes -- 36 spilled VGPRs, 0.712-0.716 vs 0.664 ms, profiles/r04aa/; dword touches of
+// the next phase's array -- -0.5% time for +27% FETCH_SIZE, profiles/r04k/, r04m/.)
 // nontemporal hints on the staged input loads / the flushed output stores (both off: 0.727-0.730
 // ms vs 0.712 for the 1M x 32 line, profiles/r04j/)
 constexpr bool kTbNtLoad = true;
@@ -305,29 +300,19 @@ __device__ __forceinline__ unsigned tb_bits(unsigned m) {
   return m;
 }
 
-template <bool STAGED>
-struct TbLpmCfg {
-  static constexpr bool DB = STAGED && kTbDMA;
-  static constexpr int WPE = DB ? 1 : 2;  // waves per SIMD (VGPR budget 512 / 256)
-};
-
-// s_waitcnt vmcnt(63): everything but the last 63 vector-memory instructions has landed --
-// with the 64 DMAs of the next array just issued, the array before them is in LDS
-__device__ __forceinline__ void tb_wait_dma_but_next() { __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | (15 << 8) | (3 << 14)); }
-__device__ __forceinline__ void tb_wait_dma_all() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0)
+constexpr int kTbLpmWPE = 2;  // waves per SIMD (VGPR budget 256)
 
 // PART (STAGED launches): 1 = only FULL tiles, 2 = every other tile; 0 = all tiles, one body.
 // (Both bodies in one kernel: 21 spilled VGPRs and 190 SGPRs, so two launches.)
 template <bool STAGED, bool EXOTIC, int PART = 0>
-__global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_eu(TbLpmCfg<STAGED>::WPE, TbLpmCfg<STAGED>::WPE))) void tiebreak_lpm_kernel(TbArgs a, const int32_t* list,
+__global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_eu(kTbLpmWPE, kTbLpmWPE))) void tiebreak_lpm_kernel(TbArgs a, const int32_t* list,
                                                                          int64_t n_list, int* fault) {
-  constexpr bool DB = TbLpmCfg<STAGED>::DB;
-  static_assert(PART == 0 || (STAGED && !DB && !EXOTIC), "FULL / rest split: staged register-batch kernels only");
-  // one buffer per wave (16.9 KB; two workgroups of four waves per CU), or two (DB)
-  __shared__ double sBuf[STAGED ? kTbLpmWaves : 1][DB ? 2 : 1][STAGED ? kTbStage + kTbDump : 1];
+  static_assert(PART == 0 || (STAGED && !EXOTIC), "FULL / rest split: staged kernels only");
+  // one buffer per wave (16.9 KB; two workgroups of four waves per CU)
+  __shared__ double sBuf[STAGED ? kTbLpmWaves : 1][STAGED ? kTbStage + kTbDump : 1];
   // FULL tiles: RN(1 / c) for group sizes c = 1..32 (tb_div_small)
   constexpr bool kFullBody = PART == 1;
-  constexpr bool kRcTab = STAGED && !DB;  // group means via the reciprocal table
+  constexpr bool kRcTab = STAGED;  // group means via the reciprocal table
   __shared__ double sRc[kRcTab ? kTbLpmMax + 1 : 1];
   if constexpr (kRcTab) {
     if (threadIdx.x <= (unsigned)kTbLpmMax) sRc[threadIdx.x] = 1.0 / (double)(threadIdx.x ? threadIdx.x : 1);
@@ -335,12 +320,8 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
   }
   const int lane = lane_id();
   const int wv = STAGED ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;  // uniform: LDS bases in SGPRs
-  double* buf = sBuf[wv][0];
-  int32_t* ibuf = reinterpret_cast<int32_t*>(buf);
-  auto use_buf = [&](int k) {
-    buf = sBuf[wv][DB ? k : 0];
-    ibuf = reinterpret_cast<int32_t*>(buf);
-  };
+  double* const buf = sBuf[wv];
+  int32_t* const ibuf = reinterpret_cast<int32_t*>(buf);
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   // a tile's metadata: this lane's market and the tile's agent range [B, B + cnt)
@@ -404,41 +385,21 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     }
     return t;
   };
-  // DB: one array of a tile into buffer k by LDS-DMA -- 256-B segments (32 doubles, one padded
-  // row) per instruction, always 64 of them (vmcnt accounting); lanes past the data re-read
-  // the tile's first dword into slack
-  auto dma_arr = [&](const double* src, int k, const Meta& t) {
-    const uint32_t* g = reinterpret_cast<const uint32_t*>(src + t.B);
-    const int nd = 2 * t.cnt;
-    double* dst = sBuf[wv][DB ? k : 0];
-    wave_sync_lds();  // this wave's reads of the buffer (the last flush) are done
-#pragma unroll 1
-    for (int q = 0; q < 64; ++q) {
-      const int d = 64 * q + lane;
-      dma_b32(g + (d < nd ? d : 0), dst + 33 * q);
-    }
-  };
   Meta cur{};
-  if constexpr (DB) {
-    cur = meta_of(wave);
-    if (cur.skip == 0) dma_arr(a.pred, 0, cur);
-  }
   // PART 2 has nothing to do when PART 1 found every tile full (the common uniform batch):
   // it then only counts itself out
   bool run = true;
-  int pfsink = 0;  // kTbTouchNext: consumes the touch loads
   // (one word per wave: a single flag word took every skipping wave's store through the
   // device-coherent path to one address -- 0.55 ms of serialised stores on a ragged batch)
-  if constexpr (PART == 2) run = a.split[wave] == a.ticket;
+  // Words are shared round-robin by launch pairs (capi.hip split_slot), possibly on other
+  // streams: PART 1 raises its word to its ticket with atomicMax, and PART 2 runs when the word
+  // holds its own ticket or a NEWER pair's (then it may run for nothing -- it skips FULL tiles
+  // itself -- but never skips a tile its own PART 1 left).  Tickets are positive and
+  // increase; after a wrap a stale larger ticket only makes PART 2 run for nothing.
+  if constexpr (PART == 2) run = a.split[wave] >= a.ticket;
   bool left = false;  // PART 1: this wave left a tile to PART 2
   for (int64_t tile = wave; run && tile * 64 < n_list; tile += nwaves) {
-    Meta nxt{};
-    if constexpr (DB) {
-      nxt = meta_of(tile + nwaves);  // (its loads wait out this tile's prediction DMA too)
-      nxt.skip = (tile + nwaves) * 64 < n_list ? nxt.skip : 3;
-    } else {
-      cur = meta_of(tile);
-    }
+    cur = meta_of(tile);
     if constexpr (PART == 1) {
       if (!cur.full) {  // (skipped tiles are never full)
         left = true;
@@ -453,10 +414,6 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     if (cur.skip) {
       if (has) {
         a.winner[m] = 0.0; a.label[m] = -1; a.n_groups[m] = -1; a.variance[m] = 0.0;
-      }
-      if constexpr (DB) {
-        if (nxt.skip == 0) dma_arr(a.pred, 0, nxt);
-        cur = nxt;
       }
       continue;
     }
@@ -473,11 +430,6 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     // per-iteration loop paid ~16 serial HBM latencies per array and tile)
     auto stage = [&](const double* src) {
       wave_sync_lds();  // the buffer's previous readers (this wave) are done
-      if constexpr (kTbStageMode == 1) {
-        dma_arr(src, 0, cur);
-        tb_wait_dma_all();
-        return;
-      }
       if (((uintptr_t)(src + B) & 15) == 0) {
 #pragma unroll 1
         for (int k0 = 0; k0 < kTbStageIt; k0 += kTbStageBatch) {
@@ -520,30 +472,11 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
       wave_sync_lds();
     };
     // FULL tiles (2048 agents): no bounds checks, NB 16-B loads per lane in flight
-    // kTbPreBatch: the next array's first NB loads are issued before the phase's output
-    // flushes, so the stage that follows waits for loads only, not for the flushes' stores
-    // (vmcnt counts both, in order)
-    double2 pv[kTbFullBatchPC];
-    auto pre_issue = [&](const double* src) {
-#pragma unroll
-      for (int k = 0; k < kTbFullBatchPC; ++k) pv[k] = tb_ld2(src + B + 2 * lane + 128 * k);
-    };
-    auto stage_full = [&](const double* src, auto nb, bool pre = false) {
+    auto stage_full = [&](const double* src, auto nb) {
       constexpr int NB = decltype(nb)::value;  // (src + B is 16-B aligned: see Meta::full)
-      static_assert(!kTbPreBatch || NB == kTbFullBatchPC, "the preloaded batch is one staging batch");
       wave_sync_lds();
-      int k0 = 0;
-      if (pre) {
-#pragma unroll
-        for (int k = 0; k < NB; ++k) {
-          const int e = 2 * lane + 128 * k;
-          buf[tb_pad(e)] = pv[k].x;
-          buf[tb_pad(e + 1)] = pv[k].y;
-        }
-        k0 = NB;
-      }
 #pragma unroll 1
-      for (; k0 < kTbStageIt; k0 += NB) {
+      for (int k0 = 0; k0 < kTbStageIt; k0 += NB) {
         double2 v[NB];
 #pragma unroll
         for (int k = 0; k < NB; ++k) v[k] = tb_ld2(src + B + 2 * lane + 128 * (k0 + k));
@@ -628,18 +561,8 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
 #pragma unroll
           for (int p = 0; p < N; ++p) u[p] = tb_bits(u[p]);
         };
-        int pf0 = 0, pf1 = 0;
-        auto touch = [&](const double* src) {
-          if constexpr (kTbTouchNext) {
-            const int* q = reinterpret_cast<const int*>(src + B) + 32 * lane;
-            pf0 = q[0];
-            pf1 = q[2048];
-          }
-        };
-        auto settle = [&]() { pfsink ^= pf0 ^ pf1; };  // (the loads landed long ago)
         // 1. keys, first-seen ordinals, sort
         stage_full(a.pred, std::integral_constant<int, kTbFullBatchPC>{});
-        touch(a.weight);
         double kp[N];  // (PART 1 runs only for round mode 0, see launch_tb_short)
 #pragma unroll
         for (int t = 0; t < N; ++t) {
@@ -659,7 +582,6 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
             ngf += g < 0 ? 1 : 0;
             u[t] = ((unsigned)go[t] << 5) | (unsigned)t;
           }
-          if constexpr (kTbPreBatch) pre_issue(a.weight);
           if (a.g_of) {
             wave_sync_lds();
 #pragma unroll
@@ -723,9 +645,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
         }
         // 3. densities
         double densp[N];
-        settle();
-        stage_full(a.weight, std::integral_constant<int, kTbFullBatchWR>{}, kTbPreBatch);
-        touch(a.rel);
+        stage_full(a.weight, std::integral_constant<int, kTbFullBatchWR>{});
         {
           const unsigned st_ = tb_bits(stm), en_ = tb_bits(enm);
           refresh_u();
@@ -739,15 +659,12 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
             densp[p] = tb_div_small(tot, cnt, sRc);
             put_sel(en_, p, u[p] >> 5, densp[p]);
           }
-          if constexpr (kTbPreBatch) pre_issue(a.rel);
           if (a.g_density) flush(a.g_density);
         }
         // 4. max reliability per group, the winner and the tie flag
         double bd = 0.0, bm = 0.0, bk = 0.0;
         bool tie = false;
-        settle();
-        stage_full(a.rel, std::integral_constant<int, kTbFullBatchWR>{}, kTbPreBatch);
-        touch(a.conf);
+        stage_full(a.rel, std::integral_constant<int, kTbFullBatchWR>{});
         {
           const unsigned st_ = tb_bits(stm), en_ = tb_bits(enm);
           refresh_u();
@@ -768,12 +685,10 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
             bm = upd ? mx : bm;
             bk = upd ? kp[p] : bk;
           }
-          if constexpr (kTbPreBatch) pre_issue(a.conf);
           if (a.g_maxrel) flush(a.g_maxrel);
         }
         // 5. variance (input order), per-group mean confidences
-        settle();
-        stage_full(a.conf, std::integral_constant<int, kTbFullBatchPC>{}, kTbPreBatch);
+        stage_full(a.conf, std::integral_constant<int, kTbFullBatchPC>{});
         if (kTbPrefetchMeta && (tile + nwaves) * 64 < n_list) meta_pre(tile + nwaves);
         double variance;
         {
@@ -839,13 +754,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
 #pragma unroll
       for (int p = 0; p < kTbLpmMax; ++p) u[p] = tb_bits(u[p]);
     };
-    if constexpr (DB) {
-      dma_arr(a.weight, 1, cur);  // streams in under phase 1
-      tb_wait_dma_but_next();     // the predictions are in buffer 0
-      use_buf(0);
-    } else if constexpr (STAGED) {
-      stage(a.pred);
-    }
+    if constexpr (STAGED) stage(a.pred);
     const double praw0 = at(a.pred, 0);  // a single agent keeps its raw prediction (tiebreak.py:89-96)
     {
       if (!EXOTIC && a.rmode == 0) {  // the common precisions: rint fast path, exact redo if flagged
@@ -858,7 +767,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
         }
       } else {
 #pragma unroll
-        for (int t = 0; t < kTbLpmMax; ++t) kp[t] = tb_round<EXOTIC>(at(a.pred, min(t, last)), a);
+        for (int t = 0; t < kTbLpmMax; ++t) kp[t] = tb_round<EXOTIC>(at(a.pred, min(t, last)), a, n >= 2);
       }
       const unsigned vm1 = tb_bits(vm);
       int go[kTbLpmMax];
@@ -926,13 +835,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     // every group <= g, and agent g (ordinal <= g) belongs to one of those -- consumed.
     // (Positions past n read slot min(31, ...) of the lane's row or the tile's slack: never used.)
     double densp[kTbLpmMax];
-    if constexpr (DB) {
-      dma_arr(a.rel, 0, cur);
-      tb_wait_dma_but_next();  // the weights are in buffer 1
-      use_buf(1);
-    } else if constexpr (STAGED) {
-      stage(a.weight);
-    }
+    if constexpr (STAGED) stage(a.weight);
     {
       const unsigned st_ = tb_bits(stm), en_ = tb_bits(enm);
       refresh_ug();
@@ -955,13 +858,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     // ---- 4. reliabilities: max per group (first maximum kept), the winner ------------------
     double bd = 0.0, bm = 0.0, bk = 0.0;
     bool tie = false;
-    if constexpr (DB) {
-      dma_arr(a.conf, 1, cur);
-      tb_wait_dma_but_next();  // the reliabilities are in buffer 0
-      use_buf(0);
-    } else if constexpr (STAGED) {
-      stage(a.rel);
-    }
+    if constexpr (STAGED) stage(a.rel);
     {
       const unsigned st_ = tb_bits(stm), en_ = tb_bits(enm);
       refresh_ug();
@@ -990,17 +887,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     }
 
     // ---- 5. confidences: variance (input order), then the per-group means -----------------
-    if constexpr (DB) {
-      if (nxt.skip == 0) {
-        dma_arr(a.pred, 0, nxt);  // the next tile's predictions stream in under phase 5
-        tb_wait_dma_but_next();
-      } else {
-        tb_wait_dma_all();
-      }
-      use_buf(1);  // the confidences
-    } else if constexpr (STAGED) {
-      stage(a.conf);
-    }
+    if constexpr (STAGED) stage(a.conf);
     double variance;
     {
       const unsigned vm5 = tb_bits(vm);
@@ -1059,11 +946,8 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
         a.variance[m] = (n == 1) ? 0.0 : variance;
       }
     }
-    if constexpr (DB) cur = nxt;
   }
-  if constexpr (DB) tb_wait_dma_all();  // no DMA outlives the wave
-  if (PART == 1 && pfsink == 0x5bd1e995 && n_list < 0) a.label[0] = pfsink;  // never: keeps the touches
-  if (PART == 1 && left && lane == 0) a.split[wave] = a.ticket;
+  if (PART == 1 && left && lane == 0) atomicMax(&a.split[wave], a.ticket);
 }
 
 // n > 64: one workgroup per market.  (rounded key, index) pairs are bitonic-sorted in
@@ -1296,7 +1180,7 @@ static int launch_tb_short(const TbArgs& a, const int32_t* market_list, int64_t 
     // run a kernel specialised for them, then a second launch takes every other tile (each
     // launch only reads the offsets of the tiles it leaves to the other)
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-    bool split = kTbStageMode != 2 && !EXOTIC && a.rmode == 0 && al16(a.pred) && al16(a.conf) &&
+    bool split = !EXOTIC && a.rmode == 0 && al16(a.pred) && al16(a.conf) &&
                  al16(a.weight) && al16(a.rel);
     const void* fn = market_list ? reinterpret_cast<const void*>(&tiebreak_lpm_kernel<false, EXOTIC>)
                      : split     ? reinterpret_cast<const void*>(&tiebreak_lpm_kernel<true, false, 1>)
@@ -1313,7 +1197,8 @@ static int launch_tb_short(const TbArgs& a, const int32_t* market_list, int64_t 
       static std::atomic<int> tickets{0};
       TbArgs b = a;
       b.split = split_slot();
-      do b.ticket = tickets.fetch_add(1) + 1; while (b.ticket == 0);
+      // positive; after a wrap, older (larger) tickets left in words only make PART 2 run
+      b.ticket = (tickets.fetch_add(1) & 0x3fffffff) + 1;
       if (!b.split) {
         set_error("tiebreak: no device split words");
         return BCE_EHIP;

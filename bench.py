@@ -67,6 +67,8 @@ def parse(argv=None):
                    help="consensus summation mode (default: exact for c2, where it costs nothing; fast -- "
                         "the north star's fixed-order trees within 1e-9 -- for c3, with the exact-mode "
                         "time reported beside it)")
+    p.add_argument("--c3-sources", type=int, default=1_000_000,
+                   help="c3: Zipf source universe (SURVEY d3: 1M; 2M / 10M = the large-table lines)")
     p.add_argument("--agents", type=int, default=16384, help="config 5 agents")
     p.add_argument("--compact", action="store_true",
                    help="c2: scalars only (consensus, confidence, total weight, uniqueSources, validation) -- "

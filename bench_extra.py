@@ -253,7 +253,7 @@ def _graphed(step, dev):
 def _c3(args, world, rank, barrier, max_over, sum_over):
     from bayesian_engine import batch
 
-    S = 1_000_000
+    S = getattr(args, "c3_sources", 1_000_000)
     total = 100_000_000
     M, off, sid, prob, table_host = make_c3(world, rank, total, S)
     n = int(off[-1])
@@ -321,7 +321,7 @@ def _c3(args, world, rank, barrier, max_over, sum_over):
                    "markets_this_rank": Mloc, "signals_this_rank": n, "unique_per_market_mean": sum_u / max(Mloc, 1),
                    "bins": plan.bin_start.tolist(), "parallelism": f"markets sharded over {world} rank(s), no collective"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc("pmc_c3.json", signals_this_rank=n),
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc("pmc_c3.json", signals_this_rank=n) if S == 1_000_000 else None,
                      "kernel": "consensus (all bins, one step)",
                      "bytes_per_launch": bytes_step, "avg_launch_ms": per * 1e3,
                      f"{other}_mode": ({"ms_per_step": wall2 / a2.steps * 1e3, "avg_launch_ms": per2 * 1e3,
@@ -882,7 +882,7 @@ def c3_shards(args):
     a2 = copy.copy(args)
 
     def time_one(w, r):
-        M, off, sid, prob, (rel_h, conf_h, present) = make_c3(w, r)
+        M, off, sid, prob, (rel_h, conf_h, present) = make_c3(w, r, S=getattr(args, "c3_sources", 1_000_000))
         T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
         table = batch.SourceTable.from_arrays(T(rel_h), T(conf_h), T(present))
         d_off, d_sid, d_prob = T(off), T(sid), T(prob)

@@ -86,11 +86,6 @@ int bce_debug_set_spin_cap(int cap);
 /* Self-test of the wide kernel's VALU lane exchanges (DPP / permlane swaps) and wave scan:
  * one wave writes 13*64 words to `out` (see consensus_wide.hip); tests run it first. */
 int bce_debug_lane_selftest(unsigned* out, void* stream);
-/* A/B hook: 1 makes bce_consensus_planned run every wide bin (65..4096 signals) in one
- * persistent launch of the all-bins team kernel (8-wave workgroups pulling items of 8/NW
- * markets from a device queue); 0 (the default) launches one kernel per wide bin.  Returns
- * the previous setting.  (Environment: BCE_WIDE_TEAM=1.) */
-int bce_debug_set_wide_team(int on);
 /* Host run of the exact big-integer round(x, ndigits) the tie-break kernels use for
  * 23 <= ndigits <= 323 and -308 <= ndigits <= -16 (valid for any 1 <= |ndigits| in range):
  * for the CPU tests against Python round().  *overflow = 1 where CPython raises

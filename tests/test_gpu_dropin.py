@@ -914,6 +914,41 @@ def test_tiebreak_max_len_skips_host_scan():
         N.check_faults(torch.device("cuda", 0), "max_len too small")
 
 
+def test_tiebreak_wave_kernel_reports_market_longer_than_64():
+    """max_len=64 selects the wave-per-market kernel; a 100-agent market inside the batch is
+    left with the empty marker and reported by the fault word -- never computed from wrapped
+    lanes.  The 64-agent market beside it is still computed."""
+    import torch
+    from bayesian_engine import _native as N
+    from bayesian_engine import batch
+    lens = np.array([64, 100, 5], np.int64)
+    off, pred, conf, weight, rel = _tb_inputs(lens, 33)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    r = batch.tiebreak(T(off), T(pred), T(conf), T(weight), T(rel), max_len=64)
+    with pytest.raises(N.BCEError, match="longer than"):
+        N.check_faults(torch.device("cuda", 0), "max_len 64, a 100-agent market")
+    assert int(r.n_groups[1].item()) == -1 and int(r.label[1].item()) == -1
+    assert int(r.n_groups[0].item()) >= 1 and int(r.n_groups[2].item()) >= 1
+
+
+def test_tiebreak_exotic_single_agent_huge_prediction_does_not_raise():
+    """precision -308 with a huge prediction alone in its market: the reference returns
+    agents[0].prediction unrounded (tiebreak.py:89-96) and raises nothing, so the lane kernel
+    must not report round()'s overflow for 1-agent (or empty) markets."""
+    import torch
+    from bayesian_engine import _native as N
+    from bayesian_engine import batch
+    off = np.array([0, 1, 3, 3], np.int64)  # a 1-agent market, a 2-agent market, an empty one
+    pred = np.array([1.7e308, 0.5, 0.25])
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    ones = np.ones(3)
+    r = batch.tiebreak(T(off), T(pred), T(ones * 0.5), T(ones), T(ones * 0.5), precision=-308, offsets_host=off)
+    torch.cuda.synchronize()
+    N.check_faults(torch.device("cuda", 0), "exotic precision, single huge agent")
+    assert float(r.winner[0].item()) == 1.7e308
+    assert float(r.winner[1].item()) == round(0.5, -308)
+
+
 @pytest.mark.parametrize("precision", [6, 0, -2, 30])
 def test_tiebreak_ragged_lane_kernel_vs_oracle(precision):
     """Markets of 0..32 agents (every tile ragged: the general lane-per-market body, PART 2 of

@@ -207,14 +207,10 @@ def test_wide_ordered_inputs(pattern, mode):
 
 
 @pytest.mark.parametrize("mode", MODES)
-def test_wide_team_kernel_matches_per_bin_launches(mode):
-    """The all-bins team kernel (one persistent launch, 8-wave workgroups pulling items of
-    8/NW markets from a device queue, lockstep teams) against one launch per bin: EXACT
-    bit-identical; FAST within 1e-9 of the oracle either way and bit-identical wherever both
-    paths use the same team shape (every bin but 1025..1536 and 2049..3072, which the team
-    kernel runs on 4 / 8 waves instead of 3 / 6).  Bin sizes leave short last items (dummy
-    teams), and one bin is empty."""
-    from bayesian_engine import _native as N
+def test_wide_planned_every_bin_vs_oracle(mode):
+    """One planned call over every wide bin (65..128 .. 3073..4096, the non-power-of-two 1536 /
+    3072 bins included) plus short markets, one bin empty: within 1e-9 of the oracle in FAST and
+    bit-exact in EXACT, and a second call reproduces every bit."""
     rng = np.random.default_rng(77)
     lens = np.concatenate([rng.integers(65, 129, 37), rng.integers(129, 257, 9), rng.integers(513, 1025, 7),
                            rng.integers(1025, 1537, 3), rng.integers(1537, 2049, 5), rng.integers(3073, 4097, 3),
@@ -222,22 +218,8 @@ def test_wide_team_kernel_matches_per_bin_launches(mode):
     rng.shuffle(lens)
     g = _zipf_case(lens, 200_000, 77, base=11)
     exp = orc.consensus_csr(g["offsets"], g["sid"], g["prob"], g["rel"], g["conf"], g["present"])
-    L = N.lib()
-    outs = {}
-    for team in (1, 0):
-        prev = L.bce_debug_set_wide_team(team)
-        try:
-            outs[team] = _run(g, mode=mode)
-        finally:
-            L.bce_debug_set_wide_team(prev)
-        _compare_vec(outs[team], exp, g["offsets"], exact=(mode == "exact"))
-    same = (lens <= 1024) | ((lens > 1536) & (lens <= 2048)) | (lens > 3072)
-    for k in ("consensus", "confidence", "total_weight", "n_unique", "err_idx"):
-        if mode == "exact":
-            assert np.array_equal(outs[1][k], outs[0][k], equal_nan=True), k
-        else:
-            assert np.array_equal(outs[1][k][same], outs[0][k][same], equal_nan=True), k
-    # repeated launches reuse the queue words (each launch leaves its pair zeroed)
+    out = _run(g, mode=mode)
+    _compare_vec(out, exp, g["offsets"], exact=(mode == "exact"))
     again = _run(g, mode=mode)
-    for k in ("consensus", "n_unique", "usid"):
-        assert np.array_equal(again[k], outs[1][k], equal_nan=True), k
+    for k in ("consensus", "confidence", "total_weight", "n_unique", "usid", "weight", "nweight"):
+        assert np.array_equal(again[k], out[k], equal_nan=True), k

@@ -24,7 +24,9 @@ for f in glob.glob(os.path.join(o, "p*", "**", "*counter_collection.csv"), recur
         k = r["Kernel_Name"]
         if "bce::" not in k:
             continue
-        k = k.split("(")[0].replace("void bce::", "").replace("(anonymous namespace)::", "")
+        # drop the namespace before cutting at the argument list: "(anonymous namespace)" holds
+        # the first "(" of every kernel in an unnamed namespace
+        k = k.replace("(anonymous namespace)::", "").replace("void bce::", "").split("(")[0]
         acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
 for k, d in sorted(acc.items()):
     print(k)

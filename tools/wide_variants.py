@@ -27,47 +27,20 @@ OUT = tab_variants.OUT
 # EXACT np2 split, FAST np2 merge, no DPP fusion, no swap stages, the s_memtime phase timer,
 # gather windows, late probabilities, dedup-before-sort, M0 save/restore) were source patches
 # of the pre-round-4 kernel; their results are in DESIGN.md §4.2 and profiles/archive/r03*/.  They no
-# longer apply to the refactored per-market body and were dropped.  The all-bins team kernel
-# against one launch per bin is a runtime switch: BCE_WIDE_TEAM=0 with "wbase".
+# longer apply to the refactored per-market body and were dropped.
+# Round 5: the all-bins team kernel, the rotated sorted-probability layout (kWideSwz) and the
+# tie-break's LDS-DMA staging (kTbStageMode 1/2), pre-issued batches (kTbPreBatch) and next-array
+# touches (kTbTouchNext) were removed from csrc/ (verdict r04 item 7); their A/Bs are recorded in
+# DESIGN.md §4.2 / §4.9 and profiles/r04c, r04e, r04f, r04k, r04m, r04aa.
 VARIANTS = {
     "wbase": [],
-    # round-3 thread-major sorted-probability layout (4-way conflicts on the step-3 stores)
-    "wswz": [("consensus_wide.hip", "constexpr bool kWideSwz = false;", "constexpr bool kWideSwz = true;")],
-    # (thread-major layout) the short-market side-stream kernels launched after the team kernel
-    "tafter": [
-               ("consensus.hip", """  if (team) {
-    for (int b = 0; b <= side_last && !rc; ++b) {""", """  if (team) {
-    if (!rc) {
-      ConsArgs a = base;
-      a.list = order;
-      a.n_list = bin_start_host[BCE_NBINS - 1] - bin_start_host[kPlanSideLast + 1];
-      rc = launch_wide_team(a, bin_start_host, st);
-    }
-    for (int b = 0; b <= side_last && !rc; ++b) {"""),
-               ("consensus.hip", """      rc = seg_ok ? launch_seg_for_len(lens[b], a, side) : launch_long_lds(a, side);
-    }
-    if (!rc) {
-      ConsArgs a = base;
-      a.list = order;
-      a.n_list = bin_start_host[BCE_NBINS - 1] - bin_start_host[kPlanSideLast + 1];
-      rc = launch_wide_team(a, bin_start_host, st);
-    }""", """      rc = seg_ok ? launch_seg_for_len(lens[b], a, side) : launch_long_lds(a, side);
-    }""")],
-    # (thread-major layout) the team kernel one workgroup short per two CUs (room for the side stream)
-    "tless": [
-              ("consensus_wide.hip", "  int64_t grid = (int64_t)cu_count() * per_cu;\n  if (grid > items) grid = items;",
-               "  int64_t grid = (int64_t)cu_count() * per_cu - cu_count() / 2;\n  if (grid > items) grid = items;")],
-    # tie-break lane kernel: LDS-DMA staging into the one buffer (1) / two buffers (2)
-    "tbdma1": [("tiebreak.hip", "constexpr int kTbStageMode = 0;", "constexpr int kTbStageMode = 1;")],
-    "tbdma2": [("tiebreak.hip", "constexpr int kTbStageMode = 0;", "constexpr int kTbStageMode = 2;")],
-    # tie-break without the FULL-tile kernel (one general launch, round 3's body)
+    # tie-break FULL tiles: staging batches of the predictions / confidences (shipped: 8)
     "tbpc16": [("tiebreak.hip", "constexpr int kTbFullBatchPC = 8;", "constexpr int kTbFullBatchPC = 16;")],
     "tbpc4": [("tiebreak.hip", "constexpr int kTbFullBatchPC = 8;", "constexpr int kTbFullBatchPC = 4;")],
     # tie-break staging / flush without the nontemporal hints (0.727-0.730 vs 0.712 ms, r04j)
     "tbnont": [("tiebreak.hip", "constexpr bool kTbNtLoad = true;", "constexpr bool kTbNtLoad = false;"),
                ("tiebreak.hip", "constexpr bool kTbNtStore = true;", "constexpr bool kTbNtStore = false;")],
     "tbnopre": [("tiebreak.hip", "constexpr bool kTbPrefetchMeta = true;", "constexpr bool kTbPrefetchMeta = false;")],
-    "tbtouch": [("tiebreak.hip", "constexpr bool kTbTouchNext = false;", "constexpr bool kTbTouchNext = true;")],
     # FULL tiles: staging batches (shipped: 8 and 8)
     "tbwr4": [("tiebreak.hip", "constexpr int kTbFullBatchWR = 8;", "constexpr int kTbFullBatchWR = 4;")],
     "tbwr16": [("tiebreak.hip", "constexpr int kTbFullBatchWR = 8;", "constexpr int kTbFullBatchWR = 16;")],
@@ -78,10 +51,10 @@ VARIANTS = {
     "nsnont": [("elementwise.hip", "constexpr bool kNsNtLoad = true;", "constexpr bool kNsNtLoad = false;"),
                ("elementwise.hip", "constexpr bool kNsNtStore = true;", "constexpr bool kNsNtStore = false;")],
     "aggw1": [("aggregate.hip", "constexpr int kAggWpe = 6;", "constexpr int kAggWpe = 1;")],
-    "tbprebatch": [("tiebreak.hip", "constexpr bool kTbPreBatch = false;", "constexpr bool kTbPreBatch = true;")],
     "tab4w": [("consensus_tab.hip", "constexpr int kTabWaves = 8;", "constexpr int kTabWaves = 4;")],
     "tbkvsort": [("tiebreak.hip", "constexpr bool kTbFullKeysInLds = true;", "constexpr bool kTbFullKeysInLds = false;")],
-    "tbnofull": [("tiebreak.hip", "const bool split = kTbStageMode != 2 && !EXOTIC && a.rmode == 0 && al16(a.pred)",
+    # tie-break without the FULL-tile kernel (one general launch)
+    "tbnofull": [("tiebreak.hip", "bool split = !EXOTIC && a.rmode == 0 && al16(a.pred)",
                   "const bool split = false && al16(a.pred)")],
     # ---- ablations (timing only; outputs are wrong by construction -- no parity gate) ----
     # the sort network run twice (the second pass on sorted keys costs the same)
