@@ -26,12 +26,13 @@ int blocks_per_cu(const void* fn, int threads, size_t lds, int fallback, const c
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (device, kernel).  Thread-safe.
 int ensure_dynamic_lds(const void* fn, int bytes);
 
-// The planned launch's side stream (one per device): side_fork records a fork event on
-// `st`, makes the side stream wait on it and takes the device's fork lock, which the
-// caller holds until side_join has made `st` wait on the side stream's work -- so two host
+// The planned launch's side streams (kSideStreams per device): side_fork records a fork
+// event on `st`, makes the first k side streams wait on it and takes the device's fork lock,
+// which the caller holds until side_join has made `st` wait on their work -- so two host
 // threads planning on different streams never wait on each other's fork/join events.
-int side_fork(hipStream_t st, hipStream_t* side, std::unique_lock<std::mutex>* lock);
-int side_join(hipStream_t st);
+constexpr int kSideStreams = 3;
+int side_fork(hipStream_t st, int k, hipStream_t* sides, std::unique_lock<std::mutex>* lock);
+int side_join(hipStream_t st, int k);
 
 }  // namespace bce
 

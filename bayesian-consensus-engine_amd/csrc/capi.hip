@@ -45,8 +45,8 @@ struct DevCtx {
   int* fault = nullptr;
   hipError_t init_err = hipSuccess;
   std::mutex side_mu;  // held from the plan's fork to its join (bce_consensus_planned)
-  hipStream_t side = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipStream_t side[kSideStreams] = {};  // side[0]: the short-market bins' stream
+  hipEvent_t ev_fork = nullptr, ev_join[kSideStreams] = {};
   int* split = nullptr;               // kQueueSlots blocks of kSplitWords tie-break ticket words
   std::atomic<unsigned> split_next{0};
 };
@@ -63,9 +63,11 @@ DevCtx* dev_ctx() {
     int* p = nullptr;
     hipError_t e = hipMalloc((void**)&p, sizeof(int));
     if (e == hipSuccess) e = hipMemset(p, 0, sizeof(int));  // synchronous: done before first use
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+    for (int k = 0; k < kSideStreams; ++k) {
+      if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side[k], hipStreamNonBlocking);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join[k], hipEventDisableTiming);
+    }
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
     int* sw = nullptr;
     if (e == hipSuccess) e = hipMalloc((void**)&sw, (size_t)kQueueSlots * kSplitWords * sizeof(int));
     if (e == hipSuccess) e = hipMemset(sw, 0, (size_t)kQueueSlots * kSplitWords * sizeof(int));
@@ -133,23 +135,28 @@ int ensure_dynamic_lds(const void* fn, int bytes) {
   return BCE_OK;
 }
 
-int side_fork(hipStream_t st, hipStream_t* side, std::unique_lock<std::mutex>* lock) {
+int side_fork(hipStream_t st, int k, hipStream_t* sides, std::unique_lock<std::mutex>* lock) {
   DevCtx* c = dev_ctx();
-  if (!c || !c->side) {
+  if (k == 0) return BCE_OK;
+  if (!c || !c->side[0] || k < 0 || k > kSideStreams) {
     set_error("side stream unavailable: %s", c ? hipGetErrorString(c->init_err) : "no device");
     return BCE_EHIP;
   }
   *lock = std::unique_lock<std::mutex>(c->side_mu);
   BCE_HIP(hipEventRecord(c->ev_fork, st));
-  BCE_HIP(hipStreamWaitEvent(c->side, c->ev_fork, 0));
-  *side = c->side;
+  for (int i = 0; i < k; ++i) {
+    BCE_HIP(hipStreamWaitEvent(c->side[i], c->ev_fork, 0));
+    sides[i] = c->side[i];
+  }
   return BCE_OK;
 }
 
-int side_join(hipStream_t st) {
+int side_join(hipStream_t st, int k) {
   DevCtx* c = dev_ctx();
-  BCE_HIP(hipEventRecord(c->ev_join, c->side));
-  BCE_HIP(hipStreamWaitEvent(st, c->ev_join, 0));
+  for (int i = 0; i < k; ++i) {
+    BCE_HIP(hipEventRecord(c->ev_join[i], c->side[i]));
+    BCE_HIP(hipStreamWaitEvent(st, c->ev_join[i], 0));
+  }
   return BCE_OK;
 }
 

@@ -51,13 +51,15 @@ constexpr int kWaveRun = 48;  // FAST: duplicate runs longer than this are summe
 // (PN = 64*NN*R, a power of two): NN > NW is a non-power-of-two bin -- the network's
 // missing waves hold +inf keys, so every exchange with them leaves the key in place and
 // they are never materialised (6 waves for 2049..3072 signals, 3 for 1025..1536).
-template <int NW, int R, bool FAST, int NN = NW>
+// KT: the sort key, (sid << IB) | input index -- 32 bits while n_sources <= 2^(32 - IB), else
+// 64 bits (large tables, DESIGN.md §4.2 "Large source tables").
+template <int NW, int R, bool FAST, int NN = NW, class KT = unsigned>
 struct WideCfg {
   static constexpr int NT = 64 * NW;
   static constexpr int P = NT * R;
   static constexpr int PN = 64 * NN * R;
   static constexpr int IB = ilog2c(PN);
-  static constexpr int XROW = R;      // exchange row (u32), two buffers
+  static constexpr int LW = (int)(sizeof(KT) / 4);  // u32 words per key
   static constexpr int HR = (R < kWideHR) ? R : kWideHR;
   // register budget: workgroups of >= 4 waves get 4 waves per SIMD (<= 128 VGPRs), so two
   // LDS-sized workgroups share a CU
@@ -65,11 +67,18 @@ struct WideCfg {
   // CU: C3 fast 1.55 -> 1.72 ms from its spills, profiles/r03g/wide_ab.txt)
   static constexpr int WPE = kWideWPE;
   static constexpr int A_DBL = P + 64;  // + the run sums' read-ahead
-  // region B (u32): sort exchange rows, then leaders [P] (+ exact: chain buffers
+  // region B (u32): sort exchange rows (32-bit keys: two alternating buffers of P words;
+  // 64-bit keys: one buffer of P keys), then leaders [P] keys (+ exact: chain buffers
   // [2][3][NT] doubles + the chain's read-ahead)
-  static constexpr int LEAD_U32 = FAST ? P : P + 2 * (6 * NT + 32);
-  static constexpr int B_U32 = (2 * NT * XROW > LEAD_U32) ? 2 * NT * XROW : LEAD_U32;
+  static constexpr int X_U32 = 2 * P;
+  static constexpr int LEAD_U32 = LW * P + (FAST ? 0 : 2 * (6 * NT + 32));
+  static constexpr int B_U32 = (X_U32 > LEAD_U32) ? X_U32 : LEAD_U32;
 };
+
+// 64-bit key halves through the 32-bit lane primitives
+__device__ __forceinline__ unsigned k_lo(uint64_t v) { return (unsigned)v; }
+__device__ __forceinline__ unsigned k_hi(uint64_t v) { return (unsigned)(v >> 32); }
+__device__ __forceinline__ uint64_t k_make(unsigned hi, unsigned lo) { return ((uint64_t)hi << 32) | lo; }
 
 // v from lane ^ M (whole wave) for the masks the flip-form sort uses -- all VALU, no LDS
 // round trip: DPP for the in-row patterns, the CDNA4 half-exchanges v_permlane16_swap /
@@ -101,6 +110,11 @@ __device__ __forceinline__ unsigned lane_xor(unsigned v) {
     static_assert(M == 1, "unsupported lane distance");
     return v;
   }
+}
+
+template <int M>
+__device__ __forceinline__ uint64_t lane_xor(uint64_t v) {
+  return k_make(lane_xor<M>(k_hi(v)), lane_xor<M>(k_lo(v)));
 }
 
 // Inclusive prefix sum over the wave with DPP (GFX9 row shifts + row broadcasts).
@@ -211,6 +225,37 @@ __device__ __forceinline__ void dpp_stage8(unsigned (&key)[8], uint64_t lower) {
 // in the first register -- so one min/max pair does the stage for both keys, and a second
 // swap puts them back.  Four VALU per two keys, no lane masks.
 template <int M, int R>
+__device__ __forceinline__ void swap_stage(uint64_t (&key)[R]) {  // 64-bit keys: both halves swapped
+#pragma unroll
+  for (int r = 0; r < R; r += 2) {
+    uint64_t a, b;
+    if constexpr (M == 32) {
+      const auto h = __builtin_amdgcn_permlane32_swap(k_hi(key[r]), k_hi(key[r + 1]), false, false);
+      const auto l = __builtin_amdgcn_permlane32_swap(k_lo(key[r]), k_lo(key[r + 1]), false, false);
+      a = k_make(h[0], l[0]);
+      b = k_make(h[1], l[1]);
+    } else {
+      const auto h = __builtin_amdgcn_permlane16_swap(k_hi(key[r]), k_hi(key[r + 1]), false, false);
+      const auto l = __builtin_amdgcn_permlane16_swap(k_lo(key[r]), k_lo(key[r + 1]), false, false);
+      a = k_make(h[0], l[0]);
+      b = k_make(h[1], l[1]);
+    }
+    const uint64_t lo = a < b ? a : b, hi = a < b ? b : a;
+    if constexpr (M == 32) {
+      const auto h = __builtin_amdgcn_permlane32_swap(k_hi(lo), k_hi(hi), false, false);
+      const auto l = __builtin_amdgcn_permlane32_swap(k_lo(lo), k_lo(hi), false, false);
+      key[r] = k_make(h[0], l[0]);
+      key[r + 1] = k_make(h[1], l[1]);
+    } else {
+      const auto h = __builtin_amdgcn_permlane16_swap(k_hi(lo), k_hi(hi), false, false);
+      const auto l = __builtin_amdgcn_permlane16_swap(k_lo(lo), k_lo(hi), false, false);
+      key[r] = k_make(h[0], l[0]);
+      key[r + 1] = k_make(h[1], l[1]);
+    }
+  }
+}
+
+template <int M, int R>
 __device__ __forceinline__ void swap_stage(unsigned (&key)[R]) {
 #pragma unroll
   for (int r = 0; r < R; r += 2) {
@@ -237,15 +282,16 @@ __device__ __forceinline__ void swap_stage(unsigned (&key)[R]) {
 // the first stage of merge K pairs q with q ^ (K-1), the others pair q with q ^ J, and the
 // lower position always keeps the minimum -- no direction bits anywhere.  Threads t >= 64*NW
 // (a non-power-of-two bin's missing waves) hold +inf: their partners keep their own keys.
-template <int NN, int NW, int R, int K, int J>
-__device__ __forceinline__ void wide_stage(unsigned (&key)[R], unsigned* sX, int t, int lane) {
+template <int NN, int NW, int R, int K, int J, class KT>
+__device__ __forceinline__ void wide_stage(KT (&key)[R], unsigned* sX, int t, int lane) {
   constexpr bool flip = (J == K / 2);
+  constexpr bool K64 = sizeof(KT) == 8;
   if constexpr (flip ? (K <= R) : (J < R)) {  // inside a thread: min/max pairs
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int r2 = flip ? (r ^ (K - 1)) : (r | J);
       if (flip ? (r < r2) : ((r & J) == 0)) {
-        const unsigned x = key[r], y = key[r2];
+        const KT x = key[r], y = key[r2];
         key[r] = x < y ? x : y;
         key[r2] = x < y ? y : x;
       }
@@ -253,7 +299,7 @@ __device__ __forceinline__ void wide_stage(unsigned (&key)[R], unsigned* sX, int
   } else if constexpr (flip ? (K <= 64 * R) : (J < 64 * R)) {  // across lanes (never crosses a wave)
     constexpr int MK = flip ? (K / R - 1) : (J / R);
     const bool lower = (lane & (flip ? (K / R / 2) : MK)) == 0;
-    if constexpr (R == 8 && dpp_fusable(MK)) {
+    if constexpr (!K64 && R == 8 && dpp_fusable(MK)) {
       dpp_stage8<MK, flip>(key, (uint64_t)ballot(lower));
       if constexpr (J > 1) wide_stage<NN, NW, R, K, J / 2>(key, sX, t, lane);
       return;
@@ -269,21 +315,60 @@ __device__ __forceinline__ void wide_stage(unsigned (&key)[R], unsigned* sX, int
       // bit 4 -- the pairs are the same; the upper half then holds its bitonic sequence
       // reversed, which the following half-cleaners sort as well (a reversed bitonic
       // sequence is bitonic), so the merge's output is the same sorted sequence
-      unsigned nk[R];
+      KT nk[R];
 #pragma unroll
-      for (int r = 0; r < R; ++r)
-        nk[r] = (unsigned)__builtin_amdgcn_update_dpp((int)key[r], (int)key[R - 1 - r], 0x140, 0xA, 0xF, false);
+      for (int r = 0; r < R; ++r) {
+        if constexpr (K64) {
+          nk[r] = k_make((unsigned)__builtin_amdgcn_update_dpp((int)k_hi(key[r]), (int)k_hi(key[R - 1 - r]), 0x140, 0xA,
+                                                               0xF, false),
+                         (unsigned)__builtin_amdgcn_update_dpp((int)k_lo(key[r]), (int)k_lo(key[R - 1 - r]), 0x140, 0xA,
+                                                               0xF, false));
+        } else {
+          nk[r] = (unsigned)__builtin_amdgcn_update_dpp((int)key[r], (int)key[R - 1 - r], 0x140, 0xA, 0xF, false);
+        }
+      }
 #pragma unroll
       for (int r = 0; r < R; ++r) key[r] = nk[r];
       swap_stage<16, R>(key);
       if constexpr (J > 1) wide_stage<NN, NW, R, K, J / 2>(key, sX, t, lane);
       return;
     }
-    unsigned y[R];
+    KT y[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) y[r] = lane_xor<MK>(key[flip ? R - 1 - r : r]);
 #pragma unroll
     for (int r = 0; r < R; ++r) key[r] = ((key[r] < y[r]) == lower) ? key[r] : y[r];
+  } else if constexpr (K64) {  // across waves, 64-bit keys: one LDS buffer, two barriers
+    constexpr int MT = flip ? (K / R - 1) : (J / R);
+    const bool lower = (t & (flip ? (K / R / 2) : MT)) == 0;
+    // planes of 2 keys: key r of thread t at (r/2)*NT*2 + t*2 + r%2 (16-B accesses, a wave's
+    // 64 accesses consecutive)
+    uint64_t* const buf = reinterpret_cast<uint64_t*>(sX);
+    constexpr int PL = 2 * 64 * NW;  // keys per plane
+#pragma unroll
+    for (int r = 0; r < R; r += 2) {
+      uint4 v;
+      v.x = k_lo(key[r]); v.y = k_hi(key[r]); v.z = k_lo(key[r + 1]); v.w = k_hi(key[r + 1]);
+      *reinterpret_cast<uint4*>(buf + (r >> 1) * PL + t * 2) = v;
+    }
+    __syncthreads();
+    uint64_t y[R];
+    const bool real = NN == NW || (t ^ MT) < 64 * NW;  // partner in a missing wave: +inf
+#pragma unroll
+    for (int r = 0; r < R; r += 2) {
+      const uint4 v = real ? *reinterpret_cast<const uint4*>(buf + (r >> 1) * PL + (t ^ MT) * 2)
+                           : make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+      y[r] = k_make(v.y, v.x);
+      y[r + 1] = k_make(v.w, v.z);
+    }
+    __syncthreads();  // every read done before the next stage rewrites the buffer
+    if (__builtin_amdgcn_readfirstlane((int)lower)) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) key[r] = key[r] < y[flip ? R - 1 - r : r] ? key[r] : y[flip ? R - 1 - r : r];
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) key[r] = key[r] < y[flip ? R - 1 - r : r] ? y[flip ? R - 1 - r : r] : key[r];
+    }
   } else {  // across waves, through LDS rows; buffers alternate, so the previous reads
             // of this buffer finished before the last stage's barrier
     constexpr int MT = flip ? (K / R - 1) : (J / R);
@@ -321,8 +406,8 @@ __device__ __forceinline__ void wide_stage(unsigned (&key)[R], unsigned* sX, int
   if constexpr (J > 1) wide_stage<NN, NW, R, K, J / 2>(key, sX, t, lane);
 }
 
-template <int NN, int NW, int R, int K = 2>
-__device__ __forceinline__ void wide_sort(unsigned (&key)[R], unsigned* sX, int t, int lane) {
+template <int NN, int NW, int R, int K = 2, class KT>
+__device__ __forceinline__ void wide_sort(KT (&key)[R], unsigned* sX, int t, int lane) {
   wide_stage<NN, NW, R, K, K / 2>(key, sX, t, lane);
   if constexpr (K < 64 * NN * R) wide_sort<NN, NW, R, 2 * K>(key, sX, t, lane);
 }
@@ -447,20 +532,20 @@ __device__ __forceinline__ void chain_add(double& acc, const double* src, int ce
 //   region A  P doubles (+ read-ahead pad): input-order probs, then sorted probs in place
 //   region B  sort exchange rows, then leaders [P] (+ exact: chain buffers [2][3][NT])
 //   small     per-wave last keys / counts, totals, error index, exact hand-off counters
-template <int NW, int R, bool FAST, int NN>
+template <int NW, int R, bool FAST, int NN, class KT = unsigned>
 struct WideLds {
-  using Cfg = WideCfg<NW, R, FAST, NN>;
+  using Cfg = WideCfg<NW, R, FAST, NN, KT>;
   static constexpr int A_BYTES = Cfg::A_DBL * 8;
   static constexpr int B_BYTES = ((Cfg::B_U32 * 4 + 15) / 16) * 16;
   static constexpr int TOT_OFF = A_BYTES + B_BYTES;          // sTot [3*NW] doubles
-  static constexpr int LAST_OFF = TOT_OFF + 24 * NW;          // sLast [NW]
-  static constexpr int CNT_OFF = LAST_OFF + 4 * NW;           // sCnt [NW]
+  static constexpr int LAST_OFF = TOT_OFF + 24 * NW;          // sLast [NW] keys
+  static constexpr int CNT_OFF = LAST_OFF + (int)sizeof(KT) * NW;  // sCnt [NW]
   static constexpr int MISC_OFF = CNT_OFF + 4 * NW;           // sErr, sRdy[2], sDone
   static constexpr int BYTES = ((MISC_OFF + 16 + 15) / 16) * 16;
   double* sA;
   unsigned* sB;
   double* sTot;
-  unsigned* sLast;
+  KT* sLast;
   int* sCnt;
   int* sErr;
   int* sRdy;
@@ -469,7 +554,7 @@ struct WideLds {
       : sA(reinterpret_cast<double*>(base)),
         sB(reinterpret_cast<unsigned*>(base + A_BYTES)),
         sTot(reinterpret_cast<double*>(base + TOT_OFF)),
-        sLast(reinterpret_cast<unsigned*>(base + LAST_OFF)),
+        sLast(reinterpret_cast<KT*>(base + LAST_OFF)),
         sCnt(reinterpret_cast<int*>(base + CNT_OFF)),
         sErr(reinterpret_cast<int*>(base + MISC_OFF)),
         sRdy(reinterpret_cast<int*>(base + MISC_OFF + 4)),
@@ -495,19 +580,19 @@ __device__ __forceinline__ void wide_load(const ConsArgs& a, int64_t off, int n,
 // One market (m, off, n) on a workgroup of NW waves; t = thread.  ps / pp hold
 // its sids and probabilities (loaded by the caller); issue_next() is called once the keys are
 // built, to start the workgroup's next market's loads into ps / pp.
-template <int NW, int R, bool FAST, int NN, class NextFn>
-__device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW, R, FAST, NN>& L, const int t,
+template <int NW, int R, bool FAST, int NN, class KT, class NextFn>
+__device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW, R, FAST, NN, KT>& L, const int t,
                                             const int32_t m, const int64_t off, int n, unsigned (&ps)[R],
                                             double (&pp)[R], NextFn&& issue_next) {
-  using Cfg = WideCfg<NW, R, FAST, NN>;
-  constexpr int NT = Cfg::NT, P = Cfg::P, IB = Cfg::IB, HR = Cfg::HR;
-  constexpr unsigned QMASK = (unsigned)Cfg::PN - 1u;  // the input-index bits of a key
+  using Cfg = WideCfg<NW, R, FAST, NN, KT>;
+  constexpr int NT = Cfg::NT, P = Cfg::P, IB = Cfg::IB, HR = Cfg::HR, LW = Cfg::LW;
+  constexpr KT QMASK = (KT)Cfg::PN - 1u;  // the input-index bits of a key
   constexpr int kNoErr = 0x7fffffff;
   double* const sA = L.sA;
   unsigned* const sB = L.sB;
   unsigned* const sX = sB;                                            // sort exchange rows
-  unsigned* const sLead = sB;                                         // [u] sid<<IB | q0
-  double* const sWAC = reinterpret_cast<double*>(sB + P);             // exact: [2][3][NT]
+  KT* const sLead = reinterpret_cast<KT*>(sB);                        // [u] sid<<IB | q0
+  double* const sWAC = reinterpret_cast<double*>(sB + LW * P);        // exact: [2][3][NT]
   // FAST: the region past the leaders (the dead exchange rows) parks w[j] for normalizedWeight
   // when the market's uniques fit -- C3's Zipf markets have u <= 0.55 n, which fits in ~all
   // of them -- instead of reading the weight output back (each load there waits for this
@@ -515,8 +600,9 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
   // (race-free: the next market's first wave-crossing stage writes exchange buffer 0 =
   // sB[0, P); buffer 1 = sB[P, 2P) is written only after that stage's barrier, which every
   // thread reaches after its own tail)
-  constexpr int WFREE = FAST ? (Cfg::B_U32 - P) / 2 : 0;
-  double* const sW = reinterpret_cast<double*>(sB + P);
+  // (64-bit keys: the leaders fill region B, nothing is parked)
+  constexpr int WFREE = FAST ? (Cfg::B_U32 - LW * P) / 2 : 0;
+  double* const sW = reinterpret_cast<double*>(sB + LW * P);
 
   const int lane = lane_id();
   const int wv = __builtin_amdgcn_readfirstlane(t >> 6);  // wave within the workgroup (uniform)
@@ -527,14 +613,14 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
   const bool wback = (NW > 1) && a.weight != nullptr;
 
   // ---- 1. keys; next market's metadata + sids --------------------------------------
-  unsigned key[R];
+  KT key[R];
   bool badsid = false;
 #pragma unroll
   for (int c = 0; c < R; ++c) {
     const int i = c * NT + t;
     const unsigned s = ps[c];
     badsid |= (i < n) && (s > smax);
-    key[c] = (i < n) ? ((s < smax ? s : smax) << IB) | (unsigned)i : 0xFFFFFFFFu;
+    key[c] = (i < n) ? ((KT)(s < smax ? s : smax) << IB) | (KT)i : ~(KT)0;
   }
   if (ballot(badsid)) raise_fault(a.fault, kFaultSid);
   int myerr = kNoErr;
@@ -569,13 +655,18 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
     const int q = t * R + r;
     x[r] = (q < n) ? sA[key[r] & QMASK] : 0.0;
   }
-  const unsigned prev_in_wave = (unsigned)__builtin_amdgcn_update_dpp(0, (int)key[R - 1], 0x138, 0xF, 0xF, false);  // wave_shr:1
-  const unsigned prev_key = (lane > 0) ? prev_in_wave : (wv > 0 ? L.sLast[wv - 1] : 0u);
+  KT prev_in_wave;  // wave_shr:1
+  if constexpr (LW == 2)
+    prev_in_wave = k_make((unsigned)__builtin_amdgcn_update_dpp(0, (int)k_hi(key[R - 1]), 0x138, 0xF, 0xF, false),
+                          (unsigned)__builtin_amdgcn_update_dpp(0, (int)k_lo(key[R - 1]), 0x138, 0xF, 0xF, false));
+  else
+    prev_in_wave = (unsigned)__builtin_amdgcn_update_dpp(0, (int)key[R - 1], 0x138, 0xF, 0xF, false);
+  const KT prev_key = (lane > 0) ? prev_in_wave : (wv > 0 ? L.sLast[wv - 1] : (KT)0);
   unsigned lead = 0;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int q = t * R + r;
-    const unsigned ps0 = ((r == 0) ? prev_key : key[r - 1]) >> IB;
+    const KT ps0 = ((r == 0) ? prev_key : key[r - 1]) >> IB;
     const bool is = (q < n) && (q == 0 || (key[r] >> IB) != ps0);
     lead |= is ? (1u << r) : 0u;
   }
@@ -596,7 +687,7 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
   for (int r = 0; r < R; ++r) {
     if (lead & (1u << r)) {
       const int jj = base + __popc(lead & ((1u << r) - 1u));
-      sLead[jj] = (key[r] & ~QMASK) | (unsigned)(t * R + r);
+      sLead[jj] = (key[r] & ~QMASK) | (KT)(t * R + r);
     }
   }
   if (t == 0) {
@@ -647,9 +738,9 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
           sids[i] = pwd[i] = 0;
           rc[i] = make_double2(0.5, 0.25);  // DEFAULT_RELIABILITY / _CONFIDENCE (empty table)
           if (jj < u) {
-            const unsigned lv = sLead[jj];
+            const KT lv = sLead[jj];
             q0s[i] = (int)(lv & QMASK);
-            sids[i] = min(lv >> IB, smax);
+            sids[i] = (unsigned)min(lv >> IB, (KT)smax);
             q1s[i] = (jj + 1 < u) ? (int)(sLead[jj + 1] & QMASK) : n;
             if (a.n_sources > 0) {
               rc[i] = a.relconf[sids[i]];
@@ -720,9 +811,9 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
       sids[i] = pwd[i] = 0;
       rc[i] = make_double2(0.5, 0.25);  // DEFAULT_RELIABILITY / _CONFIDENCE (empty table)
       if (jj < u) {
-        const unsigned lv = sLead[jj];
+        const KT lv = sLead[jj];
         q0s[i] = (int)(lv & QMASK);
-        sids[i] = min(lv >> IB, smax);  // <= smax by construction of the key; clamped anyway
+        sids[i] = (unsigned)min(lv >> IB, (KT)smax);  // <= smax by construction of the key; clamped anyway
         q1s[i] = (jj + 1 < u) ? (int)(sLead[jj + 1] & QMASK) : n;
         if (a.n_sources > 0) {
           rc[i] = a.relconf[sids[i]];
@@ -881,9 +972,9 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
 
 // One bin per launch: a persistent grid of NW-wave workgroups strides over the bin's market
 // list (one market per workgroup at a time, the next one's loads issued during this one).
-template <int NW, int R, bool FAST, int NN = NW>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg<NW, R, FAST, NN>::WPE, 8))) void consensus_wide_kernel(ConsArgs a) {
-  using LD = WideLds<NW, R, FAST, NN>;
+template <int NW, int R, bool FAST, int NN = NW, class KT = unsigned>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg<NW, R, FAST, NN, KT>::WPE, 8))) void consensus_wide_kernel(ConsArgs a) {
+  using LD = WideLds<NW, R, FAST, NN, KT>;
   __shared__ __attribute__((aligned(16))) unsigned char smem[LD::BYTES];
   const LD L(smem);
   const int t = threadIdx.x;
@@ -924,7 +1015,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
     const int32_t m = nm;
     const int64_t off = noff;
     const int n = nn;
-    wide_market<NW, R, FAST, NN>(a, L, t, m, off, n, ps, pp, [&]() {
+    wide_market<NW, R, FAST, NN, KT>(a, L, t, m, off, n, ps, pp, [&]() {
       if (li + G < a.n_list) {
         meta(li + G);
         wide_load<NW, R>(a, noff, nn, t, ps, pp);
@@ -933,15 +1024,23 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
   }
 }
 
+template <int NW, int R, bool FAST, int NN, class KT>
+int launch_wide_kt(const ConsArgs& a, hipStream_t st) {
+  const void* fn = reinterpret_cast<const void*>(&consensus_wide_kernel<NW, R, FAST, NN, KT>);
+  const int per_cu = blocks_per_cu(fn, 64 * NW, 0, 1, "consensus_wide_kernel");
+  const int64_t cap = grid_cap(a, per_cu);
+  const int grid = (int)(a.n_list < cap ? a.n_list : cap);
+  hipLaunchKernelGGL((consensus_wide_kernel<NW, R, FAST, NN, KT>), dim3(grid), dim3(64 * NW), 0, st, a);
+  return check_launch("consensus_wide_kernel");
+}
+
+// 32-bit keys while the sid fits beside the IB index bits, 64-bit keys for larger tables
 template <int NW, int R, bool FAST, int NN = NW>
 int launch_wide(const ConsArgs& a, hipStream_t st) {
   if (a.n_list == 0) return BCE_OK;
-  const void* fn = reinterpret_cast<const void*>(&consensus_wide_kernel<NW, R, FAST, NN>);
-  const int per_cu = blocks_per_cu(fn, 64 * NW, 0, 1, "consensus_wide_kernel");
-  const int64_t cap = (int64_t)cu_count() * per_cu;
-  const int grid = (int)(a.n_list < cap ? a.n_list : cap);
-  hipLaunchKernelGGL((consensus_wide_kernel<NW, R, FAST, NN>), dim3(grid), dim3(64 * NW), 0, st, a);
-  return check_launch("consensus_wide_kernel");
+  constexpr int IB = WideCfg<NW, R, FAST, NN>::IB;
+  if ((int64_t)a.n_sources <= (1ll << (32 - IB))) return launch_wide_kt<NW, R, FAST, NN, unsigned>(a, st);
+  return launch_wide_kt<NW, R, FAST, NN, uint64_t>(a, st);
 }
 
 // (NW, R[, NN]) per length bin: P = 64*NW*R >= max_len; the 1536 and 3072 bins run the
@@ -989,10 +1088,6 @@ extern "C" int bce_debug_lane_selftest(unsigned* out, void* stream) {
   return check_launch("lane_xor_selftest_kernel");
 }
 
-int wide_key_bits(int64_t max_len) {
-  return max_len <= 128 ? 7 : max_len <= 256 ? 8 : max_len <= 512 ? 9 : max_len <= 1024 ? 10 : max_len <= 2048 ? 11
-                                                                                                                 : 12;
-}
 
 int launch_wide_len(int64_t max_len, const ConsArgs& a, hipStream_t st) {
   return (a.mode == BCE_MODE_FAST) ? launch_wide_mode<true>(max_len, a, st) : launch_wide_mode<false>(max_len, a, st);

@@ -408,7 +408,33 @@ def bench_c2(args, world, rank):
         if not args.no_parity:
             ok = parity_all_outputs(res, cpu_out, offsets, uniq)
             out["parity_vs_oracle"] = {"all_equal": all(ok.values()), "outputs": ok}
+    if world > 1 and not args.no_parity:
+        # every rank checks its own shard (a bounded prefix of its batch) against the
+        # restatement, after the timed region
+        out["parity_ranks"] = gather_ranks(rank_parity(res, offsets, sid, prob, rel, conf, present, uniq,
+                                                       rank), world)
     return out
+
+
+def rank_parity(res, offsets, sid, prob, rel, conf, present, unique, rank, m_sample=20000):
+    """This rank's outputs for its first m_sample markets vs the C restatement run on them
+    (all eight outputs bit for bit; N > 1 lines, where the full-size check runs on no rank)."""
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as orc
+
+    m = min(m_sample, len(offsets) - 1)
+    sub = offsets[:m + 1]
+    n = int(sub[-1])
+    cpu = orc.consensus_csr(sub - sub[0], sid[:n], prob[:n], rel, conf, present)
+    keys = ("consensus", "confidence", "total_weight", "n_unique", "err_idx")
+    got = {k: getattr(res, k)[:m].cpu().numpy() for k in keys}
+    ok = {k: bool(np.array_equal(got[k], cpu[k], equal_nan=True)) for k in keys}
+    if unique:
+        u = cpu["n_unique"].astype(np.int64)
+        pos = np.repeat(sub[:-1], u) + (np.arange(int(u.sum())) - np.repeat(np.cumsum(u) - u, u))
+        for k in ("usid", "weight", "nweight"):
+            ok[k] = bool(np.array_equal(getattr(res, k)[:n].cpu().numpy()[pos], cpu[k][pos], equal_nan=True))
+    return {"rank": rank, "markets": m, "signals": n, "all_equal": all(ok.values())}
 
 
 # (config, steps, warmup, clock ramp s): the clock ramp as in each config's own line

@@ -310,6 +310,16 @@ def _c3(args, world, rank, barrier, max_over, sum_over):
                               "tolerance": "bit-exact" if md == "exact" else "1e-9 abs (float outputs)",
                               "max_abs_dev": dv}
             del res2
+    parity_ranks = None
+    if world > 1 and not args.no_parity:
+        # every rank checks its whole shard (the timed mode's last step) against the
+        # restatement on its share of the host cores, after the timed region
+        from bench import cpu_consensus_threaded, gather_ranks
+
+        cpu = cpu_consensus_threaded(off, sid, prob, *table_host, max(1, _threads() // world))
+        ok, dv = _parity_c3(res, cpu, off, exact=(mode == "exact"))
+        parity_ranks = gather_ranks({"rank": rank, "markets": len(off) - 1, "signals": n, "mode": mode,
+                                     "all_ok": all(ok.values()), "max_abs_dev": dv}, world)
     return {
         "metric": "signals aggregated/sec (node), 100M-signal ragged CSR (config 3)",
         "value": sig / wall, "unit": "signals/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -328,6 +338,7 @@ def _c3(args, world, rank, barrier, max_over, sum_over):
                                         "frac": bytes_step / per2 / 1e9 / HBM_PEAK_GBS} if per2 else None)},
         "cpu_baseline": cpu_line,
         "parity_vs_oracle": parity,
+        "parity_ranks": parity_ranks,
     }
 
 

@@ -43,3 +43,24 @@ def test_world_size_mismatch_fails():
              env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert p.returncode != 0
     assert "WORLD_SIZE=1" in (p.stderr + p.stdout)
+
+
+def test_rank_parity_checker_on_host_outputs():
+    """bench.rank_parity (each rank's own-shard check on N > 1 lines) against the restatement's
+    own outputs: equal -> all_equal; one flipped weight bit -> not (CPU, no GPU)."""
+    import types
+
+    import numpy as np
+    import torch
+
+    sys.path.insert(0, ROOT)
+    import bench
+    from oracle import oracle as orc
+
+    offsets, sid, prob, rel, conf, present = bench.make_c2(300, 32, 500, seed=4)
+    cpu = orc.consensus_csr(offsets, sid, prob, rel, conf, present)
+    res = types.SimpleNamespace(**{k: torch.from_numpy(np.array(v)) for k, v in cpu.items()})
+    ok = bench.rank_parity(res, offsets, sid, prob, rel, conf, present, True, 1, m_sample=200)
+    assert ok["all_equal"] and ok["markets"] == 200 and ok["signals"] == 6400
+    res.weight[3] = float(np.nextafter(res.weight[3].item(), 2.0))
+    assert not bench.rank_parity(res, offsets, sid, prob, rel, conf, present, True, 1, m_sample=200)["all_equal"]

@@ -1,0 +1,126 @@
+"""Sharded consensus (markets shard over ranks with no communication),
+run on one GPU exactly as each rank of an N-rank job runs its shard, against the unsharded run
+and the oracle.
+
+Each rank r of ``sharding.shard_markets(offsets, N, r)`` gets the market range [m0, m1):
+  * rebased: its own CSR copy (offsets[m0:m1+1] - offsets[m0], the sid / prob slices), its own
+    plan (bench.py / bench_extra.make_c3 build a rank's batch this way);
+  * offset view: offsets[m0:m1+1] unrebased over the full sid / prob arrays (batch.consensus
+    accepts offsets[0] != 0; per-unique outputs land at the absolute CSR positions).
+Concatenated in rank order, every output must equal the single unsharded call bit for bit (a
+market's result depends only on its own signals and the kernel its length selects, in both
+modes) and the oracle (bit-exact in EXACT, 1e-9 in FAST).  This is what the driver's 8-GPU
+SCALE run relies on.
+"""
+import numpy as np
+import pytest
+import torch
+
+from golden_util import load_npz
+from oracle import oracle as orc
+from test_gpu_consensus import _compare_vec, _dev
+
+pytestmark = pytest.mark.gpu
+
+KEYS_M = ("consensus", "confidence", "total_weight", "n_unique", "err_idx")
+KEYS_U = ("usid", "weight", "nweight")
+
+
+def _c3_like(total, S, seed):
+    """make_c3's law at a smaller size: log-uniform lengths on [1, 4096], Zipf(1.1)."""
+    rng = np.random.default_rng(seed)
+    lens = np.floor(np.exp(rng.uniform(0, np.log(4097), size=total // 300 + 10))).astype(np.int64)
+    cs = np.cumsum(lens)
+    M = int(np.searchsorted(cs, total) + 1)
+    lens = lens[:M]
+    lens[-1] -= int(cs[M - 1] - total)
+    off = np.zeros(M + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    z = rng.zipf(1.1, size=total)
+    bad = np.nonzero(z > S)[0]
+    while bad.size:
+        z[bad] = rng.zipf(1.1, size=bad.size)
+        bad = bad[z[bad] > S]
+    sid = rng.permutation(S).astype(np.int32)[z - 1]
+    prob = rng.random(total)
+    prob[rng.random(total) < 1e-4] = 1.5
+    rel, conf = rng.uniform(0.1, 1.0, S), rng.random(S)
+    present = (rng.random(S) < 0.9).astype(np.uint8)
+    return dict(offsets=off, sid=sid, prob=prob, rel=rel, conf=conf, present=present)
+
+
+def _c2_like(M, L, S, seed):
+    rng = np.random.default_rng(seed)
+    off = np.arange(0, M * L + 1, L, dtype=np.int64)
+    sid = rng.integers(0, S, M * L, dtype=np.int32)
+    prob = rng.random(M * L)
+    rel, conf = rng.uniform(0.1, 1.0, S), rng.random(S)
+    present = (rng.random(S) < 0.9).astype(np.uint8)
+    return dict(offsets=off, sid=sid, prob=prob, rel=rel, conf=conf, present=present)
+
+
+def _case(name):
+    if name == "c3_slice":
+        d = load_npz("c3_slice.npz")
+        return {k: d[k] for k in ("offsets", "sid", "prob", "rel", "conf", "present")}
+    if name == "c3_like":
+        return _c3_like(3_000_000, 1_000_000, 5)
+    return _c2_like(1_000_000, 32, 10_000, 6)
+
+
+def _call(off_h, sid_d, prob_d, table, N_sig, mode, uniform, dev):
+    from bayesian_engine import batch
+    off_d = torch.from_numpy(np.ascontiguousarray(off_h)).to(dev)
+    res = batch._alloc(len(off_h) - 1, N_sig, dev, True, True)
+    if uniform:
+        batch.consensus(off_d, sid_d, prob_d, table, max_len=32, mode=mode, out=res)
+    else:
+        batch.consensus(off_d, sid_d, prob_d, table, plan=batch.Plan.build(off_h, dev), mode=mode, out=res)
+    torch.cuda.synchronize()
+    return {k: getattr(res, k).cpu().numpy() for k in KEYS_M + KEYS_U}
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("mode", ["exact", "fast"])
+@pytest.mark.parametrize("name", ["c3_slice", "c3_like", "c2_1M"])
+def test_sharded_consensus_matches_unsharded_and_oracle(name, mode):
+    from bayesian_engine import _native as N
+    from bayesian_engine import batch
+    from bayesian_engine.sharding import shard_markets
+    g = _case(name)
+    off = g["offsets"]
+    M, n = len(off) - 1, int(off[-1])
+    uniform = name == "c2_1M"
+    dev = torch.device("cuda", 0)
+    table = batch.SourceTable.from_arrays(_dev(g["rel"]), _dev(g["conf"]), _dev(g["present"]))
+    sid_d, prob_d = _dev(g["sid"], np.int32), _dev(g["prob"])
+    full = _call(off, sid_d, prob_d, table, n, mode, uniform, dev)
+    exp = orc.consensus_csr(off, g["sid"], g["prob"], g["rel"], g["conf"], g["present"])
+    _compare_vec(full, exp, off, exact=(mode == "exact"))
+    u = exp["n_unique"].astype(np.int64)
+    pos = np.repeat(off[:-1], u) + (np.arange(int(u.sum())) - np.repeat(np.cumsum(u) - u, u))
+    for world in (2, 8):
+        cat = {k: np.zeros_like(full[k]) for k in KEYS_M + KEYS_U}
+        view = {k: np.zeros_like(full[k]) for k in KEYS_M + KEYS_U}
+        for r in range(world):
+            m0, m1 = shard_markets(off, world, r)
+            a, b = int(off[m0]), int(off[m1])
+            # rebased: the rank's own batch
+            loc = off[m0:m1 + 1] - a
+            o = _call(loc, _dev(g["sid"][a:b], np.int32), _dev(g["prob"][a:b]), table, b - a, mode, uniform, dev)
+            for k in KEYS_M:
+                cat[k][m0:m1] = o[k][:m1 - m0]
+            for k in KEYS_U:
+                cat[k][a:b] = o[k][:b - a]
+            # offset view over the full arrays (absolute CSR positions)
+            o = _call(off[m0:m1 + 1], sid_d, prob_d, table, n, mode, uniform, dev)
+            for k in KEYS_M:
+                view[k][m0:m1] = o[k][:m1 - m0]
+            for k in KEYS_U:
+                view[k][a:b] = o[k][a:b]
+        N.check_faults(dev, f"{name} {world} shards")
+        for got, how in ((cat, "rebased"), (view, "offset view")):
+            for k in KEYS_M:
+                assert got[k].tobytes() == full[k].tobytes(), (world, how, k)
+            for k in KEYS_U:
+                assert got[k][pos].tobytes() == full[k][pos].tobytes(), (world, how, k)

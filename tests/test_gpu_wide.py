@@ -3,7 +3,7 @@
 consensus_wide_kernel<NW, R> packs (sid, input index) into 32 bits, so these cases sit on
 its edges: every length bin boundary, Zipf-heavy duplicate runs (C3's source law), one
 source for a whole 4096-signal market, the largest table the packed key allows
-(S = 2^20 at P = 4096) and one past it (falls back to the LDS-sort kernel), NaN /
+(S = 2^20 at P = 4096) and past it (64-bit keys: up to 16M sources in every bin), NaN /
 out-of-range probabilities and non-positive reliabilities.  Bit-exact (==) in
 BCE_MODE_EXACT; BCE_MODE_FAST (fixed-order tree totals) within 1e-9 absolute on consensus,
 confidence, total weight and normalizedWeight, bit-exact on everything else.
@@ -110,7 +110,7 @@ def test_wide_non_power_of_two_bins_direct(top, mode):
 
 def test_wide_key_limit_and_fallback():
     """S = 2^20 is the largest table the 32-bit key takes at P = 4096 (top sid at the last
-    index); S = 2^20 + 1 sends the 2049..4096 bin to the LDS-sort kernel."""
+    index); S = 2^20 + 1 sends the 2049..4096 bin to the 64-bit-key instantiation."""
     for S in (1 << 20, (1 << 20) + 1):
         lens = np.array([4096, 4096, 3000, 2500, 2048, 1000, 200])
         g = _zipf_case(lens, S, 9, a=1.05)
@@ -223,3 +223,45 @@ def test_wide_planned_every_bin_vs_oracle(mode):
     again = _run(g, mode=mode)
     for k in ("consensus", "confidence", "total_weight", "n_unique", "usid", "weight", "nweight"):
         assert np.array_equal(again[k], out[k], equal_nan=True), k
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("S", [(1 << 21) + 3, 10_000_000, (1 << 24) - 1])
+def test_wide_64bit_keys_large_tables(S, mode):
+    """Tables past the packed 32-bit key (S > 2^(32 - IB)): every wide bin runs its 64-bit-key
+    instantiation (the one-buffer wave-crossing stages, 64-bit permlane swap pairs and lane
+    stages).  Zipf markets at every bin edge, the largest sids at the top of each market, sids
+    that agree in their low 20 bits (a 32-bit key would merge them), against the oracle."""
+    rng = np.random.default_rng(S % 1000)
+    lens = np.concatenate([np.exp(rng.uniform(np.log(65), np.log(4096), 150)).astype(np.int64), EDGES, [0, 1, 64]])
+    rng.shuffle(lens)
+    g = _zipf_case(lens, S, S % 977, base=3)
+    off = g["offsets"] - g["offsets"][0]
+    for m in range(0, len(lens), 3):
+        a, b = int(off[m]), int(off[m + 1])
+        if b - a >= 4:
+            g["sid"][a] = S - 1
+            g["sid"][a + 1] = (S - 1) & 0xFFFFF        # same low 20 bits as S - 1
+            g["sid"][a + 2] = ((S - 1) & 0xFFFFF) | (1 << 20)
+            g["sid"][b - 1] = S - 1
+    _check(g, mode)
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_wide_64bit_keys_ordered_and_single_source(mode):
+    """64-bit keys (S = 2^22) on ordered, reversed and single-source markets at every bin edge:
+    every compare of a stage goes the same way, and runs thousands of terms long."""
+    S = 1 << 22
+    lens = np.array(EDGES * 2 + [4096, 3000], np.int64)
+    off = np.zeros(len(lens) + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    n = int(off[-1])
+    sid = np.zeros(n, np.int32)
+    for m, L in enumerate(lens):
+        i = np.arange(L)
+        v = [S - 1 - 3 * i, 5 + 4099 * i, np.full(L, S - 2)][m % 3]
+        sid[off[m]:off[m + 1]] = np.clip(v, 0, S - 1)
+    rng = np.random.default_rng(8)
+    g = dict(offsets=off, sid=sid, prob=rng.random(n), rel=rng.uniform(0.1, 1.0, S), conf=rng.random(S),
+             present=(rng.random(S) < 0.8).astype(np.uint8))
+    _check(g, mode)

@@ -22,7 +22,7 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "bayesian-consensus-engine_amd", "csrc")
-OUT = os.path.join(ROOT, "tools", "ablate_build")
+OUT = os.path.join(ROOT, "tools", "bin", "variants")  # gitignored; travels to the GPU box
 SRCS = ["capi.hip", "consensus.hip", "consensus_tab.hip", "consensus_wide.hip", "elementwise.hip", "tiebreak.hip",
         "stats.hip", "aggregate.hip"]
 CPP_SRCS = ["jsonl.cpp"]
