@@ -1474,7 +1474,7 @@ int launch_seg(const ConsArgs& a, hipStream_t st) {
   if (tiles == 0) return BCE_OK;
   // persistent grid: every workgroup resident at once, tiles dealt round-robin
   const int per_cu = blocks_per_cu(reinterpret_cast<const void*>(&consensus_seg_kernel<G, TM>), 64, 0, 8);
-  const int64_t cap = grid_cap(a, per_cu);
+  const int64_t cap = (int64_t)cu_count() * per_cu;
   const int grid = (int)(tiles < cap ? tiles : cap);
   hipLaunchKernelGGL((consensus_seg_kernel<G, TM>), dim3(grid), dim3(64), 0, st, a);
   return check_launch("consensus_seg_kernel");
@@ -1485,7 +1485,7 @@ int launch_lpm(const ConsArgs& a, hipStream_t st) {
   const int64_t tiles = (a.n_list + kWave - 1) / kWave;
   if (tiles == 0) return BCE_OK;
   const int per_cu = blocks_per_cu(reinterpret_cast<const void*>(&consensus_lpm_kernel<G>), 64, 0, 4);
-  const int64_t cap = grid_cap(a, per_cu);
+  const int64_t cap = (int64_t)cu_count() * per_cu;
   const int grid = (int)(tiles < cap ? tiles : cap);
   hipLaunchKernelGGL((consensus_lpm_kernel<G>), dim3(grid), dim3(64), 0, st, a);
   return check_launch("consensus_lpm_kernel");
@@ -1546,7 +1546,7 @@ int launch_seg_for_len(int max_len, const ConsArgs& a, hipStream_t st) {
 
 int launch_long_lds(const ConsArgs& a, hipStream_t st) {
   if (a.n_list == 0) return BCE_OK;
-  const int64_t cap = grid_cap(a, 2);
+  const int64_t cap = (int64_t)cu_count() * 2;
   const int grid = (int)(a.n_list < cap ? a.n_list : cap);
   hipLaunchKernelGGL((consensus_long_kernel<true>), dim3(grid), dim3(kLongThreads), 0, st, a);
   return check_launch("consensus_long_kernel<lds>");
@@ -1669,9 +1669,8 @@ static_assert(BCE_NBINS == 13, "bin table");
 static constexpr int64_t kBinMax[BCE_NBINS - 1] = {8, 16, 32, 64, 128, 256, 512, 1024, 1536, 2048, 3072, kLongMaxLds};
 constexpr int kBinNp2Lo = 8, kBinNp2Hi = 10;  // the 1536 and 3072 bins
 static_assert(kBinMax[kBinNp2Lo] == 1536 && kBinMax[kBinNp2Hi] == 3072, "non-power-of-two bins");
-constexpr int kPlanSideLast = 3;  // bins 0..3 (n <= 64): the short-market kernels
-constexpr int kPlanStreams = 4;   // concurrent streams of a planned call (st + kSideStreams)
-static_assert(kPlanStreams - 1 <= kSideStreams, "side streams");
+constexpr int kPlanSideLast = 3;  // bins 0..3 (n <= 64) run on the side stream
+constexpr double kMergeRounds = 3.0;  // merge a small call's bins below this many resident rounds
 static int bin_of(int64_t n) {
   for (int b = 0; b < BCE_NBINS - 1; ++b)
     if (n <= kBinMax[b]) return b;
@@ -1749,67 +1748,57 @@ extern "C" int bce_consensus_planned(const int64_t* offsets, int64_t n_markets, 
   base.fault = fault_word();
   base.spin_cap = spin_cap();
   const bool seg_ok = n_sources <= (1 << 25);
-  // EXACT: the non-power-of-two bins (1025..1536, 2049..3072) ride in the launch of the
-  // power-of-two bin above them (their markets sit right below it in `order`).  The exact
-  // kernel's LDS chain buffers allow two workgroups per CU at 3/6 waves as at 4/8, so the
-  // smaller workgroup only loses latency hiding, and a separate launch adds a tail.
-  const bool merge_np2 = mode == BCE_MODE_EXACT;
-  // Launch units (one kernel each): bin b's markets, plus the bin below it when merged.
-  struct Unit {
-    int b, b0;
-    double cost;
-    int stream;
-  };
-  Unit units[BCE_NBINS];
-  int nu = 0;
-  double total_cost = 0.0;
-  for (int b = BCE_NBINS - 1; b >= 0; --b) {
-    if (merge_np2 && (b == kBinNp2Lo || b == kBinNp2Hi)) continue;
-    const int b0 = (merge_np2 && (b == kBinNp2Lo + 1 || b == kBinNp2Hi + 1)) ? b - 1 : b;
-    double cost = 0.0;
-    for (int k = b0; k <= b; ++k) {
-      // signals ~ markets x the bin's mid length; the wide kernels cost about the same per
-      // signal in every bin (profiles/r04g/c3_kernel_stats.csv), the short-market kernels more
-      const double lo = k ? (double)kBinMax[k - 1] : 0.0, hi = k < BCE_NBINS - 1 ? (double)kBinMax[k] : 2.0 * lo;
-      cost += (double)(bin_start_host[k + 1] - bin_start_host[k]) * 0.5 * (lo + hi) * (k <= kPlanSideLast ? 2.0 : 1.0);
-    }
-    if (bin_start_host[b + 1] == bin_start_host[b0]) continue;
-    units[nu++] = Unit{b, b0, cost, 0};
-    total_cost += cost;
-  }
-  // Streams: the units are dealt longest-processing-time first onto kPlanStreams streams (st and
-  // kPlanStreams - 1 side streams), each launch capped to its stream's share of the resident
-  // grid, so the streams run side by side for the whole step and end together -- one ramp and
-  // one tail per step instead of one per bin, which is what a 1/8 market shard of C3 loses
-  // (DESIGN.md §5).  Each stream runs its units longest bin first (LPT inside a launch too).
-  double load[kPlanStreams] = {};
-  {
-    int idx[BCE_NBINS];
-    for (int i = 0; i < nu; ++i) idx[i] = i;
-    std::stable_sort(idx, idx + nu, [&](int x, int y) { return units[x].cost > units[y].cost; });
-    for (int i = 0; i < nu; ++i) {
-      int best = 0;
-      for (int k = 1; k < kPlanStreams; ++k) best = load[k] < load[best] ? k : best;
-      units[idx[i]].stream = best;
-      load[best] += units[idx[i]].cost;
-    }
-  }
-  hipStream_t streams[kPlanStreams];
-  streams[0] = st;
+  // The short-market bins (n <= 64) are small latency-bound launches: they run on a side
+  // stream while the long bins run on st, longest first (joined before return).  Measured
+  // on C3: 1.73 -> 1.65 ms; moving wide bins to the side stream too, or forking every bin
+  // over 2-8 streams, was slower (profiles/r02_c3_plan_streams.jsonl); so was dealing every
+  // bin over 2 or 4 streams with the resident grid shared out by estimated work (round 5,
+  // profiles/r05b/: one 8th of C3 0.233 -> 0.294 / 0.307 ms).
+  hipStream_t side = st;
   std::unique_lock<std::mutex> fork_lock;
-  rc = side_fork(st, kPlanStreams - 1, streams + 1, &fork_lock);
+  constexpr int side_last = kPlanSideLast;
+  rc = side_fork(st, 1, &side, &fork_lock);
   if (rc) return rc;
-  for (int i = 0; i < nu && !rc; ++i) {  // units are in bin order, longest first
-    const int b = units[i].b, b0 = units[i].b0;
+  // Launches: bin b runs with the markets of bins lo[b]..b in one kernel sized for bin b (its
+  // own markets first, then the shorter bins' -- consensus_wide_kernel's list_hi).
+  //   EXACT: the non-power-of-two bins (1025..1536, 2049..3072) always ride in the launch of the
+  //   power-of-two bin above them: the exact kernel's LDS chain buffers allow two workgroups per
+  //   CU at 3/6 waves as at 4/8, so the smaller workgroup only loses latency hiding, and a
+  //   separate launch adds a tail.
+  //   Small calls (a market shard, kMergeRounds): a launch whose markets would fill fewer than
+  //   kMergeRounds rounds of its resident grid costs a ramp and a tail for little work, so FAST
+  //   merges the non-power-of-two bins the same way and the 65..512 bins run as one 1-wave
+  //   launch -- fewer, fuller launches for a 1/8 shard of C3.
+  int lo[BCE_NBINS];
+  for (int b = 0; b < BCE_NBINS; ++b) lo[b] = b;
+  auto cnt = [&](int b0, int b1) { return bin_start_host[b1 + 1] - bin_start_host[b0]; };
+  auto few = [&](int b0, int b1) {
+    return cnt(b0, b1) > 0 && (double)cnt(b0, b1) < kMergeRounds * (double)wide_resident(kBinMax[b1], mode, n_sources);
+  };
+  for (int b : {kBinNp2Lo + 1, kBinNp2Hi + 1})
+    if (mode == BCE_MODE_EXACT || few(b - 1, b)) lo[b] = b - 1;
+  if (few(kPlanSideLast + 1, kPlanSideLast + 3)) lo[kPlanSideLast + 3] = kPlanSideLast + 1;  // 65..512 as one
+  bool merged_away[BCE_NBINS] = {};
+  for (int b = 0; b < BCE_NBINS; ++b)
+    for (int k = lo[b]; k < b; ++k) merged_away[k] = true;
+  // Longest bins first, except that the 2049..3072 bin precedes the 3073..4096 one: its
+  // 6-wave workgroups leave 4 of a CU's 16 wave slots free (two per CU at 128 VGPRs), which
+  // the side stream's short-market kernels then fill (C3 fast -1.3%,
+  // profiles/r03x/order_ab.txt).
+  static const int kOrder[BCE_NBINS] = {12, 10, 11, 9, 8, 7, 6, 5, 4, 3, 2, 1, 0};
+  for (int oi = 0; oi < BCE_NBINS && !rc; ++oi) {
+    const int b = kOrder[oi];
+    if (merged_away[b]) continue;
+    const int b0 = lo[b];
     ConsArgs a = base;
     a.list = order + bin_start_host[b0];
     a.n_list = bin_start_host[b + 1] - bin_start_host[b0];
-    if (b0 != b) {  // merged: this bin's (longer) markets first, then the bin below
+    if (b0 != b) {  // merged: this bin's (longer) markets first, then the bins below
       a.list_hi = order + bin_start_host[b];
       a.n_hi = bin_start_host[b + 1] - bin_start_host[b];
     }
-    a.grid_share = total_cost > 0.0 ? (float)(load[units[i].stream] / total_cost) : 1.0f;
-    hipStream_t sb = streams[units[i].stream];
+    if (a.n_list == 0) continue;
+    hipStream_t sb = (b <= side_last) ? side : st;
     if (b <= 3 && seg_ok) {
       static const int lens[4] = {8, 16, 32, 64};
       rc = launch_seg_for_len(lens[b], a, sb);
@@ -1819,18 +1808,19 @@ extern "C" int bce_consensus_planned(const int64_t* offsets, int64_t n_markets, 
       // scratch stride from the caller's sizing (bce_consensus_scratch_bytes)
       const int grid = (int)(a.n_list < kHugeGrid ? a.n_list : kHugeGrid);
       const int64_t P = scratch_bytes / ((int64_t)grid * 4 * 8);
-      if (P <= kLongMaxLds) {  // not BCE_REQUIRE: the side streams must still be joined
+      if (P <= kLongMaxLds) {  // not BCE_REQUIRE: the side stream must still be joined
         set_error("planned: scratch too small for the >4096 bin");
         rc = BCE_EINVAL;
         break;
       }
       a.scratch = scratch;
       a.scratch_stride = P;
-      hipLaunchKernelGGL((consensus_long_kernel<false>), dim3(grid), dim3(kLongThreads), 0, sb, a);
+      hipLaunchKernelGGL((consensus_long_kernel<false>), dim3(grid), dim3(kLongThreads), 0, st, a);
       rc = check_launch("consensus_long_kernel<global>");
     }
+    if (rc) break;
   }
-  const int rj = side_join(st, kPlanStreams - 1);  // join even after a failed launch: st must not run ahead
+  const int rj = side_join(st, 1);  // join even after a failed launch: st must not run ahead
   if (!rc) rc = rj;
   return rc;
 }

@@ -37,17 +37,7 @@ struct ConsArgs {
   int* fault;         // device word: set to a kFault* code by a wave that gave up
   int spin_cap;       // bounded waits of the persistent pipe kernel (polls before giving up)
   int32_t tab_rows;   // tab kernel, hybrid table: rows [0, tab_rows) staged in LDS, the rest read from relconf
-  float grid_share;   // host only: this launch's share of the resident grid (<= 0: all of it)
 };
-
-// Resident-grid cap of a persistent launch: every CU's per_cu workgroups, or the launch's
-// share of them when it runs beside other launches (bce_consensus_planned's streams).
-inline int64_t grid_cap(const ConsArgs& a, int per_cu) {
-  const int64_t full = (int64_t)cu_count() * per_cu;
-  if (!(a.grid_share > 0.0f) || a.grid_share >= 1.0f) return full;
-  const int64_t g = (int64_t)((double)full * a.grid_share + 0.5);
-  return g < 1 ? 1 : g;
-}
 
 // Device fault codes (bce_fault_check reports them).
 constexpr int kFaultSpinLoader = 1;   // pipe kernel: loader never saw a slot released
@@ -180,6 +170,8 @@ int launch_tab32(const ConsArgs& a, hipStream_t st);
 // Register-sort kernel (consensus_wide.hip) for 64 < n <= 4096: keys (sid << ib) | index with
 // ib = log2 of the bin's padded size (7..12), 32 bits while n_sources <= 2^(32 - ib), else 64.
 int launch_wide_len(int64_t max_len, const ConsArgs& a, hipStream_t st);
+// Resident workgroups (every CU's share) of the wide kernel launch_wide_len would pick.
+int64_t wide_resident(int64_t max_len, int32_t mode, int32_t n_sources);
 // kSplitWords words (one per wave of the grid) for a tie-break FULL/rest launch pair
 // (tiebreak.hip; written with a per-launch ticket)
 constexpr int kSplitWords = 4096;

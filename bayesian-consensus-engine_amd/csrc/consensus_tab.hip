@@ -56,6 +56,8 @@ namespace bce {
 namespace {
 
 constexpr int kTabWaves = 8;  // waves per workgroup (two per SIMD); one workgroup per CU (LDS-bound)
+// The next tile's metadata read at the top of a tile (true) or after its walk (false)
+constexpr bool kTabMetaEarly = false;
 constexpr int kPL = 8;         // lanes per 128-B piece of a market row (16 B each)
 constexpr int kLB = 3;         // log2 kPL
 constexpr int kMG = 64 / kPL;  // markets per load instruction
@@ -258,12 +260,14 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
     // and 40 store address offsets would stay live across the whole tile
     int lane = lane_id();
     asm volatile("" : "+v"(lane));
-    const int64_t m0 = tile * 64, mk = m0 + tmkt(lane);
-    const bool has = mk < M;
+    const int64_t m0 = tile * 64;
     const int64_t off = cur.off, B = cur.B;
     const int n = cur.n;
     const bool reg = cur.reg;
-    const Meta nxt = meta(tile + stride, lane);
+    // the next tile's metadata: read here (kTabMetaEarly) or after the walk, so its registers
+    // are not live through the sort and the walk
+    Meta nxt{};
+    if constexpr (kTabMetaEarly) nxt = meta(tile + stride, lane);
 
     // ---- lane = market, s[t] = sid, pw = probabilities ------------------------------------
     if (reg) {
@@ -408,13 +412,21 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
 
     // ---- per-market results (lane = market, coalesced) -----------------------------------
     __builtin_amdgcn_s_setprio(2);
-    if (has) {
-      const bool null_ = (total == 0.0);  // core.py:131-133
-      a.consensus[mk] = null_ ? 0.0 : ws / total;
-      a.confidence[mk] = null_ ? 0.0 : cs / total;
-      a.total_weight[mk] = total;
-      a.n_unique[mk] = u;
-      if (a.err_idx) a.err_idx[mk] = err;
+    if constexpr (!kTabMetaEarly) nxt = meta(tile + stride, lane_id());
+    {
+      // the market index re-derived here: held from the top of the tile, it and the five
+      // output addresses built from it stay live through the sort and the walk (spills)
+      int ln = lane_id();
+      asm volatile("" : "+v"(ln));
+      const int64_t mk2 = m0 + tmkt(ln);
+      if (mk2 < M) {
+        const bool null_ = (total == 0.0);  // core.py:131-133
+        a.consensus[mk2] = null_ ? 0.0 : ws / total;
+        a.confidence[mk2] = null_ ? 0.0 : cs / total;
+        a.total_weight[mk2] = total;
+        a.n_unique[mk2] = u;
+        if (a.err_idx) a.err_idx[mk2] = err;
+      }
     }
     if (!do_any) {
       __builtin_amdgcn_s_setprio(0);
@@ -502,7 +514,12 @@ __global__ __launch_bounds__(64 * kTabWaves) void consensus_tab32_kernel(ConsArg
         }
       }
     } else {
-      // per-lane rows (irregular tiles): weight first, then normalizedWeight
+      // per-lane rows (irregular tiles): weight first, then normalizedWeight.  The row start
+      // is read again here (L2) rather than held through the tile.
+      int ln = lane_id();
+      asm volatile("" : "+v"(ln));
+      const int64_t mk2 = m0 + tmkt(ln);
+      const int64_t off = (mk2 < M) ? a.offsets[mk2] : 0;
 #pragma unroll
       for (int j = 0; j < 32; ++j) {
         if (j < u) {

@@ -1025,10 +1025,35 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg
 }
 
 template <int NW, int R, bool FAST, int NN, class KT>
+int64_t resident_kt() {
+  const void* fn = reinterpret_cast<const void*>(&consensus_wide_kernel<NW, R, FAST, NN, KT>);
+  return (int64_t)cu_count() * blocks_per_cu(fn, 64 * NW, 0, 1, "consensus_wide_kernel");
+}
+
+template <int NW, int R, bool FAST, int NN = NW>
+int64_t resident_wide(int32_t n_sources) {
+  constexpr int IB = WideCfg<NW, R, FAST, NN>::IB;
+  return ((int64_t)n_sources <= (1ll << (32 - IB))) ? resident_kt<NW, R, FAST, NN, unsigned>()
+                                                     : resident_kt<NW, R, FAST, NN, uint64_t>();
+}
+
+template <bool FAST>
+int64_t resident_mode(int64_t max_len, int32_t n_sources) {
+  if (max_len <= 128) return resident_wide<1, 2, FAST>(n_sources);
+  if (max_len <= 256) return resident_wide<1, 4, FAST>(n_sources);
+  if (max_len <= 512) return resident_wide<1, 8, FAST>(n_sources);
+  if (max_len <= 1024) return resident_wide<2, 8, FAST>(n_sources);
+  if (max_len <= 1536) return resident_wide<3, 8, FAST, 4>(n_sources);
+  if (max_len <= 2048) return resident_wide<4, 8, FAST>(n_sources);
+  if (max_len <= 3072) return resident_wide<6, 8, FAST, 8>(n_sources);
+  return resident_wide<8, 8, FAST>(n_sources);
+}
+
+template <int NW, int R, bool FAST, int NN, class KT>
 int launch_wide_kt(const ConsArgs& a, hipStream_t st) {
   const void* fn = reinterpret_cast<const void*>(&consensus_wide_kernel<NW, R, FAST, NN, KT>);
   const int per_cu = blocks_per_cu(fn, 64 * NW, 0, 1, "consensus_wide_kernel");
-  const int64_t cap = grid_cap(a, per_cu);
+  const int64_t cap = (int64_t)cu_count() * per_cu;
   const int grid = (int)(a.n_list < cap ? a.n_list : cap);
   hipLaunchKernelGGL((consensus_wide_kernel<NW, R, FAST, NN, KT>), dim3(grid), dim3(64 * NW), 0, st, a);
   return check_launch("consensus_wide_kernel");
@@ -1088,6 +1113,10 @@ extern "C" int bce_debug_lane_selftest(unsigned* out, void* stream) {
   return check_launch("lane_xor_selftest_kernel");
 }
 
+
+int64_t wide_resident(int64_t max_len, int32_t mode, int32_t n_sources) {
+  return (mode == BCE_MODE_FAST) ? resident_mode<true>(max_len, n_sources) : resident_mode<false>(max_len, n_sources);
+}
 
 int launch_wide_len(int64_t max_len, const ConsArgs& a, hipStream_t st) {
   return (a.mode == BCE_MODE_FAST) ? launch_wide_mode<true>(max_len, a, st) : launch_wide_mode<false>(max_len, a, st);

@@ -7,10 +7,12 @@ Each rank r of ``sharding.shard_markets(offsets, N, r)`` gets the market range [
     plan (bench.py / bench_extra.make_c3 build a rank's batch this way);
   * offset view: offsets[m0:m1+1] unrebased over the full sid / prob arrays (batch.consensus
     accepts offsets[0] != 0; per-unique outputs land at the absolute CSR positions).
-Concatenated in rank order, every output must equal the single unsharded call bit for bit (a
-market's result depends only on its own signals and the kernel its length selects, in both
-modes) and the oracle (bit-exact in EXACT, 1e-9 in FAST).  This is what the driver's 8-GPU
-SCALE run relies on.
+Concatenated in rank order, every output must equal the single unsharded call: bit for bit in
+EXACT (and the oracle's), and in FAST bit for bit on the integer outputs, usid and weight and
+within the north star's 1e-9 on consensus / confidence / total weight / normalizedWeight -- a
+small call (a shard) may run a length bin in the launch of the bin above it (fewer, fuller
+launches, bce_consensus_planned's kMergeRounds), whose wider workgroup sums the FAST partial
+totals in another fixed order.  This is what the driver's 8-GPU SCALE run relies on.
 """
 import numpy as np
 import pytest
@@ -119,8 +121,13 @@ def test_sharded_consensus_matches_unsharded_and_oracle(name, mode):
             for k in KEYS_U:
                 view[k][a:b] = o[k][a:b]
         N.check_faults(dev, f"{name} {world} shards")
+        floats = ("consensus", "confidence", "total_weight", "nweight")
         for got, how in ((cat, "rebased"), (view, "offset view")):
-            for k in KEYS_M:
-                assert got[k].tobytes() == full[k].tobytes(), (world, how, k)
-            for k in KEYS_U:
-                assert got[k][pos].tobytes() == full[k][pos].tobytes(), (world, how, k)
+            for k in KEYS_M + KEYS_U:
+                a_, b_ = (got[k][pos], full[k][pos]) if k in KEYS_U else (got[k], full[k])
+                if mode == "fast" and k in floats:
+                    np.testing.assert_allclose(a_, b_, rtol=0, atol=1e-9, equal_nan=True, err_msg=f"{world} {how} {k}")
+                else:
+                    assert a_.tobytes() == b_.tobytes(), (world, how, k)
+            # the shards against the oracle as well (FAST: the same 1e-9)
+            _compare_vec(got, exp, off, exact=(mode == "exact"))

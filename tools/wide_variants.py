@@ -34,10 +34,9 @@ OUT = tab_variants.OUT
 # DESIGN.md §4.2 / §4.9 and profiles/r04c, r04e, r04f, r04k, r04m, r04aa.
 VARIANTS = {
     "wbase": [],
-    # planned call on fewer concurrent streams (shipped: 4 = st + 3 side streams)
-    "ps1": [("consensus.hip", "constexpr int kPlanStreams = 4;", "constexpr int kPlanStreams = 1;")],
-    "ps2": [("consensus.hip", "constexpr int kPlanStreams = 4;", "constexpr int kPlanStreams = 2;")],
-    "ps3": [("consensus.hip", "constexpr int kPlanStreams = 4;", "constexpr int kPlanStreams = 3;")],
+    # small planned calls without the bin merges (shipped: merge below 3 resident rounds)
+    "nomerge": [("consensus.hip", "constexpr double kMergeRounds = 3.0;", "constexpr double kMergeRounds = 0.0;")],
+    "merge6": [("consensus.hip", "constexpr double kMergeRounds = 3.0;", "constexpr double kMergeRounds = 6.0;")],
     # tie-break FULL tiles: staging batches of the predictions / confidences (shipped: 8)
     "tbpc16": [("tiebreak.hip", "constexpr int kTbFullBatchPC = 8;", "constexpr int kTbFullBatchPC = 16;")],
     "tbpc4": [("tiebreak.hip", "constexpr int kTbFullBatchPC = 8;", "constexpr int kTbFullBatchPC = 4;")],
