@@ -1670,7 +1670,7 @@ static constexpr int64_t kBinMax[BCE_NBINS - 1] = {8, 16, 32, 64, 128, 256, 512,
 constexpr int kBinNp2Lo = 8, kBinNp2Hi = 10;  // the 1536 and 3072 bins
 static_assert(kBinMax[kBinNp2Lo] == 1536 && kBinMax[kBinNp2Hi] == 3072, "non-power-of-two bins");
 constexpr int kPlanSideLast = 3;  // bins 0..3 (n <= 64) run on the side stream
-constexpr double kMergeRounds = 3.0;  // merge a small call's bins below this many resident rounds
+constexpr double kMergeRounds = 6.0;  // merge a small call's bins below this many resident rounds
 static int bin_of(int64_t n) {
   for (int b = 0; b < BCE_NBINS - 1; ++b)
     if (n <= kBinMax[b]) return b;
