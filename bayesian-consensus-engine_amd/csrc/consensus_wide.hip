@@ -219,60 +219,6 @@ __device__ __forceinline__ void dpp_stage8(unsigned (&key)[8], uint64_t lower) {
   for (int r = 0; r < 8; ++r) key[r] = o[r];
 }
 
-// 64-bit keys: the same fused compare-exchange with the partner's key read through DPP -- a
-// v_sub_co_u32_dpp / v_subb_co_u32_dpp borrow chain leaves (partner < key) in VCC, s_xor with
-// the lower-lane mask, then one v_cndmask_b32_dpp per half: 4 VALU per key instead of the
-// generic path's two DPP moves, a 64-bit compare and two selects.  Every pattern that reads
-// the same partner for all lanes (quad_perm, row_ror:8, row_half_mirror, row_mirror); M = 4
-// (ror 12 or ror 4 by lane) stays generic.  Two keys per block: r and its partner key s.
-#define BCE_DPP_CAS64(OL, OH, KL, KH, PL, PH, C)                                          \
-  "v_sub_co_u32_dpp %[jl], vcc, %[" PL "], %[" KL "] " C " row_mask:0xf bank_mask:0xf\n"      \
-  "v_subb_co_u32_dpp %[jh], vcc, %[" PH "], %[" KH "], vcc " C " row_mask:0xf bank_mask:0xf\n" \
-  "s_xor_b64 vcc, vcc, %[lm]\n"                                                            \
-  "v_cndmask_b32_dpp %[" OL "], %[" PL "], %[" KL "], vcc " C " row_mask:0xf bank_mask:0xf\n"  \
-  "v_cndmask_b32_dpp %[" OH "], %[" PH "], %[" KH "], vcc " C " row_mask:0xf bank_mask:0xf\n"
-// FLIP: key r pairs with the partner's key s and key s with the partner's key r
-#define BCE_DPP_PAIR64(C, FLIP)                                                                    \
-  do {                                                                                             \
-    if (FLIP)                                                                                      \
-      asm("s_nop 1\n" BCE_DPP_CAS64("o0l", "o0h", "k0l", "k0h", "k1l", "k1h", C)                 \
-              BCE_DPP_CAS64("o1l", "o1h", "k1l", "k1h", "k0l", "k0h", C)                           \
-          : [o0l] "=&v"(o0l), [o0h] "=&v"(o0h), [o1l] "=&v"(o1l), [o1h] "=&v"(o1h), [jl] "=&v"(jl), \
-            [jh] "=&v"(jh)                                                                         \
-          : [k0l] "v"(k0l), [k0h] "v"(k0h), [k1l] "v"(k1l), [k1h] "v"(k1h), [lm] "s"(lower)       \
-          : "vcc", "scc");                                                                         \
-    else                                                                                           \
-      asm("s_nop 1\n" BCE_DPP_CAS64("o0l", "o0h", "k0l", "k0h", "k0l", "k0h", C)                 \
-              BCE_DPP_CAS64("o1l", "o1h", "k1l", "k1h", "k1l", "k1h", C)                           \
-          : [o0l] "=&v"(o0l), [o0h] "=&v"(o0h), [o1l] "=&v"(o1l), [o1h] "=&v"(o1h), [jl] "=&v"(jl), \
-            [jh] "=&v"(jh)                                                                         \
-          : [k0l] "v"(k0l), [k0h] "v"(k0h), [k1l] "v"(k1l), [k1h] "v"(k1h), [lm] "s"(lower)       \
-          : "vcc", "scc");                                                                         \
-  } while (0)
-
-constexpr bool dpp_fusable64(int M) { return M == 1 || M == 2 || M == 3 || M == 7 || M == 8 || M == 15; }
-
-template <int M, bool FLIP, int R>
-__device__ __forceinline__ void dpp_stage64(uint64_t (&key)[R], uint64_t lower) {
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int q = FLIP ? R - 1 - r : r + 1;  // the block's second key
-    if (FLIP ? (r >= q) : (r & 1)) continue;
-    const unsigned k0l = k_lo(key[r]), k0h = k_hi(key[r]), k1l = k_lo(key[q]), k1h = k_hi(key[q]);
-    unsigned o0l, o0h, o1l, o1h, jl, jh;
-    if constexpr (M == 1) BCE_DPP_PAIR64("quad_perm:[1,0,3,2]", FLIP);
-    else if constexpr (M == 2) BCE_DPP_PAIR64("quad_perm:[2,3,0,1]", FLIP);
-    else if constexpr (M == 3) BCE_DPP_PAIR64("quad_perm:[3,2,1,0]", FLIP);
-    else if constexpr (M == 7) BCE_DPP_PAIR64("row_half_mirror", FLIP);
-    else if constexpr (M == 8) BCE_DPP_PAIR64("row_ror:8", FLIP);
-    else BCE_DPP_PAIR64("row_mirror", FLIP);
-    (void)jl;
-    (void)jh;
-    key[r] = k_make(o0h, o0l);
-    key[q] = k_make(o1h, o1l);
-  }
-}
-
 // Half-cleaner across lane bit 4 or 5 (l ^ 16, l ^ 32) on pairs of keys: v_permlane16/32_swap
 // of keys (a, b) leaves each lane holding both members of one pair -- a[l] and a[l ^ M] in
 // the lanes with the bit clear, b[l ^ M] and b[l] in the others, the lower position always
@@ -355,11 +301,6 @@ __device__ __forceinline__ void wide_stage(KT (&key)[R], unsigned* sX, int t, in
     const bool lower = (lane & (flip ? (K / R / 2) : MK)) == 0;
     if constexpr (!K64 && R == 8 && dpp_fusable(MK)) {
       dpp_stage8<MK, flip>(key, (uint64_t)ballot(lower));
-      if constexpr (J > 1) wide_stage<NN, NW, R, K, J / 2>(key, sX, t, lane);
-      return;
-    }
-    if constexpr (K64 && R >= 2 && dpp_fusable64(MK)) {
-      dpp_stage64<MK, flip>(key, (uint64_t)ballot(lower));
       if constexpr (J > 1) wide_stage<NN, NW, R, K, J / 2>(key, sX, t, lane);
       return;
     }

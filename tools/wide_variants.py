@@ -34,20 +34,12 @@ OUT = tab_variants.OUT
 # DESIGN.md §4.2 / §4.9 and profiles/r04c, r04e, r04f, r04k, r04m, r04aa.
 VARIANTS = {
     "wbase": [],
-    # 64-bit keys without the fused DPP compare-exchange lane stages (generic moves + compares)
-    "k64gen": [("consensus_wide.hip", "constexpr bool dpp_fusable64(int M) { return M == 1 ||",
-                "constexpr bool dpp_fusable64(int M) { return false && M == 1 ||")],
-    # C5 MFMA pass with a 4-waves-per-SIMD register budget (<= 128 VGPRs; shipped: 140, 3 waves)
-    "c5w4": [("stats.hip", "__global__ __launch_bounds__(256) void reestimate_votes_mfma_kernel(",
-              "__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void reestimate_votes_mfma_kernel(")],
-    "c5w5": [("stats.hip", "__global__ __launch_bounds__(256) void reestimate_votes_mfma_kernel(",
-              "__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) void reestimate_votes_mfma_kernel(")],
     # small planned calls without the bin merges / merging below 3 resident rounds (shipped: 6)
     "nomerge": [("consensus.hip", "constexpr double kMergeRounds = 6.0;", "constexpr double kMergeRounds = 0.0;")],
     "merge3": [("consensus.hip", "constexpr double kMergeRounds = 6.0;", "constexpr double kMergeRounds = 3.0;")],
-    # C2 tab kernel: the next tile's metadata read at the top of the tile (round 4) instead of
-    # after the walk (shipped: late, no spill stores in the tile loop)
-    "tabearly": [("consensus_tab.hip", "constexpr bool kTabMetaEarly = false;", "constexpr bool kTabMetaEarly = true;")],
+    # C2 tab kernel: the next tile's metadata read after the walk (no spill stores in the tile
+    # loop; shipped: at the top of the tile, as round 4)
+    "tablate": [("consensus_tab.hip", "constexpr bool kTabMetaEarly = true;", "constexpr bool kTabMetaEarly = false;")],
     # tie-break FULL tiles: staging batches of the predictions / confidences (shipped: 8)
     "tbpc16": [("tiebreak.hip", "constexpr int kTbFullBatchPC = 8;", "constexpr int kTbFullBatchPC = 16;")],
     "tbpc4": [("tiebreak.hip", "constexpr int kTbFullBatchPC = 8;", "constexpr int kTbFullBatchPC = 4;")],
