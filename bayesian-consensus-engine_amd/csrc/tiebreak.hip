@@ -444,15 +444,25 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
       sRowN[wv][lane] = n;
       wave_sync_lds();
     }
-    // GATHER: row r's agents [0, cnt) <-> global [off_r, off_r + cnt), NP / 4 lanes per row
-    // (4 agents each), 64 / (NP / 4) rows per pass; `load` reads a slot, `save` writes it
-    constexpr int kGL = NP / 4, kGR = 64 / kGL;
+    // GATHER: row r's agents [0, cnt) <-> global [off_r, off_r + cnt) as 16-B aligned pairs:
+    // NP / 2 lanes per row, lane c of a row owns the pair starting at agent 2c - (off_r & 1)
+    // (the row's aligned start), 64 / (NP / 2) rows per pass, NP / 2 passes -- one 16-B access
+    // per lane and pass, as many as the contiguous staging of a full tile.  A 32-agent row
+    // starting at an odd agent has one agent past its last pair (`tail`).  body(r, i, ro, rn)
+    // gets the row's agent index i of the pair's first element (-1 .. NP - 1).
+    constexpr int kGL = NP / 2, kGR = 64 / kGL;
     auto rows_copy = [&](auto&& body) {
-#pragma unroll 2
+#pragma unroll 4
       for (int pass = 0; pass < kGL; ++pass) {
         const int r = pass * kGR + lane / kGL, c = lane % kGL;
-        body(r, 4 * c, sRowOff[wv][r], sRowN[wv][r]);
+        const int64_t ro = sRowOff[wv][r];
+        body(r, 2 * c - (int)(ro & 1), ro, sRowN[wv][r]);
       }
+    };
+    auto rows_tail = [&](auto&& body) {  // agent NP of an odd-start NP-agent row, one lane each
+      const int r = lane;
+      const int64_t ro = sRowOff[wv][r];
+      if ((ro & 1) && sRowN[wv][r] == NP) body(r, NP - 1, ro);
     };
     // every lane reads inside its own row (positions past n re-read the last agent); a lane
     // with an empty market reads the tile's first agent (masked later)
@@ -465,14 +475,14 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     auto stage = [&](const double* src) {
       wave_sync_lds();  // the buffer's previous readers (this wave) are done
       if constexpr (GATHER) {
-        rows_copy([&](int r, int i0, int64_t ro, int rn) {
-          double v[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = (i0 + e < rn) ? src[ro + i0 + e] : 0.0;
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (i0 + e < rn) buf[tb_pad(NP * r + i0 + e)] = v[e];
+        rows_copy([&](int r, int i, int64_t ro, int rn) {
+          if (i + 1 >= 0 && i < rn) {  // the pair [i, i + 1] touches the row
+            const double2 v = tb_ld2(src + ro + i);  // 16-B aligned: ro + i is even
+            if (i >= 0) buf[tb_pad(NP * r + i)] = v.x;
+            if (i + 1 < rn) buf[tb_pad(NP * r + i + 1)] = v.y;
+          }
         });
+        rows_tail([&](int r, int i, int64_t ro) { buf[tb_pad(NP * r + i)] = src[ro + i]; });
         wave_sync_lds();
         return;
       }
@@ -539,11 +549,17 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     auto flush = [&](double* dst) {
       wave_sync_lds();
       if constexpr (GATHER) {
-        rows_copy([&](int r, int i0, int64_t ro, int rn) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (i0 + e < rn) dst[ro + i0 + e] = buf[tb_pad(NP * r + i0 + e)];
+        // a pair wholly inside the row leaves as one 16-B store; a pair the row shares with
+        // its neighbour writes only its own agent
+        rows_copy([&](int r, int i, int64_t ro, int rn) {
+          if (i >= 0 && i + 1 < rn) {
+            tb_st2(dst + ro + i, buf[tb_pad(NP * r + i)], buf[tb_pad(NP * r + i + 1)]);
+          } else {
+            if (i >= 0 && i < rn) dst[ro + i] = buf[tb_pad(NP * r + i)];
+            if (i + 1 >= 0 && i + 1 < rn) dst[ro + i + 1] = buf[tb_pad(NP * r + i + 1)];
+          }
         });
+        rows_tail([&](int r, int i, int64_t ro) { dst[ro + i] = buf[tb_pad(NP * r + i)]; });
         wave_sync_lds();
         return;
       }
@@ -561,11 +577,11 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     auto flush_i32 = [&](int32_t* dst) {
       wave_sync_lds();
       if constexpr (GATHER) {
-        rows_copy([&](int r, int i0, int64_t ro, int rn) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (i0 + e < rn) dst[ro + i0 + e] = ibuf[tb_pad(NP * r + i0 + e)];
+        rows_copy([&](int r, int i, int64_t ro, int rn) {
+          if (i >= 0 && i < rn) dst[ro + i] = ibuf[tb_pad(NP * r + i)];
+          if (i + 1 >= 0 && i + 1 < rn) dst[ro + i + 1] = ibuf[tb_pad(NP * r + i + 1)];
         });
+        rows_tail([&](int r, int i, int64_t ro) { dst[ro + i] = ibuf[tb_pad(NP * r + i)]; });
         wave_sync_lds();
         return;
       }
@@ -1246,9 +1262,15 @@ static int launch_tb_short(const TbArgs& a, const int32_t* market_list, int64_t 
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     bool split = !EXOTIC && a.rmode == 0 && al16(a.pred) && al16(a.conf) &&
                  al16(a.weight) && al16(a.rel);
-    // market lists: rows gathered into LDS, NP = the list's bound rounded up to 8 / 16 / 32
+    // market lists: rows gathered into LDS as 16-B aligned pairs (every array 16-B aligned;
+    // else each lane reads and writes its own row in global memory), NP = the list's bound
+    // rounded up to 8 / 16 / 32
     const int np = max_len <= 8 ? 8 : max_len <= 16 ? 16 : 32;
-    const void* fn = market_list ? (np == 8    ? reinterpret_cast<const void*>(&tiebreak_lpm_kernel<true, EXOTIC, 0, 8, true>)
+    const bool gather = al16(a.pred) && al16(a.conf) && al16(a.weight) && al16(a.rel) &&
+                        (!a.g_key || al16(a.g_key)) && (!a.g_density || al16(a.g_density)) &&
+                        (!a.g_avgconf || al16(a.g_avgconf)) && (!a.g_maxrel || al16(a.g_maxrel));
+    const void* fn = (market_list && !gather) ? reinterpret_cast<const void*>(&tiebreak_lpm_kernel<false, EXOTIC>)
+                     : market_list ? (np == 8    ? reinterpret_cast<const void*>(&tiebreak_lpm_kernel<true, EXOTIC, 0, 8, true>)
                                     : np == 16 ? reinterpret_cast<const void*>(&tiebreak_lpm_kernel<true, EXOTIC, 0, 16, true>)
                                                : reinterpret_cast<const void*>(&tiebreak_lpm_kernel<true, EXOTIC, 0, 32, true>))
                      : split     ? reinterpret_cast<const void*>(&tiebreak_lpm_kernel<true, false, 1>)
@@ -1259,7 +1281,9 @@ static int launch_tb_short(const TbArgs& a, const int32_t* market_list, int64_t 
     split = split && blocks * kTbLpmWaves <= kSplitWords;  // one split word per wave of the grid
     hipStream_t st = as_stream(stream);
     const dim3 grid((int)blocks), block(64 * kTbLpmWaves);
-    if (market_list) {
+    if (market_list && !gather) {
+      hipLaunchKernelGGL((tiebreak_lpm_kernel<false, EXOTIC>), grid, block, 0, st, a, market_list, nl, fault_word());
+    } else if (market_list) {
       if (np == 8)
         hipLaunchKernelGGL((tiebreak_lpm_kernel<true, EXOTIC, 0, 8, true>), grid, block, 0, st, a, market_list, nl,
                            fault_word());

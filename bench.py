@@ -62,6 +62,8 @@ def parse(argv=None):
     p.add_argument("--markets", type=int, default=1_000_000)
     p.add_argument("--len", type=int, default=32)
     p.add_argument("--ragged", action="store_true", help="tb: market lengths uniform on 1..--len")
+    p.add_argument("--tb-contiguous", action="store_true",
+                   help="tb: contiguous tiles only (no length-bucket plan), the A/B for batch.tiebreak_plan")
     p.add_argument("--sources", type=int, default=10_000)
     p.add_argument("--mode", default=None, choices=["exact", "fast"],
                    help="consensus summation mode (default: exact for c2, where it costs nothing; fast -- "

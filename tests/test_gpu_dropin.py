@@ -1059,6 +1059,18 @@ def test_tiebreak_market_list_gather_bounds():
         N.check_faults(torch.device("cuda", 0), f"list bound {bound}")
         for k in ("winner", "label", "n_groups", "variance"):
             assert getattr(r, k).cpu().numpy()[sel].tobytes() == getattr(ref, k).cpu().numpy()[sel].tobytes(), (bound, k)
+    # arrays 8-B but not 16-B aligned: the per-lane row path, same results
+    U = lambda a: torch.from_numpy(np.concatenate([[0.0], a])).cuda()[1:]  # noqa: E731
+    du = [d[0], U(pred), U(conf), U(weight), U(rel)]
+    sel = np.nonzero(lens <= 30)[0].astype(np.int32)
+    r = batch.tiebreak(*d, max_len=32)
+    outs = [N.ptr(getattr(r, k)) for k in ("winner", "label", "n_groups", "variance", "g_key", "g_count",
+                                           "g_density", "g_avgconf", "g_maxrel", "g_of")]
+    assert L.bce_tiebreak_csr(N.ptr(d[0]), len(lens), N.ptr(T(sel)), len(sel), *[N.ptr(x) for x in du[1:]], 30, 6,
+                              *outs, N.stream(d[0].device)) == 0
+    torch.cuda.synchronize()
+    for k in ("winner", "label", "n_groups", "variance"):
+        assert getattr(r, k).cpu().numpy()[sel].tobytes() == getattr(ref, k).cpu().numpy()[sel].tobytes(), k
     # a listed market longer than the bound
     sel = np.array([0, int(np.argmax(lens)), 1], np.int32)
     r = batch.tiebreak(*d, max_len=32)
