@@ -326,14 +326,18 @@ class TiePlan:
     buckets: Optional[list]  # [(device int32 list, max_len)], or None: contiguous tiles
 
 
-# relative cost of a 64-market tile: contiguous FULL (every market 32 agents) / contiguous
-# ragged (the general 32-position body) / gathered buckets of 8 / 16 / 32 positions
-_TILE_COST = {"full": 0.55, "ragged": 1.0, 8: 0.22, 16: 0.5, 32: 1.05}
+# relative cost of a 64-market tile, measured (profiles/r05f/, 1M markets): contiguous FULL
+# (every market 32 agents: 42 ns per tile) / contiguous ragged (the general 32-position body:
+# 46 ns) / gathered buckets of 8 / 16 / 32 positions (20 / 40 / 70 ns).  The lane kernels are
+# latency-bound by their stage -> compute -> flush phases, so fewer positions per lane save
+# less than the arithmetic suggests, and a uniform 1..32 ragged batch stays contiguous
+# (buckets 0.788 vs 0.732 ms); a batch of mostly short markets is bucketed.
+_TILE_COST = {"full": 0.91, "ragged": 1.0, 8: 0.43, 16: 0.87, 32: 1.52}
 
 
-def tiebreak_plan(offsets_host: np.ndarray, device=None) -> TiePlan:
+def tiebreak_plan(offsets_host: np.ndarray, device=None, force: bool = False) -> TiePlan:
     """Length buckets for batch.tiebreak (markets of <= 32 agents), when they cost less than
-    the contiguous tiles by the kernels' relative tile costs (_TILE_COST)."""
+    the contiguous tiles by the kernels' relative tile costs (_TILE_COST), or always (force)."""
     lens = np.diff(np.asarray(offsets_host, np.int64))
     if len(lens) == 0 or int(lens.max()) > 32:
         return TiePlan(None)
@@ -345,7 +349,7 @@ def tiebreak_plan(offsets_host: np.ndarray, device=None) -> TiePlan:
     edges = ((0, 8), (9, 16), (17, 32))
     idx = [np.nonzero((lens >= lo) & (lens <= hi))[0].astype(np.int32) for lo, hi in edges]
     bucket = sum(_TILE_COST[hi] * ((len(i) + 63) // 64) for (lo, hi), i in zip(edges, idx))
-    if bucket >= 0.9 * contig:
+    if bucket >= 0.9 * contig and not force:
         return TiePlan(None)
     dev = device or N.device()
     return TiePlan([(torch.from_numpy(i).to(dev), hi) for (lo, hi), i in zip(edges, idx) if len(i)])

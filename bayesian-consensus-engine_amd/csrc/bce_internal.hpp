@@ -30,7 +30,7 @@ int ensure_dynamic_lds(const void* fn, int bytes);
 // event on `st`, makes the first k side streams wait on it and takes the device's fork lock,
 // which the caller holds until side_join has made `st` wait on their work -- so two host
 // threads planning on different streams never wait on each other's fork/join events.
-constexpr int kSideStreams = 2;
+constexpr int kSideStreams = 1;
 int side_fork(hipStream_t st, int k, hipStream_t* sides, std::unique_lock<std::mutex>* lock);
 int side_join(hipStream_t st, int k);
 

@@ -1671,7 +1671,6 @@ constexpr int kBinNp2Lo = 8, kBinNp2Hi = 10;  // the 1536 and 3072 bins
 static_assert(kBinMax[kBinNp2Lo] == 1536 && kBinMax[kBinNp2Hi] == 3072, "non-power-of-two bins");
 constexpr int kPlanSideLast = 3;  // bins 0..3 (n <= 64) run on the side stream
 constexpr double kMergeRounds = 6.0;  // merge a small call's bins below this many resident rounds
-constexpr bool kSmallSide = true;     // a small call's 65..1024 bins on a second side stream
 static int bin_of(int64_t n) {
   for (int b = 0; b < BCE_NBINS - 1; ++b)
     if (n <= kBinMax[b]) return b;
@@ -1754,13 +1753,13 @@ extern "C" int bce_consensus_planned(const int64_t* offsets, int64_t n_markets, 
   // on C3: 1.73 -> 1.65 ms; moving wide bins to the side stream too, or forking every bin
   // over 2-8 streams, was slower (profiles/r02_c3_plan_streams.jsonl); so was dealing every
   // bin over 2 or 4 streams with the resident grid shared out by estimated work (round 5,
-  // profiles/r05b/: one 8th of C3 0.233 -> 0.294 / 0.307 ms).
-  hipStream_t sides[2] = {st, st};
+  // profiles/r05b/: one 8th of C3 0.233 -> 0.294 / 0.307 ms), and a small call's 65..1024
+  // launches on a second side stream (0.2188 -> 0.2325 ms, profiles/r05f/).
+  hipStream_t side = st;
   std::unique_lock<std::mutex> fork_lock;
   constexpr int side_last = kPlanSideLast;
-  rc = side_fork(st, 2, sides, &fork_lock);
+  rc = side_fork(st, 1, &side, &fork_lock);
   if (rc) return rc;
-  const hipStream_t side = sides[0];
   // Launches: bin b runs with the markets of bins lo[b]..b in one kernel sized for bin b (its
   // own markets first, then the shorter bins' -- consensus_wide_kernel's list_hi).
   //   EXACT: the non-power-of-two bins (1025..1536, 2049..3072) always ride in the launch of the
@@ -1783,9 +1782,6 @@ extern "C" int bce_consensus_planned(const int64_t* offsets, int64_t n_markets, 
   bool merged_away[BCE_NBINS] = {};
   for (int b = 0; b < BCE_NBINS; ++b)
     for (int k = lo[b]; k < b; ++k) merged_away[k] = true;
-  // A small call's 65..1024 launches (a round or two of 1- and 2-wave workgroups, latency-
-  // bound) run on a second side stream beside the long bins (kSmallSide)
-  const bool small = kSmallSide && lo[kPlanSideLast + 3] != kPlanSideLast + 3;
   // Longest bins first, except that the 2049..3072 bin precedes the 3073..4096 one: its
   // 6-wave workgroups leave 4 of a CU's 16 wave slots free (two per CU at 128 VGPRs), which
   // the side stream's short-market kernels then fill (C3 fast -1.3%,
@@ -1803,7 +1799,7 @@ extern "C" int bce_consensus_planned(const int64_t* offsets, int64_t n_markets, 
       a.n_hi = bin_start_host[b + 1] - bin_start_host[b];
     }
     if (a.n_list == 0) continue;
-    hipStream_t sb = (b <= side_last) ? side : (small && b <= kPlanSideLast + 4) ? sides[1] : st;
+    hipStream_t sb = (b <= side_last) ? side : st;
     if (b <= 3 && seg_ok) {
       static const int lens[4] = {8, 16, 32, 64};
       rc = launch_seg_for_len(lens[b], a, sb);
@@ -1825,7 +1821,7 @@ extern "C" int bce_consensus_planned(const int64_t* offsets, int64_t n_markets, 
     }
     if (rc) break;
   }
-  const int rj = side_join(st, 2);  // join even after a failed launch: st must not run ahead
+  const int rj = side_join(st, 1);  // join even after a failed launch: st must not run ahead
   if (!rc) rc = rj;
   return rc;
 }

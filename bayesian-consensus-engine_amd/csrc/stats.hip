@@ -238,8 +238,9 @@ __global__ __launch_bounds__(256) void reestimate_agreement_votes_kernel(
 // w[a + (l >> 4)]), B = a 4-agent x 16-market block of P (lane l holds
 // P[a + (l >> 4)][m0 + 16j + (l & 15)]), so every row of D is the block's 16 column sums (a
 // GEMV leaves 15 of 16 rows redundant; the kernel is HBM-bound either way).  A wave owns 64
-// markets (four 16-column accumulators), 16 agents per step (16 loads in flight), and the
-// vote words come from the same loads (below).
+// markets (four 16-column accumulators), 16 agents per step (16 loads in flight).  The
+// vote bits come from the same loads: ballot j holds bit 16k + n = (P[a+k][m0+16j+n] >=
+// 0.5), regrouped per agent into the vote_bits word layout of the exact kernel.
 // The sums are in MFMA order, not agent order (within 4*A*2^-53 of the exact consensus);
 // markets whose consensus lies within 8*A*2^-53 of 0.5 -- where the vote could differ --
 // (or whose column holds a finite cell outside [0, 1], where that bound does not hold) are
@@ -251,6 +252,7 @@ __global__ __launch_bounds__(256) void reestimate_agreement_votes_kernel(
 // fixup kernels exit at once and the exact kernel (launched behind them, gated on the same
 // word) computes the iteration instead -- same results, exact-mode speed.
 typedef double mfma_d4 __attribute__((ext_vector_type(4)));
+constexpr int kMfmaSteps = 4;  // 4-agent MFMA steps per loop iteration (16 agents)
 
 __global__ __launch_bounds__(256) void reestimate_total_kernel(const double* __restrict__ w, int64_t A,
                                                                double* __restrict__ total_fast,
@@ -280,39 +282,14 @@ __global__ __launch_bounds__(256) void reestimate_total_kernel(const double* __r
   }
 }
 
-// The exact kernel's load schedule (round 5, verdict r04 item 6): lane = market column, 16
-// agent rows per step as coalesced 512-B row segments, the rows' vote ballots are the vote
-// words directly; each group of 4 rows is regrouped for the MFMA B operand by a 4 x 4
-// transpose of 16-lane groups (two v_permlane32_swap and two v_permlane16_swap levels per
-// 32-bit half), so lane l then holds P[a + l/16][m0 + 16j + l%16] of block j.  (Round 3's
-// kernel loaded the B layout directly -- 4 rows x 128 B per instruction -- and ran 6% behind
-// the exact kernel: 24.8 vs 23.4 ms per iteration, profiles/r05d/.)
-__device__ __forceinline__ void xpose16x4(double (&x)[4]) {
-  unsigned lo[4], hi[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    lo[k] = (unsigned)__double_as_longlong(x[k]);
-    hi[k] = (unsigned)((unsigned long long)__double_as_longlong(x[k]) >> 32);
-  }
-  auto sw32 = [](unsigned& a, unsigned& b) {
-    const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
-    a = r[0];
-    b = r[1];
-  };
-  auto sw16 = [](unsigned& a, unsigned& b) {
-    const auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
-    a = r[0];
-    b = r[1];
-  };
-  // groups g of register k: T[k][g]; after the two levels register j holds T[0..3][j]
-  sw32(lo[0], lo[2]); sw32(hi[0], hi[2]);
-  sw32(lo[1], lo[3]); sw32(hi[1], hi[3]);
-  sw16(lo[0], lo[1]); sw16(hi[0], hi[1]);
-  sw16(lo[2], lo[3]); sw16(hi[2], hi[3]);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) x[k] = __longlong_as_double((long long)(((unsigned long long)hi[k] << 32) | lo[k]));
-}
-
+// Round 5 (verdict r04 item 6): fed from the exact kernel's load schedule instead -- lane =
+// market column, 16 rows as coalesced 512-B segments, the vote words straight from the row
+// ballots, each 4-row group regrouped for the B operand by a 4 x 4 transpose of 16-lane
+// groups (two permlane32 and two permlane16 swap levels per 32-bit half) -- the pass took
+// 28.7 ms against this kernel's 26.0 and the exact kernel's 23.2 (same box, profiles/r05f/):
+// 128 VGPRs (4 waves per SIMD) and a transpose per 4 rows for no load-side gain.  A 4-waves-
+// per-SIMD budget for this kernel (106 VGPRs) measured 24.86 vs 24.77 ms (profiles/r05d/).
+// Both are HBM streams of P; the exact agent-order kernel stays the default.
 __global__ __launch_bounds__(256) void reestimate_votes_mfma_kernel(
     const double* __restrict__ P, int64_t A, int64_t M, int64_t ld, const double* __restrict__ w,
     const double* __restrict__ total_fast, double* __restrict__ cons, uint8_t* __restrict__ null_out,
@@ -320,53 +297,70 @@ __global__ __launch_bounds__(256) void reestimate_votes_mfma_kernel(
     unsigned long long* __restrict__ ok_words, int32_t* __restrict__ nflag, int32_t* __restrict__ flags) {
   if (nflag[1]) return;  // weights outside [0, inf): the gated exact kernel does this iteration
   const int lane = lane_id();
-  const int64_t m = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const int64_t k = m >> 6;  // vote word = 64 markets
+  const int64_t k = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;  // vote word = 64 markets
   const int64_t m0 = k << 6;
   if (m0 >= M) return;  // wave-uniform
-  const bool in = m < M;
-  const double* col = P + (in ? m : 0);
+  const int ka = lane >> 4, n = lane & 15;
   mfma_d4 acc[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) acc[j] = mfma_d4{0.0, 0.0, 0.0, 0.0};
+  bool inm[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) inm[j] = m0 + 16 * j + n < M;
   unsigned long long* vb = vote_bits + k * A;
-  bool odd = false;   // a cell outside [0, 1] (or NaN) in this lane's column
-  bool hnan = false;  // a NaN cell in this lane's column
-  const int ka = lane >> 4;
-  for (int64_t a = 0; a < A; a += kVoteRows) {
-    double v[kVoteRows];
+  bool odd[4] = {false, false, false, false};  // a cell outside [0, 1] (or NaN) in this lane's column
+  bool hnan[4] = {false, false, false, false};  // a NaN cell in this lane's column
+  for (int64_t a = 0; a < A; a += 4 * kMfmaSteps) {
+    double v[kMfmaSteps][4], wa[kMfmaSteps];
 #pragma unroll
-    for (int q = 0; q < kVoteRows; ++q) v[q] = (in && a + q < A) ? col[(a + q) * ld] : 0.0;
-    unsigned long long mine = 0;
+    for (int q = 0; q < kMfmaSteps; ++q) {
+      const int64_t ag = a + 4 * q + ka;
+      const bool ain = ag < A;
+      wa[q] = ain ? w[ag] : 0.0;
 #pragma unroll
-    for (int q = 0; q < kVoteRows; ++q) {
-      odd = odd || !(v[q] >= 0.0 && v[q] <= 1.0);
-      hnan = hnan || (v[q] != v[q]);
-      const unsigned long long b = ballot(in && a + q < A && v[q] >= 0.5);  // market.py:298-299
-      mine = (lane == q) ? b : mine;
+      for (int j = 0; j < 4; ++j) v[q][j] = (ain && inm[j]) ? P[ag * ld + m0 + 16 * j + n] : 0.0;
     }
-    if (lane < kVoteRows && a + lane < A) vb[a + lane] = mine;
 #pragma unroll
-    for (int g = 0; g < kVoteRows / 4; ++g) {
-      double x[4] = {v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
-      xpose16x4(x);  // x[j]: lane l holds P[a + 4g + l/16][m0 + 16j + l%16]
-      const int64_t ag = a + 4 * g + ka;
-      const double wa = ag < A ? w[ag] : 0.0;
+    for (int q = 0; q < kMfmaSteps; ++q) {
+      unsigned long long bal[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(wa, x[j], acc[j], 0, 0, 0);
+      for (int j = 0; j < 4; ++j) {
+        acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(wa[q], v[q][j], acc[j], 0, 0, 0);
+        odd[j] = odd[j] || !(v[q][j] >= 0.0 && v[q][j] <= 1.0);
+        hnan[j] = hnan[j] || (v[q][j] != v[q][j]);
+        bal[j] = ballot(a + 4 * q + ka < A && inm[j] && v[q][j] >= 0.5);  // market.py:298-299
+      }
+      // agent a + 4q + lane's vote word (lanes 0..3): its 16-bit slice of every ballot
+      unsigned long long word = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) word |= ((bal[j] >> (16 * (lane & 3))) & 0xFFFFull) << (16 * j);
+      if (lane < 4 && a + 4 * q + lane < A) vb[a + 4 * q + lane] = word;
     }
   }
   // lane L = 16j + n' holds market m0 + L's sum in acc[j] (every row of D is the same)
   const int jj = lane >> 4;
   const double ws = (jj == 0) ? acc[0][0] : (jj == 1) ? acc[1][0] : (jj == 2) ? acc[2][0] : acc[3][0];
+  const int64_t m = m0 + lane;
+  const bool in = m < M;
   const double total = *total_fast;
   const bool isnull = (total == 0.0);  // w >= 0: zero in every order iff every weight is zero
   const double c = isnull ? 0.0 : ws / total;
   // |fast - exact| <= ~4*A*2^-53 for cells in [0, 1] (both sums of non-negative terms within
   // A*2^-53 relative of the true one, c <= 1); a column holding another finite value is
   // always redone, a column holding a NaN never (NaN in every order)
+  unsigned long long oddm = 0, nanm = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    unsigned long long b = ballot(odd[j]);
+    b |= (b >> 16) | (b >> 32) | (b >> 48);
+    oddm |= (b & 0xFFFFull) << (16 * j);
+    unsigned long long q = ballot(hnan[j]);
+    q |= (q >> 16) | (q >> 32) | (q >> 48);
+    nanm |= (q & 0xFFFFull) << (16 * j);
+  }
   const double bound = 8.0 * (double)(A + 2) * 0x1p-53;
-  const bool near = in && !isnull && !hnan && (fabs(c - 0.5) <= bound || odd);
+  const bool colnan = (nanm >> lane) & 1ull;
+  const bool near = in && !isnull && !colnan && (fabs(c - 0.5) <= bound || ((oddm >> lane) & 1ull));
   if (in) {
     cons[m] = c;
     null_out[m] = isnull ? 1 : 0;

@@ -1008,8 +1008,13 @@ def test_tiebreak_length_buckets_vs_oracle(precision):
     keys = np.array([round(float(x), precision) for x in pred], np.float64)
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
     d = [T(off), T(pred), T(conf), T(weight), T(rel)]
-    plan = batch.tiebreak_plan(off)
+    plan = batch.tiebreak_plan(off, force=True)
     assert plan.buckets is not None and [hi for _, hi in plan.buckets] == [8, 16, 32]
+    # the cost model keeps a uniform 0..32 batch contiguous and buckets a batch of short markets
+    assert batch.tiebreak_plan(off).buckets is None
+    short = np.zeros(3001, np.int64)
+    short[1:] = np.cumsum(rng.integers(0, 11, 3000))
+    assert batch.tiebreak_plan(short).buckets is not None
     r = batch.tiebreak(*d, precision=precision, plan=plan)
     c = batch.tiebreak(*d, precision=precision, max_len=32)
     torch.cuda.synchronize()

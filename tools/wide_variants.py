@@ -34,8 +34,6 @@ OUT = tab_variants.OUT
 # DESIGN.md §4.2 / §4.9 and profiles/r04c, r04e, r04f, r04k, r04m, r04aa.
 VARIANTS = {
     "wbase": [],
-    # small planned calls with every wide bin on st (shipped: 65..1024 on a second side stream)
-    "noside2": [("consensus.hip", "constexpr bool kSmallSide = true;", "constexpr bool kSmallSide = false;")],
     # small planned calls without the bin merges / merging below 3 resident rounds (shipped: 6)
     "nomerge": [("consensus.hip", "constexpr double kMergeRounds = 6.0;", "constexpr double kMergeRounds = 0.0;")],
     "merge3": [("consensus.hip", "constexpr double kMergeRounds = 6.0;", "constexpr double kMergeRounds = 3.0;")],
