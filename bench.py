@@ -27,8 +27,9 @@ Also measured here:
 Before the W warmup steps the device runs the step for --prewarm-s seconds so the clocks
 have ramped (a 20-step run then matches a 200-step one); that time is reported.
 Other configs (--config c3|c4|c5|ns|agg|tb) are secondary bench lines; the default is c2,
-and at N=1 the default run also appends c3, c4, tb and c5 (reduced steps, each with its
-roofline, CPU baseline and full-size parity) under "secondary" (--no-secondary skips them).
+and at N=1 the default run also appends c3, c3 over a 10M-source table, c4, tb and c5 (reduced
+steps, each with its roofline, CPU baseline and full-size parity) under "secondary"
+(--no-secondary skips them).
 """
 from __future__ import annotations
 
@@ -439,8 +440,10 @@ def rank_parity(res, offsets, sid, prob, rel, conf, present, unique, rank, m_sam
     return {"rank": rank, "markets": m, "signals": n, "all_equal": all(ok.values())}
 
 
-# (config, steps, warmup, clock ramp s): the clock ramp as in each config's own line
-SECONDARY = (("c3", 20, 3, 1.0), ("c4", 100, 10, 1.0), ("tb", 10, 2, 1.0), ("c5", 4, 1, 0.5))
+# (line, config, steps, warmup, clock ramp s, extra args): the clock ramp as in each config's own
+# line; c3_S10M = config 3 over C4's 10M-source table (64-bit sort keys, verdict r04 item 4)
+SECONDARY = (("c3", "c3", 20, 3, 1.0, {}), ("c3_S10M", "c3", 10, 2, 0.5, {"c3_sources": 10_000_000}),
+             ("c4", "c4", 100, 10, 1.0, {}), ("tb", "tb", 10, 2, 1.0, {}), ("c5", "c5", 4, 1, 0.5, {}))
 
 
 def run_secondary(args, world, rank) -> dict:
@@ -454,16 +457,18 @@ def run_secondary(args, world, rank) -> dict:
     from bench_extra import run_extra
 
     out = {}
-    for cfg, steps, warmup, ramp in SECONDARY:
+    for line, cfg, steps, warmup, ramp, extra in SECONDARY:
         a2 = copy.copy(args)
         a2.config, a2.steps, a2.warmup, a2.prewarm_s, a2.mode = cfg, steps, warmup, ramp, None
+        for k, v in extra.items():
+            setattr(a2, k, v)
         t0 = time.perf_counter()
         try:
             j = run_extra(a2, world, rank)
             r = j.get("roofline") or {}
             cb = j.get("cpu_baseline") or {}
             par = j.get("parity_vs_oracle")
-            out[cfg] = {"metric": j["metric"], "value": j["value"], "unit": j["unit"], "steps": steps,
+            out[line] = {"metric": j["metric"], "value": j["value"], "unit": j["unit"], "steps": steps,
                         "ms_per_step": j["ms_per_step"], "dtype": j.get("dtype"), "config": j.get("config"),
                         "roofline": {k: r.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic",
                                                            "kernel", "bytes_per_launch", "avg_launch_ms", "mfma",
@@ -471,10 +476,10 @@ def run_secondary(args, world, rank) -> dict:
                         "cpu_baseline": cb or None, "parity_vs_oracle": par,
                         "wall_s": round(time.perf_counter() - t0, 1)}
         except Exception as exc:  # a secondary line never takes the headline down
-            out[cfg] = {"error": f"{type(exc).__name__}: {exc}"}
+            out[line] = {"error": f"{type(exc).__name__}: {exc}"}
         gc.collect()
         torch.cuda.empty_cache()
-        print(f"[bench] secondary {cfg}: {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
+        print(f"[bench] secondary {line}: {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
     return out
 
 
