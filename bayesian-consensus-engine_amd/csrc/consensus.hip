@@ -1782,7 +1782,6 @@ extern "C" int bce_consensus_planned(const int64_t* offsets, int64_t n_markets, 
   bool merged_away[BCE_NBINS] = {};
   for (int b = 0; b < BCE_NBINS; ++b)
     for (int k = lo[b]; k < b; ++k) merged_away[k] = true;
-  base.small_call = lo[kPlanSideLast + 3] != kPlanSideLast + 3 ? 1 : 0;  // the 65..512 bins merged
   // Longest bins first, except that the 2049..3072 bin precedes the 3073..4096 one: its
   // 6-wave workgroups leave 4 of a CU's 16 wave slots free (two per CU at 128 VGPRs), which
   // the side stream's short-market kernels then fill (C3 fast -1.3%,

@@ -37,7 +37,6 @@ struct ConsArgs {
   int* fault;         // device word: set to a kFault* code by a wave that gave up
   int spin_cap;       // bounded waits of the persistent pipe kernel (polls before giving up)
   int32_t tab_rows;   // tab kernel, hybrid table: rows [0, tab_rows) staged in LDS, the rest read from relconf
-  int32_t small_call;  // host only: a planned call of few resident rounds per bin (a market shard)
 };
 
 // Device fault codes (bce_fault_check reports them).

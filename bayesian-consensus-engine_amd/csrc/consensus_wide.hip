@@ -40,7 +40,6 @@
 constexpr int kWideHR = 1;       // rounds of NT uniques whose gathers are in flight together (2: C3 fast +6%)
 constexpr int kWideWPE = 4;      // min waves per SIMD (register budget; 4 vs 2: exact -1.3%, fast unchanged)
 constexpr int kWideNWBF = 4;     // FAST nweight read-backs per batch (1: 1.645, 2: 1.634, 4: 1.587 ms C3)
-constexpr bool kSmallWide = true;  // small FAST calls: 4-wave 1024-key and 8-wave 2048-key bins (R = 4)
 
 namespace bce {
 namespace {
@@ -1071,18 +1070,14 @@ int launch_wide(const ConsArgs& a, hipStream_t st) {
 
 // (NW, R[, NN]) per length bin: P = 64*NW*R >= max_len; the 1536 and 3072 bins run the
 // 2048 / 4096-key network on 3 / 6 waves
-// A small FAST call (a market shard: a round or two of resident workgroups per bin) runs the
-// 513..1024 and 1025..2048 bins on twice the waves per market (R = 4): half the rounds' latency
-// for the same work, so the last, partly filled round costs less (kSmallWide).
+// (Round 5: a market shard's 513..1024 / 1025..2048 bins on 4 / 8 waves with R = 4 -- half the
+// latency per market, more rounds -- made one 8th of C3 slower, 0.2069-0.2072 -> 0.2274-0.2300
+// ms, profiles/r05g/; removed.)
 template <bool FAST>
 int launch_wide_mode(int64_t max_len, const ConsArgs& a, hipStream_t st) {
   if (max_len <= 128) return launch_wide<1, 2, FAST>(a, st);
   if (max_len <= 256) return launch_wide<1, 4, FAST>(a, st);
   if (max_len <= 512) return launch_wide<1, 8, FAST>(a, st);
-  if constexpr (FAST && kSmallWide) {
-    if (a.small_call && max_len <= 1024) return launch_wide<4, 4, FAST>(a, st);
-    if (a.small_call && max_len <= 2048) return launch_wide<8, 4, FAST>(a, st);
-  }
   if (max_len <= 1024) return launch_wide<2, 8, FAST>(a, st);
   if (max_len <= 1536) return launch_wide<3, 8, FAST, 4>(a, st);
   if (max_len <= 2048) return launch_wide<4, 8, FAST>(a, st);

@@ -34,8 +34,6 @@ OUT = tab_variants.OUT
 # DESIGN.md §4.2 / §4.9 and profiles/r04c, r04e, r04f, r04k, r04m, r04aa.
 VARIANTS = {
     "wbase": [],
-    # small FAST calls on the default 2- / 4-wave (R = 8) configurations (shipped: R = 4, 4 / 8 waves)
-    "nosmallwide": [("consensus_wide.hip", "constexpr bool kSmallWide = true;", "constexpr bool kSmallWide = false;")],
     # small planned calls without the bin merges / merging below 3 resident rounds (shipped: 6)
     "nomerge": [("consensus.hip", "constexpr double kMergeRounds = 6.0;", "constexpr double kMergeRounds = 0.0;")],
     "merge3": [("consensus.hip", "constexpr double kMergeRounds = 6.0;", "constexpr double kMergeRounds = 3.0;")],
