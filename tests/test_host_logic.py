@@ -274,3 +274,33 @@ def test_markstein_quotients_match_ieee_division(tmp_path):
     subprocess.run([cc, "-O2", "-ffp-contract=off", "-o", str(exe), src, "-lm"], check=True)
     out = subprocess.run([str(exe), "100"], check=True, capture_output=True, text=True).stdout
     assert out.strip().startswith("0 of "), out
+
+
+def test_tiebreak_plan_buckets_by_measured_tile_costs():
+    """batch.tiebreak_plan (host only): buckets of <= 8 / 9..16 / 17..32 agents exactly when
+    they cost less than contiguous tiles by the measured per-tile costs (profiles/r05f/): a
+    uniform 1..32 ragged batch and a uniform 32 batch stay contiguous, a batch of short markets
+    is bucketed, a batch with a market past 32 agents is never bucketed; every market lands in
+    exactly one bucket."""
+    import torch
+    from bayesian_engine import batch
+    rng = np.random.default_rng(5)
+    cpu = torch.device("cpu")
+
+    def off(lens):
+        o = np.zeros(len(lens) + 1, np.int64)
+        o[1:] = np.cumsum(lens)
+        return o
+
+    assert batch.tiebreak_plan(off(rng.integers(1, 33, 20000)), cpu).buckets is None
+    assert batch.tiebreak_plan(off(np.full(20000, 32)), cpu).buckets is None
+    assert batch.tiebreak_plan(off(np.append(rng.integers(0, 5, 1000), 33)), cpu).buckets is None
+    lens = rng.integers(0, 13, 20000)
+    p = batch.tiebreak_plan(off(lens), cpu)
+    assert p.buckets is not None
+    seen = np.concatenate([b.numpy() for b, _ in p.buckets])
+    assert np.array_equal(np.sort(seen), np.arange(len(lens)))
+    for b, hi in p.buckets:
+        assert lens[b.numpy()].max() <= hi
+    forced = batch.tiebreak_plan(off(rng.integers(1, 33, 500)), cpu, force=True)
+    assert [hi for _, hi in forced.buckets] == [8, 16, 32]
