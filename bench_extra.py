@@ -331,7 +331,8 @@ def _c3(args, world, rank, barrier, max_over, sum_over):
                    "markets_this_rank": Mloc, "signals_this_rank": n, "unique_per_market_mean": sum_u / max(Mloc, 1),
                    "bins": plan.bin_start.tolist(), "parallelism": f"markets sharded over {world} rank(s), no collective"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc("pmc_c3.json", signals_this_rank=n) if S == 1_000_000 else None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": (_pmc("pmc_c3.json", signals_this_rank=n) if S == 1_000_000 else
+                                 _pmc(f"pmc_c3_S{S // 1_000_000}M.json", signals_this_rank=n, sources=S)),
                      "kernel": "consensus (all bins, one step)",
                      "bytes_per_launch": bytes_step, "avg_launch_ms": per * 1e3,
                      f"{other}_mode": ({"ms_per_step": wall2 / a2.steps * 1e3, "avg_launch_ms": per2 * 1e3,

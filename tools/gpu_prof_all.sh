@@ -10,6 +10,7 @@ bash tools/gpu_profile.sh c2 consensus_tab32_kernel markets=1000000 signals_per_
 bash tools/gpu_profile.sh c4 replay_step_kernel sources_this_rank=10000000 -- --config c4 && \
 bash tools/gpu_profile.sh c3 consensus signals_this_rank=100000000 steps_total=7 stream_read_bytes=1201627112 -- --config c3 --single-mode && \
 python3 tools/pmc_summary.py span gpurun_out/prof_c3/stats "bce::" 12 > gpurun_out/prof_c3/step_span.json && \
+bash tools/gpu_profile.sh c3S10M consensus signals_this_rank=100000000 sources=10000000 steps_total=7 stream_read_bytes=1201627112 -- --config c3 --single-mode --c3-sources 10000000 && \
 bash tools/gpu_profile.sh tb "tiebreak_lpm_kernel<true, false, 1>" markets=1000000 -- --config tb && \
 bash tools/gpu_profile.sh c5 reestimate_consensus_votes_kernel markets_this_rank=1000000 mode=exact -- --config c5 --steps 2 --warmup 1 --single-mode && \
 python3 tools/pmc_summary.py stats gpurun_out/prof_c5/stats reestimate_agreement_votes_kernel > gpurun_out/prof_c5/stats_agreement.json && \
