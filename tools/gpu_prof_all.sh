@@ -11,7 +11,7 @@ bash tools/gpu_profile.sh c4 replay_step_kernel sources_this_rank=10000000 -- --
 bash tools/gpu_profile.sh c3 consensus signals_this_rank=100000000 steps_total=7 stream_read_bytes=1201627112 -- --config c3 --single-mode && \
 python3 tools/pmc_summary.py span gpurun_out/prof_c3/stats "bce::" 12 > gpurun_out/prof_c3/step_span.json && \
 bash tools/gpu_profile.sh c3S10M consensus signals_this_rank=100000000 sources=10000000 steps_total=7 stream_read_bytes=1201627112 -- --config c3 --single-mode --c3-sources 10000000 && \
-bash tools/gpu_profile.sh tb "tiebreak_lpm_kernel<true, false, 1>" markets=1000000 -- --config tb && \
+bash tools/gpu_profile.sh tb "tiebreak_lpm_kernel<true, false, 1, 32, false>" markets=1000000 -- --config tb && \
 bash tools/gpu_profile.sh c5 reestimate_consensus_votes_kernel markets_this_rank=1000000 mode=exact -- --config c5 --steps 2 --warmup 1 --single-mode && \
 python3 tools/pmc_summary.py stats gpurun_out/prof_c5/stats reestimate_agreement_votes_kernel > gpurun_out/prof_c5/stats_agreement.json && \
 python3 tools/pmc_summary.py pmc gpurun_out/prof_c5/fetch gpurun_out/prof_c5/write reestimate_agreement_votes_kernel \
