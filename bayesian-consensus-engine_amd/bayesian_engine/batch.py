@@ -544,10 +544,14 @@ def reestimate(P: torch.Tensor, iters: int, w0: float = 0.5, w: Optional[torch.T
     Each round reads P once: the consensus pass records every cell's vote as one bit and the
     agreement pass counts from those bits (bce_reestimate_consensus_votes /
     bce_reestimate_agreement_votes; A*ceil(M/64)*8 bytes of scratch).  ``mode="fast"``
-    runs the consensus pass on the matrix cores (bce_reestimate_consensus_votes_mfma:
-    consensus within 4*A*2^-53, votes and agreement counts identical to exact).  Its
-    summation order needs every weight finite and >= 0; the library checks that on the
-    device and runs the exact kernel for an iteration whose weights break it."""
+    runs the same exact agent-order kernel: it already streams P at the HBM rate, and the
+    matrix-core form measured slower, so the exact sums are also the
+    fastest ones within FAST's 1e-9.  ``mode="mfma"`` runs the consensus pass on the matrix
+    cores (bce_reestimate_consensus_votes_mfma: consensus within 4*A*2^-53, votes and
+    agreement counts identical to exact) -- the config-5 MFMA form the north star reports
+    utilisation for.  Its summation order needs every weight finite and >= 0; the library
+    checks that on the device and runs the exact kernel for an iteration whose weights
+    break it."""
     L = N.require_gpu()
     A, M = P.shape
     dev = P.device
@@ -563,10 +567,10 @@ def reestimate(P: torch.Tensor, iters: int, w0: float = 0.5, w: Optional[torch.T
     words = torch.empty((2, K), dtype=torch.int64, device=dev)  # cvote, ok
     hist = []
     st = N.stream(dev)
-    if mode not in _MODES:
-        raise ValueError(f"mode must be one of {sorted(_MODES)}")
+    if mode not in _MODES and mode != "mfma":
+        raise ValueError(f"mode must be one of {sorted([*_MODES, 'mfma'])}")
     scratch = None
-    if mode == "fast":
+    if mode == "mfma":
         nb = int(L.bce_reestimate_mfma_scratch_bytes(M))
         scratch = torch.empty((nb + 7) // 8, dtype=torch.int64, device=dev)
     for _ in range(iters):

@@ -148,6 +148,26 @@ __global__ __launch_bounds__(256) void reestimate_agreement_kernel(const double*
 // carries the total weight in agent order (core.py:107-120: the same for every column,
 // and free beside the stream), so no separate reduction launch is needed.
 constexpr int kVoteRows = 16;
+// A batch's kVoteRows weights: one vector load (lane q < kVoteRows holds w[a + q]), then a
+// readlane pair per row into SGPRs -- instead of kVoteRows scalar loads held across the batch
+// (32 SGPRs, which spilled to VGPR lanes: ~7 writelane / readlane per row).
+constexpr bool kVoteWLane = true;
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const int2 x = *reinterpret_cast<const int2*>(&v);
+  int2 y;
+  y.x = __builtin_amdgcn_readlane(x.x, l);
+  y.y = __builtin_amdgcn_readlane(x.y, l);
+  return *reinterpret_cast<const double*>(&y);
+}
+// v_writelane_b32 (the LLVM intrinsic; clang has no builtin for it): lane l of the result =
+// src (wave-uniform), every other lane keeps old -- a row's vote ballot into its agent's lane
+// without a (lane == q) mask per row held in SGPRs
+__device__ int bce_writelane(int src, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+__device__ __forceinline__ unsigned long long writelane_u64(unsigned long long v, int l, unsigned long long old) {
+  const unsigned lo = (unsigned)bce_writelane((int)(unsigned)v, l, (int)(unsigned)old);
+  const unsigned hi = (unsigned)bce_writelane((int)(unsigned)(v >> 32), l, (int)(unsigned)(old >> 32));
+  return ((unsigned long long)hi << 32) | lo;
+}
 __global__ __launch_bounds__(256) void reestimate_consensus_votes_kernel(
     const double* __restrict__ P, int64_t A, int64_t M, int64_t ld, const double* __restrict__ w,
     double* __restrict__ cons, uint8_t* __restrict__ null_out, unsigned long long* __restrict__ vote_bits,
@@ -162,21 +182,24 @@ __global__ __launch_bounds__(256) void reestimate_consensus_votes_kernel(
   if ((k << 6) >= M) return;  // whole wave past the last market (wave-uniform)
   const bool in = m < M;
   double ws = 0.0, total = 0.0;
-  const double* col = P + (in ? m : 0);
+  const double* col = P + (in ? m : 0);  // every lane's column address is valid: loads unconditional
   unsigned long long* vb = vote_bits + k * A;
   int64_t a = 0;
   for (; a + kVoteRows <= A; a += kVoteRows) {
     double v[kVoteRows];
 #pragma unroll
-    for (int q = 0; q < kVoteRows; ++q) v[q] = in ? col[(a + q) * ld] : 0.0;
+    for (int q = 0; q < kVoteRows; ++q) v[q] = col[(a + q) * ld];  // lanes past M: column 0, never stored
+    const double wl = kVoteWLane ? w[a + (lane & (kVoteRows - 1))] : 0.0;
     unsigned long long mine = 0;
 #pragma unroll
     for (int q = 0; q < kVoteRows; ++q) {
-      const double wq = w[a + q];
-      ws += (0.0 + v[q]) * wq;  // avg of one signal = 0 + p (core.py:116,136)
+      const double wq = kVoteWLane ? readlane_f64(wl, q) : w[a + q];
+      // the signal's avg is 0 + p (core.py:116,136); p * w instead of (0 + p) * w differs only
+      // in the sign of a zero product (p = -0.0), and ws -- which starts at +0.0 and so is
+      // never -0.0 under round-to-nearest -- is unchanged by adding a zero of either sign
+      ws += v[q] * wq;
       total += wq;
-      const unsigned long long b = ballot(in && v[q] >= 0.5);  // market.py:298-299
-      mine = (lane == q) ? b : mine;
+      mine = writelane_u64(ballot(in && v[q] >= 0.5), q, mine);  // market.py:298-299
     }
     if (lane < kVoteRows) vb[a + lane] = mine;
   }
@@ -234,25 +257,38 @@ __global__ __launch_bounds__(256) void reestimate_agreement_votes_kernel(
 }
 
 // ---- BCE_MODE_FAST pass 1 on the matrix cores ---------------------------------------
-// w^T P as v_mfma_f64_16x16x4_f64: A = w broadcast over the 16 rows (lane l holds
-// w[a + (l >> 4)]), B = a 4-agent x 16-market block of P (lane l holds
-// P[a + (l >> 4)][m0 + 16j + (l & 15)]), so every row of D is the block's 16 column sums (a
-// GEMV leaves 15 of 16 rows redundant; the kernel is HBM-bound either way).  A wave owns 64
-// markets (four 16-column accumulators), 16 agents per step (16 loads in flight).  The
-// vote bits come from the same loads: ballot j holds bit 16k + n = (P[a+k][m0+16j+n] >=
-// 0.5), regrouped per agent into the vote_bits word layout of the exact kernel.
-// The sums are in MFMA order, not agent order (within 4*A*2^-53 of the exact consensus);
-// markets whose consensus lies within 8*A*2^-53 of 0.5 -- where the vote could differ --
-// (or whose column holds a finite cell outside [0, 1], where that bound does not hold) are
-// listed for reestimate_fixup_kernel, which redoes them in exact agent order, so the votes
-// and therefore the agreement counts are identical to the exact path.  A column holding a
-// NaN cell sums to NaN in every order (NaN * w is NaN for any w), so it needs no redo.
+// w^T P as v_mfma_f64_16x16x4_f64, fed by the exact kernel's load schedule: lane = market
+// column m0 + lane, one coalesced 512-B row segment per agent, the row's vote ballot IS the
+// agent's vote word (no regrouping).  The lane's own cell is the B operand: lane l = n + 16k
+// holds B[k][n] = P[a][m0 + 16k + n], and A is the agent's weight on a "diagonal" --
+// lane l = i + 16k holds A[i][k] = (i % 4 == k) ? w_a : 0 -- so D[i][n] += w_a * B[i % 4][n]:
+// row i of D accumulates market m0 + 16 (i % 4) + n, one MFMA per agent row of 64 markets,
+// each market's sum in agent order (the MFMA's own rounding of the product; the three zero
+// products are exact).  Accumulator r of lane l then holds D[4 (l >> 4) + r][l & 15], i.e.
+// market m0 + 16 r + (l & 15): lane l's own sum is accumulator l >> 4.  One accumulator
+// chain (the MFMA's dependent issue is hidden by the other waves): 59 VGPRs, 8 waves per
+// SIMD, as many row loads in flight as the exact kernel (kMfmaTwoAcc: even / odd agents on
+// two chains, 80 VGPRs / 6 waves, or 64 with 4 spilled at 8 waves).
+// A zero operand times a NaN / inf cell would leak NaN into the other three markets of the
+// column, so the B operand carries non-finite cells as 0 and the lane keeps its own
+// column's flags: a NaN cell makes the consensus NaN (as in every order), any cell outside
+// [0, 1] (inf included) sends the market to reestimate_fixup_kernel's exact redo.
+// The sums are within 4*A*2^-53 of the exact consensus; markets within 8*A*2^-53 of 0.5 --
+// where the vote could differ -- are redone in exact agent order too, so the votes and
+// therefore the agreement counts are identical to the exact path.
 // Precondition of the error bound and the null test: every weight finite and >= 0.
 // reestimate_total_kernel checks it on the device; if any weight breaks it, the MFMA and
 // fixup kernels exit at once and the exact kernel (launched behind them, gated on the same
 // word) computes the iteration instead -- same results, exact-mode speed.
+// (Rounds 3-4 used A = w broadcast over 16 rows and B = a 4-agent x 16-market block --
+// 128-B row pieces and a 16-bit regrouping of four ballots per word, 25.0-26.0 ms against
+// the exact kernel's 23.2-23.6; round 5's transposed variant of it took 28.7 ms,
+// profiles/r05f/.)
 typedef double mfma_d4 __attribute__((ext_vector_type(4)));
-constexpr int kMfmaSteps = 4;  // 4-agent MFMA steps per loop iteration (16 agents)
+constexpr bool kMfmaTwoAcc = false;  // even / odd agent rows on two accumulator chains
+constexpr int kMfmaRows = 8;         // agent rows per batch (the exact kernel: kVoteRows = 16)
+constexpr bool kMfmaPrefetch = true;
+constexpr int kMfmaWpe = kMfmaPrefetch ? 6 : 8;  // waves per SIMD the VGPR budget allows
 
 __global__ __launch_bounds__(256) void reestimate_total_kernel(const double* __restrict__ w, int64_t A,
                                                                double* __restrict__ total_fast,
@@ -282,85 +318,81 @@ __global__ __launch_bounds__(256) void reestimate_total_kernel(const double* __r
   }
 }
 
-// Round 5 (verdict r04 item 6): fed from the exact kernel's load schedule instead -- lane =
-// market column, 16 rows as coalesced 512-B segments, the vote words straight from the row
-// ballots, each 4-row group regrouped for the B operand by a 4 x 4 transpose of 16-lane
-// groups (two permlane32 and two permlane16 swap levels per 32-bit half) -- the pass took
-// 28.7 ms against this kernel's 26.0 and the exact kernel's 23.2 (same box, profiles/r05f/):
-// 128 VGPRs (4 waves per SIMD) and a transpose per 4 rows for no load-side gain.  A 4-waves-
-// per-SIMD budget for this kernel (106 VGPRs) measured 24.86 vs 24.77 ms (profiles/r05d/).
-// Both are HBM streams of P; the exact agent-order kernel stays the default.
-__global__ __launch_bounds__(256) void reestimate_votes_mfma_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMfmaWpe, kMfmaWpe))) void reestimate_votes_mfma_kernel(
     const double* __restrict__ P, int64_t A, int64_t M, int64_t ld, const double* __restrict__ w,
     const double* __restrict__ total_fast, double* __restrict__ cons, uint8_t* __restrict__ null_out,
     unsigned long long* __restrict__ vote_bits, unsigned long long* __restrict__ cvote_words,
     unsigned long long* __restrict__ ok_words, int32_t* __restrict__ nflag, int32_t* __restrict__ flags) {
   if (nflag[1]) return;  // weights outside [0, inf): the gated exact kernel does this iteration
   const int lane = lane_id();
-  const int64_t k = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;  // vote word = 64 markets
-  const int64_t m0 = k << 6;
-  if (m0 >= M) return;  // wave-uniform
-  const int ka = lane >> 4, n = lane & 15;
-  mfma_d4 acc[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) acc[j] = mfma_d4{0.0, 0.0, 0.0, 0.0};
-  bool inm[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) inm[j] = m0 + 16 * j + n < M;
+  const int64_t m = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t k = m >> 6;
+  if ((k << 6) >= M) return;  // whole wave past the last market (wave-uniform)
+  const bool in = m < M;
+  const bool diag = (lane & 3) == (lane >> 4);  // A[i][k] with i = lane & 15, k = lane >> 4
+  const double* col = P + (in ? m : 0);  // every lane's column address is valid: loads unconditional
   unsigned long long* vb = vote_bits + k * A;
-  bool odd[4] = {false, false, false, false};  // a cell outside [0, 1] (or NaN) in this lane's column
-  bool hnan[4] = {false, false, false, false};  // a NaN cell in this lane's column
-  for (int64_t a = 0; a < A; a += 4 * kMfmaSteps) {
-    double v[kMfmaSteps][4], wa[kMfmaSteps];
+  mfma_d4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+  bool odd = false, hnan = false;
+  const double dsel = diag ? 1.0 : 0.0;  // A = w_a * dsel: w_a or +0 (w finite >= 0)
+  // b = the cell clamped to [0, 1], NaN -> 0 (IEEE maxNum): equal to v exactly for a cell in
+  // [0, 1] (-0.0 compares equal), so b != v marks every other cell, NaN included; and
+  // b >= 0.5 iff v >= 0.5 for every v (the vote)
+  auto row = [&](double v, double wq, mfma_d4& acc) {
+    const double b = __builtin_fmin(__builtin_fmax(v, 0.0), 1.0);
+    odd = odd || (b != v);
+    hnan = hnan || (v != v);
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(wq * dsel, b, acc, 0, 0, 0);
+  };
+  int64_t a = 0;
+  // kMfmaPrefetch: the next batch's rows are issued before this batch's MFMA chain (whose
+  // dependent issue would otherwise hold back the next loads)
+  double v[kMfmaRows];
+  if (kMfmaPrefetch && kMfmaRows <= A) {
 #pragma unroll
-    for (int q = 0; q < kMfmaSteps; ++q) {
-      const int64_t ag = a + 4 * q + ka;
-      const bool ain = ag < A;
-      wa[q] = ain ? w[ag] : 0.0;
+    for (int q = 0; q < kMfmaRows; ++q) v[q] = col[q * ld];
+  }
+  for (; a + kMfmaRows <= A; a += kMfmaRows) {
+    double vn[kMfmaRows];
+    if (kMfmaPrefetch) {
+      if (a + 2 * kMfmaRows <= A) {  // wave-uniform
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[q][j] = (ain && inm[j]) ? P[ag * ld + m0 + 16 * j + n] : 0.0;
-    }
-#pragma unroll
-    for (int q = 0; q < kMfmaSteps; ++q) {
-      unsigned long long bal[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(wa[q], v[q][j], acc[j], 0, 0, 0);
-        odd[j] = odd[j] || !(v[q][j] >= 0.0 && v[q][j] <= 1.0);
-        hnan[j] = hnan[j] || (v[q][j] != v[q][j]);
-        bal[j] = ballot(a + 4 * q + ka < A && inm[j] && v[q][j] >= 0.5);  // market.py:298-299
+        for (int q = 0; q < kMfmaRows; ++q) vn[q] = col[(a + kMfmaRows + q) * ld];
       }
-      // agent a + 4q + lane's vote word (lanes 0..3): its 16-bit slice of every ballot
-      unsigned long long word = 0;
+    } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) word |= ((bal[j] >> (16 * (lane & 3))) & 0xFFFFull) << (16 * j);
-      if (lane < 4 && a + 4 * q + lane < A) vb[a + 4 * q + lane] = word;
+      for (int q = 0; q < kMfmaRows; ++q) v[q] = col[(a + q) * ld];  // lanes past M: column 0 (b clamped)
+    }
+    const double wl = kVoteWLane ? w[a + (lane & (kMfmaRows - 1))] : 0.0;
+    unsigned long long mine = 0;
+#pragma unroll
+    for (int q = 0; q < kMfmaRows; ++q) {
+      row(v[q], kVoteWLane ? readlane_f64(wl, q) : w[a + q], (kMfmaTwoAcc && (q & 1)) ? acc1 : acc0);
+      mine = writelane_u64(ballot(in && v[q] >= 0.5), q, mine);  // market.py:298-299
+    }
+    if (lane < kMfmaRows) vb[a + lane] = mine;
+    if (kMfmaPrefetch) {
+#pragma unroll
+      for (int q = 0; q < kMfmaRows; ++q) v[q] = vn[q];
     }
   }
-  // lane L = 16j + n' holds market m0 + L's sum in acc[j] (every row of D is the same)
-  const int jj = lane >> 4;
-  const double ws = (jj == 0) ? acc[0][0] : (jj == 1) ? acc[1][0] : (jj == 2) ? acc[2][0] : acc[3][0];
-  const int64_t m = m0 + lane;
-  const bool in = m < M;
+  for (; a < A; ++a) {
+    const double v = in ? col[a * ld] : 0.0;
+    row(v, w[a], acc0);
+    const unsigned long long bq = ballot(in && v >= 0.5);
+    if (lane == 0) vb[a] = bq;
+  }
+  const int r = lane >> 4;
+  const double s0 = (r == 0) ? acc0[0] : (r == 1) ? acc0[1] : (r == 2) ? acc0[2] : acc0[3];
+  const double s1 = !kMfmaTwoAcc ? 0.0 : (r == 0) ? acc1[0] : (r == 1) ? acc1[1] : (r == 2) ? acc1[2] : acc1[3];
   const double total = *total_fast;
   const bool isnull = (total == 0.0);  // w >= 0: zero in every order iff every weight is zero
-  const double c = isnull ? 0.0 : ws / total;
+  const double c = isnull ? 0.0 : hnan ? __builtin_nan("") : (kMfmaTwoAcc ? s0 + s1 : s0) / total;
   // |fast - exact| <= ~4*A*2^-53 for cells in [0, 1] (both sums of non-negative terms within
-  // A*2^-53 relative of the true one, c <= 1); a column holding another finite value is
-  // always redone, a column holding a NaN never (NaN in every order)
-  unsigned long long oddm = 0, nanm = 0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    unsigned long long b = ballot(odd[j]);
-    b |= (b >> 16) | (b >> 32) | (b >> 48);
-    oddm |= (b & 0xFFFFull) << (16 * j);
-    unsigned long long q = ballot(hnan[j]);
-    q |= (q >> 16) | (q >> 32) | (q >> 48);
-    nanm |= (q & 0xFFFFull) << (16 * j);
-  }
+  // A*2^-53 relative of the true one, c <= 1); a column holding another value is redone,
+  // a column holding a NaN never (NaN in every order)
   const double bound = 8.0 * (double)(A + 2) * 0x1p-53;
-  const bool colnan = (nanm >> lane) & 1ull;
-  const bool near = in && !isnull && !colnan && (fabs(c - 0.5) <= bound || ((oddm >> lane) & 1ull));
+  const bool near = in && !isnull && !hnan && (fabs(c - 0.5) <= bound || odd);
   if (in) {
     cons[m] = c;
     null_out[m] = isnull ? 1 : 0;

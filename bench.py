@@ -66,10 +66,10 @@ def parse(argv=None):
     p.add_argument("--tb-contiguous", action="store_true",
                    help="tb: contiguous tiles only (no length-bucket plan), the A/B for batch.tiebreak_plan")
     p.add_argument("--sources", type=int, default=10_000)
-    p.add_argument("--mode", default=None, choices=["exact", "fast"],
+    p.add_argument("--mode", default=None, choices=["exact", "fast", "mfma"],
                    help="consensus summation mode (default: exact for c2, where it costs nothing; fast -- "
                         "the north star's fixed-order trees within 1e-9 -- for c3, with the exact-mode "
-                        "time reported beside it)")
+                        "time reported beside it); c5 only: mfma = the matrix-core pass 1")
     p.add_argument("--c3-sources", type=int, default=1_000_000,
                    help="c3: Zipf source universe (SURVEY d3: 1M; 2M / 10M = the large-table lines)")
     p.add_argument("--agents", type=int, default=16384, help="config 5 agents")
@@ -495,6 +495,8 @@ def bench_stub(args, world, rank):
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
+    if args.mode == "mfma" and args.config != "c5":
+        raise SystemExit("bench.py: --mode mfma is the config-5 matrix-core pass (--config c5)")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args, argv))
     world, rank, _ = dist_setup(args)

@@ -495,10 +495,13 @@ def _c5(args, world, rank, barrier, max_over, sum_over):
     ev_k = []
     nb = int(L.bce_reestimate_mfma_scratch_bytes(Mloc))
     scratch = torch.empty((nb + 7) // 8, dtype=torch.int64, device=dev)
+    # "fast" runs the exact kernel (batch.reestimate: it streams P at the HBM rate, the
+    # matrix-core form measured slower); "mfma" = w^T P on the matrix cores, timed beside
+    # the main mode for the MFMA utilisation report
     mode = {"m": args.mode or "exact"}
 
     def pass1():
-        if mode["m"] == "fast":  # w^T P on the matrix cores (near-0.5 markets redone exactly)
+        if mode["m"] == "mfma":  # w^T P on the matrix cores (near-0.5 markets redone exactly)
             N.check(L.bce_reestimate_consensus_votes_mfma(N.ptr(P), A, Mloc, ld, N.ptr(w), N.ptr(cons), N.ptr(nul),
                                                           N.ptr(votes), N.ptr(words[0]), N.ptr(words[1]),
                                                           N.ptr(scratch), scratch.numel() * 8, st), "c5 p1 mfma")
@@ -525,9 +528,10 @@ def _c5(args, world, rank, barrier, max_over, sum_over):
     # the other pass-1 mode, same loop on fewer steps, from the same starting weights
     import copy
     main_mode = mode["m"]
-    other, kern2 = {"mode": "exact" if main_mode == "fast" else "fast", "skipped": "--single-mode"}, None
+    other_m = "exact" if main_mode == "mfma" else "mfma"
+    other, kern2 = {"mode": other_m, "skipped": "--single-mode"}, None
     if not getattr(args, "single_mode", False):
-        mode["m"] = "exact" if main_mode == "fast" else "fast"
+        mode["m"] = other_m
         w.copy_(w_init)
         a2 = copy.copy(args)
         a2.steps, a2.warmup, a2.prewarm_s = max(2, args.steps // 2), 1, 0.0
@@ -536,14 +540,14 @@ def _c5(args, world, rank, barrier, max_over, sum_over):
         kern2 = float(np.mean([a.elapsed_time(b) for a, b in ev_k[-a2.steps:]])) / 1e3
         other = {"mode": mode["m"], "ms_per_step": wall2 / a2.steps * 1e3, "avg_launch_ms": kern2 * 1e3,
                  "frac": (8 * A * Mloc + 16 * A + 9 * Mloc) / kern2 / 1e9 / HBM_PEAK_GBS,
-                 "traffic": _pmc("pmc_c5_fast.json" if mode["m"] == "fast" else "pmc_c5.json",
+                 "traffic": _pmc("pmc_c5_mfma.json" if mode["m"] == "mfma" else "pmc_c5.json",
                                  markets_this_rank=Mloc)}
         mode["m"] = main_mode
-    t_fast = kern if main_mode == "fast" else (kern2 or float("nan"))
+    t_mfma = kern if main_mode == "mfma" else (kern2 or float("nan"))
     parity = None
     if rank == 0 and world == 1 and not args.no_parity and not args.no_cpu_baseline:
         parity = _parity_c5(P, L, N, st, args)
-        parity["fast_mode_votes"] = _parity_c5_fast(P, L, N, st)
+        parity["mfma_mode_votes"] = _parity_c5_mfma(P, L, N, st)
     # algorithmic: P once, w, agreement counts, consensus + null out (the vote bits, A*M/8
     # written and read back, are this implementation's intermediate -- in `traffic`)
     bytes_iter = 8 * A * Mloc + 16 * A + 9 * Mloc
@@ -560,26 +564,29 @@ def _c5(args, world, rank, barrier, max_over, sum_over):
                    "markets_this_rank": Mloc,
                    "parallelism": f"markets sharded by column over {world} rank(s); per-agent counts all-reduced"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc("pmc_c5_fast.json" if main_mode == "fast" else "pmc_c5.json",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc("pmc_c5_mfma.json" if main_mode == "mfma" else "pmc_c5.json",
                                                   markets_this_rank=Mloc),
                      "kernel": "reestimate_consensus_votes + reestimate_agreement_votes (one iteration)",
                      "bytes_per_launch": bytes_iter, "avg_launch_ms": kern * 1e3,
                      f"{other['mode']}_mode": other,
-                     "mfma": {"used": "fast mode pass 1 (v_mfma_f64_16x16x4_f64)", "mode_of_this_line": main_mode,
-                              "fast_ms_per_iteration": t_fast * 1e3,
-                              "contraction_tflops_fast": 2.0 * A * Mloc / t_fast / 1e12,
+                     "mfma": {"used": "mode='mfma' pass 1 (v_mfma_f64_16x16x4_f64, one agent row of 64 "
+                                      "markets per MFMA on a diagonal A operand)",
+                              "mode_of_this_line": main_mode,
+                              "mfma_ms_per_iteration": t_mfma * 1e3,
+                              "contraction_tflops_mfma": 2.0 * A * Mloc / t_mfma / 1e12,
                               "fp64_matrix_peak_tflops": 78.6,
-                              "utilisation_useful": 2.0 * A * Mloc / t_fast / 1e12 / 78.6,
-                              "utilisation_issued": 32.0 * A * Mloc / t_fast / 1e12 / 78.6,
-                              "why": "w^T P is a GEMV at 0.25 flop/B: both modes run at the HBM rate; the MFMA "
-                                     "form issues 16x the useful flops (15 of 16 rows of D are redundant) and "
-                                     "exact agent-order sums stay the default"}},
+                              "utilisation_useful": 2.0 * A * Mloc / t_mfma / 1e12 / 78.6,
+                              "utilisation_issued": 32.0 * A * Mloc / t_mfma / 1e12 / 78.6,
+                              "why": "w^T P is a GEMV at 0.25 flop/B: both forms stream P at the HBM rate; the "
+                                     "MFMA form issues 16x the useful flops (3 of 4 products per D element are "
+                                     "zeros, every D row 4x redundant) and measured slower, so mode='fast' runs "
+                                     "the exact agent-order kernel"}},
         "cpu_baseline": _cpu_c5(P, args) if rank == 0 and world == 1 else None,
         "parity_vs_oracle": parity,
     }
 
 
-def _parity_c5_fast(P, L, N, st, m=65536):
+def _parity_c5_mfma(P, L, N, st, m=65536):
     """The MFMA pass 1 against the exact one on the first m market columns (from w = 0.5 and
     from a random weight vector): vote bits, consensus votes, resolved masks, null flags and
     agreement counts identical; consensus within 4*A*2^-53."""

@@ -284,8 +284,10 @@ int bce_reestimate_consensus_votes(const double* P, int64_t A, int64_t M, int64_
 int bce_reestimate_agreement_votes(const uint64_t* vote_bits, int64_t A, int64_t M, const uint64_t* cvote_words,
                                    const uint64_t* ok_words, int64_t* agreement, int64_t* resolved,
                                    void* stream);
-/* BCE_MODE_FAST pass 1 of the single-read iteration on the matrix cores: w^T P with
- * v_mfma_f64_16x16x4_f64 (the north star's "MFMA contraction"), same outputs as
+/* Pass 1 of the single-read iteration on the matrix cores: w^T P with
+ * v_mfma_f64_16x16x4_f64 (the north star's "MFMA contraction"; batch.reestimate
+ * mode="mfma" -- mode="fast" runs bce_reestimate_consensus_votes, which streams P at the same
+ * HBM rate and measured faster), same outputs as
  * bce_reestimate_consensus_votes.  consensus within 4*A*2^-53 of the agent-order value;
  * markets within 8*A*2^-53 of 0.5 (or with a finite cell outside [0, 1]) are redone in agent
  * order, so vote_bits / cvote_words / ok_words -- and the agreement counts -- are identical

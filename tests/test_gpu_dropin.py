@@ -337,11 +337,14 @@ def test_reestimate_vs_oracle_tiles(A, M, ld_pad):
     full = np.zeros((A, M + ld_pad))
     full[:, :M] = P
     Pt = torch.from_numpy(full).cuda()[:, :M]
-    w, cons, nul, agree, _ = batch.reestimate(Pt, K)
-    assert np.array_equal(cons.cpu().numpy(), c_exp[-1])
-    assert np.array_equal(nul.cpu().numpy(), n_exp[-1])
-    assert np.array_equal(agree.cpu().numpy(), a_exp[-1])
-    assert np.array_equal(w.cpu().numpy(), w_exp)
+    for mode in ("exact", "fast"):  # fast runs the exact agent-order kernel: bit-identical
+        w, cons, nul, agree, _ = batch.reestimate(Pt, K, mode=mode)
+        assert np.array_equal(cons.cpu().numpy(), c_exp[-1]), mode
+        assert np.array_equal(nul.cpu().numpy(), n_exp[-1]), mode
+        assert np.array_equal(agree.cpu().numpy(), a_exp[-1]), mode
+        assert np.array_equal(w.cpu().numpy(), w_exp), mode
+    with pytest.raises(ValueError):
+        batch.reestimate(Pt, 1, mode="tree")
 
 
 @pytest.mark.parametrize("A,M", [(13, 1), (64, 63), (9, 129), (300, 4097), (13, 2), (64, 64), (9, 130), (300, 4096), (17, 190)])
@@ -584,7 +587,7 @@ def test_tiebreak_variance_bit_exact_1m_markets():
 
 @pytest.mark.parametrize("A,M", [(5, 70), (17, 190), (300, 4097), (4100, 1000)])
 def test_reestimate_mfma_fast_mode_matches_exact_votes(A, M):
-    """BCE_MODE_FAST pass 1 on the matrix cores (bce_reestimate_consensus_votes_mfma):
+    """mode="mfma" pass 1 on the matrix cores (bce_reestimate_consensus_votes_mfma):
     consensus within 4*A*2^-53 of the agent-order value (<= 1e-9), and -- because markets
     within 8*A*2^-53 of 0.5 (or with NaN cells) are redone in agent order -- vote bits, consensus votes,
     resolved masks, null flags and agreement counts identical to the exact pass.  Columns
@@ -711,14 +714,14 @@ def test_reestimate_mfma_nan_cells_match_exact_without_redo_cliff():
     assert np.array_equal(np.isnan(cf), np.isnan(ce)) and np.isnan(ce).all()
     from bayesian_engine import batch
     times = {}
-    for mode in ("exact", "fast"):
+    for mode in ("exact", "mfma"):
         batch.reestimate(Pt, 1, mode=mode)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         batch.reestimate(Pt, 3, mode=mode)
         torch.cuda.synchronize()
         times[mode] = time.perf_counter() - t0
-    assert times["fast"] <= 2.0 * times["exact"], times
+    assert times["mfma"] <= 2.0 * times["exact"], times
 
 
 def test_reestimate_mfma_out_of_range_cells_redone_exactly():

@@ -52,6 +52,10 @@ VARIANTS = {
     "tbwr16": [("tiebreak.hip", "constexpr int kTbFullBatchWR = 8;", "constexpr int kTbFullBatchWR = 16;")],
     "tbpc16wr16": [("tiebreak.hip", "constexpr int kTbFullBatchWR = 8;", "constexpr int kTbFullBatchWR = 16;"),
                    ("tiebreak.hip", "constexpr int kTbFullBatchPC = 8;", "constexpr int kTbFullBatchPC = 16;")],
+    # C5 MFMA pass: two accumulator chains / no next-batch prefetch (8 waves per SIMD)
+    # (shipped: one chain, 8-row batches, the next batch issued before the chain, 6 waves)
+    "c5acc2": [("stats.hip", "constexpr bool kMfmaTwoAcc = false;", "constexpr bool kMfmaTwoAcc = true;")],
+    "c5nopf": [("stats.hip", "constexpr bool kMfmaPrefetch = true;", "constexpr bool kMfmaPrefetch = false;")],
     "wdiv": [("consensus_wide.hip", "constexpr bool kWideFastRecip = true;", "constexpr bool kWideFastRecip = false;")],
     # namespace pass without its nontemporal hints (0.1752 vs 0.1665 ms, r04t)
     "nsnont": [("elementwise.hip", "constexpr bool kNsNtLoad = true;", "constexpr bool kNsNtLoad = false;"),
