@@ -54,6 +54,9 @@ __device__ __forceinline__ double key_f64(uint64_t k) {
 // of LDS allows: 0.0860 vs 0.0943 ms (+median 0.173 vs 0.193, profiles/r04w/).  Dropping the
 // cons*conf LDS array so more groups fit (the product formed in the chain) ran 2x slower
 // (0.19-0.22 ms, profiles/r04v/; code reverted): the chains' loop is the critical path.
+// Round 5: the last chunk's chains moved after the chunk loop (its next-chunk registers dead)
+// as 4-term 16-B LDS batches with the next batch read during the adds ran 0.117 vs 0.0858 ms
+// (profiles/r05o/; 8- or 16-term batches there spilled 35 / 71 VGPRs); reverted.
 constexpr int kAggWpe = 6;
 constexpr int kAggT = 256;
 constexpr int kAggPer = 4;                  // members per thread per chunk
