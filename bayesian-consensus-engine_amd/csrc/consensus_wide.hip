@@ -40,6 +40,8 @@
 constexpr int kWideHR = 1;       // rounds of NT uniques whose gathers are in flight together (2: C3 fast +6%)
 constexpr int kWideWPE = 4;      // min waves per SIMD (register budget; 4 vs 2: exact -1.3%, fast unchanged)
 constexpr int kWideNWBF = 4;     // FAST nweight read-backs per batch (1: 1.645, 2: 1.634, 4: 1.587 ms C3)
+constexpr bool kWideChainDeep = true;  // EXACT piped chain wave: chain_add_deep (16-term steps)
+constexpr bool kWideChain3 = true;     // EXACT chains run on lanes 0..2 only (exec = 3 lanes)
 
 namespace bce {
 namespace {
@@ -482,6 +484,17 @@ __device__ __forceinline__ double run_sum(const double* sA, int q0, int len) {
 // other's dependent adds (the compiler would copy loop-carried batch registers behind an
 // lgkmcnt(0)).  The < 8-term tail is added in C++ with masked terms adding +0.0 -- exact,
 // because these chains never hold -0.0.  src is 16-B aligned; reads may run 8 past ce.
+// chain_add_deep: the piped EXACT path's dedicated chain wave reads further ahead (16-term
+// steps over four 4-term batches, 12 terms ahead of the adds instead of 4; 32 fixed VGPRs);
+// reads may run 16 past ce (the chain ring holds 6 (NT - NP) = 384 doubles of slack past its
+// last chain).
+__device__ __forceinline__ void chain_tail(double& acc, const double* src, int from, int ce) {
+  double xt[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) xt[e] = src[from + e];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc += (from + e < ce) ? xt[e] : 0.0;
+}
 __device__ __forceinline__ void chain_add(double& acc, const double* src, int ce) {
   const int nfull = ce & ~7;
   if (nfull) {
@@ -519,13 +532,65 @@ __device__ __forceinline__ void chain_add(double& acc, const double* src, int ce
         : "memory", "scc", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121",
           "v122", "v123", "v124", "v125", "v126", "v127");
   }
-  if (nfull < ce) {
-    double xt[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) xt[e] = src[nfull + e];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) acc += (nfull + e < ce) ? xt[e] : 0.0;
+  if (nfull < ce) chain_tail(acc, src, nfull, ce);
+}
+// (four 4-term batches in fixed registers v[96, 127], each reloaded 16 terms ahead right after
+// its adds; six batches -- 24-term steps, 48 fixed VGPRs -- spilled 22 VGPRs in the 8-wave
+// kernel and ran C3 exact 2.00 vs 1.90 ms, profiles/r05r/)
+__device__ __forceinline__ void chain_add_deep(double& acc, const double* src, int ce) {
+  const int steps = ce / 16;
+  const int nfull = steps * 16;
+  if (steps) {
+    unsigned addr = (unsigned)(uintptr_t)src;
+    int st = steps;
+    asm volatile(
+        "ds_read_b128 v[96:99], %[ad] offset:0\n"
+        "ds_read_b128 v[100:103], %[ad] offset:16\n"
+        "ds_read_b128 v[104:107], %[ad] offset:32\n"
+        "ds_read_b128 v[108:111], %[ad] offset:48\n"
+        "ds_read_b128 v[112:115], %[ad] offset:64\n"
+        "ds_read_b128 v[116:119], %[ad] offset:80\n"
+        "ds_read_b128 v[120:123], %[ad] offset:96\n"
+        "ds_read_b128 v[124:127], %[ad] offset:112\n"
+        "1:\n"
+        "s_waitcnt lgkmcnt(6)\n"
+        "v_add_f64 %[acc], %[acc], v[96:97]\n"
+        "v_add_f64 %[acc], %[acc], v[98:99]\n"
+        "v_add_f64 %[acc], %[acc], v[100:101]\n"
+        "v_add_f64 %[acc], %[acc], v[102:103]\n"
+        "ds_read_b128 v[96:99], %[ad] offset:128\n"
+        "ds_read_b128 v[100:103], %[ad] offset:144\n"
+        "s_waitcnt lgkmcnt(6)\n"
+        "v_add_f64 %[acc], %[acc], v[104:105]\n"
+        "v_add_f64 %[acc], %[acc], v[106:107]\n"
+        "v_add_f64 %[acc], %[acc], v[108:109]\n"
+        "v_add_f64 %[acc], %[acc], v[110:111]\n"
+        "ds_read_b128 v[104:107], %[ad] offset:160\n"
+        "ds_read_b128 v[108:111], %[ad] offset:176\n"
+        "s_waitcnt lgkmcnt(6)\n"
+        "v_add_f64 %[acc], %[acc], v[112:113]\n"
+        "v_add_f64 %[acc], %[acc], v[114:115]\n"
+        "v_add_f64 %[acc], %[acc], v[116:117]\n"
+        "v_add_f64 %[acc], %[acc], v[118:119]\n"
+        "ds_read_b128 v[112:115], %[ad] offset:192\n"
+        "ds_read_b128 v[116:119], %[ad] offset:208\n"
+        "s_waitcnt lgkmcnt(6)\n"
+        "v_add_f64 %[acc], %[acc], v[120:121]\n"
+        "v_add_f64 %[acc], %[acc], v[122:123]\n"
+        "v_add_f64 %[acc], %[acc], v[124:125]\n"
+        "v_add_f64 %[acc], %[acc], v[126:127]\n"
+        "ds_read_b128 v[120:123], %[ad] offset:224\n"
+        "ds_read_b128 v[124:127], %[ad] offset:240\n"
+        "v_add_u32 %[ad], 128, %[ad]\n"
+        "s_sub_u32 %[st], %[st], 1\n"
+        "s_cmp_lg_u32 %[st], 0\n"
+        "s_cbranch_scc1 1b\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        : [acc] "+v"(acc), [ad] "+v"(addr), [st] "+s"(st)
+        :
+        : "memory", "scc", "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123", "v124", "v125", "v126", "v127");
   }
+  for (int from = nfull; from < ce; from += 8) chain_tail(acc, src, from, ce);
 }
 
 // LDS of one market's workgroup of NW waves, carved from a byte buffer.
@@ -721,7 +786,10 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
           __builtin_amdgcn_s_sleep(1);
         }
         const int ce = (u - r * NP < NP) ? u - r * NP : NP;
-        chain_add(acc, sWAC + slot * 3 * NP + (lane % 3) * NP, ce);
+        if (!kWideChain3 || lane < 3) {  // kWideChain3: only the three chain lanes read LDS
+          if constexpr (kWideChainDeep) chain_add_deep(acc, sWAC + slot * 3 * NP + (lane % 3) * NP, ce);
+          else chain_add(acc, sWAC + slot * 3 * NP + (lane % 3) * NP, ce);
+        }
         if (lane == 0) __hip_atomic_store(L.sDone, r + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       __builtin_amdgcn_s_setprio(0);
@@ -881,7 +949,7 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
           if (wv == 0) {
             __builtin_amdgcn_s_setprio(2);  // the chain is the critical path
             const int ce = (u - (h + i) * NT < NT) ? u - (h + i) * NT : NT;
-            chain_add(acc, buf + (lane % 3) * NT, ce);
+            if (!kWideChain3 || lane < 3) chain_add(acc, buf + (lane % 3) * NT, ce);
             __builtin_amdgcn_s_setprio(0);
           }
         }

@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round 5: C3 EXACT -- the piped chain wave on chain_add_deep (16-term steps, reads 12 terms
+# ahead) on lanes 0..2 only (shipped) vs every lane of the chain wave (chain64) vs the 8-term
+# chain_add (nodeep); wide / consensus GPU tests first.
+set -u
+o=gpurun_out/r05q
+mkdir -p $o
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_wide.py tests/test_gpu_consensus.py \
+  > $o/pytest.txt 2>&1 || exit $?
+for rep in 1 2; do
+  for v in ship chain64 nodeep; do
+    if [ $v = ship ]; then unset BCE_LIB; else export BCE_LIB=tools/bin/variants/$v/libbce_hip.so; fi
+    echo "[r05q] $(date +%T) $v rep $rep" >&2
+    timeout -k 10 300 python3 bench.py --config c3 --mode exact --single-mode --no-cpu-baseline --no-parity --steps 20 --warmup 3 \
+      > $o/c3x_${v}_$rep.json 2> $o/c3x_${v}_$rep.err || exit $?
+  done
+done
+unset BCE_LIB
+timeout -k 10 300 python3 bench.py --config c3 --mode exact --single-mode --steps 10 --warmup 2 > $o/c3x_parity.json 2> $o/c3x_parity.err

@@ -56,6 +56,10 @@ VARIANTS = {
     # (shipped: one chain, 8-row batches, the next batch issued before the chain, 6 waves)
     "c5acc2": [("stats.hip", "constexpr bool kMfmaTwoAcc = false;", "constexpr bool kMfmaTwoAcc = true;")],
     "c5nopf": [("stats.hip", "constexpr bool kMfmaPrefetch = true;", "constexpr bool kMfmaPrefetch = false;")],
+    # EXACT piped chain wave with the 8-term chain_add (shipped: chain_add_deep, 16-term steps)
+    "nodeep": [("consensus_wide.hip", "constexpr bool kWideChainDeep = true;", "constexpr bool kWideChainDeep = false;")],
+    # EXACT chains on every lane of the chain wave (lane % 3 picks the chain; shipped: lanes 0..2)
+    "chain64": [("consensus_wide.hip", "constexpr bool kWideChain3 = true;", "constexpr bool kWideChain3 = false;")],
     "wdiv": [("consensus_wide.hip", "constexpr bool kWideFastRecip = true;", "constexpr bool kWideFastRecip = false;")],
     # namespace pass without its nontemporal hints (0.1752 vs 0.1665 ms, r04t)
     "nsnont": [("elementwise.hip", "constexpr bool kNsNtLoad = true;", "constexpr bool kNsNtLoad = false;"),
