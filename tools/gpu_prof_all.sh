@@ -5,6 +5,8 @@
 # the c3 line's other-mode steps), so the C3 figure is per step; stream_read_bytes = the
 # streamed (coalesced) read bytes per step, whose FETCH_SIZE alone is doubled -- the table
 # gathers are counted in full (profiles/archive/r03_fetch_calib.txt).
+# The raw rocprof CSVs (> 512 KB) are deleted on the box at the end: gpurun copies back at most
+# 64 MiB of gpurun_out/.
 set -u
 bash tools/gpu_profile.sh c2 consensus_tab32_kernel markets=1000000 signals_per_market=32 sources=10000 kernel=consensus_tab32_kernel -- --no-secondary && \
 bash tools/gpu_profile.sh c4 replay_step_kernel sources_this_rank=10000000 -- --config c4 && \
@@ -19,4 +21,5 @@ python3 tools/pmc_summary.py pmc gpurun_out/prof_c5/fetch gpurun_out/prof_c5/wri
 bash tools/gpu_profile.sh c5mfma reestimate_votes_mfma_kernel markets_this_rank=1000000 mode=mfma -- --config c5 --mode mfma --steps 2 --warmup 1 --single-mode && \
 bash tools/gpu_profile.sh ns namespace_resolve_kernel sources=10000000 -- --config ns && \
 bash tools/gpu_profile.sh agg aggregate_kernel groups=10000 -- --config agg --single-mode && \
-python3 tools/roofline_check.py gpurun_out > gpurun_out/roofline_check.txt
+python3 tools/roofline_check.py gpurun_out > gpurun_out/roofline_check.txt && \
+find gpurun_out -path 'gpurun_out/prof_*' -name 'run_*.csv' -size +512k -delete
