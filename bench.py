@@ -83,6 +83,8 @@ def parse(argv=None):
     p.add_argument("--cpu-seconds", type=float, default=2.0, help="wall-clock budget of the CPU baseline")
     p.add_argument("--no-parity", action="store_true")
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
+    p.add_argument("--shard-only", action="store_true",
+                   help="with --shard: time the shard(s) only, not the full batch (kernel traces)")
     p.add_argument("--shard", default=None,
                    help="c3 only: R/N or all/N -- time rank R's (or every rank's) market shard of an N-rank "
                         "run in this one process, no process group (predicted strong scaling)")

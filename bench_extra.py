@@ -935,12 +935,12 @@ def c3_shards(args):
     for r in ranks:
         shards.append(time_one(world, r))
         print(f"[c3 shards] {r}/{world}: {shards[-1]['kernel_ms']:.4f} ms", file=sys.stderr, flush=True)
-    full = time_one(1, 0)
+    full = None if getattr(args, "shard_only", False) else time_one(1, 0)
     ms = [s["kernel_ms"] for s in shards]
     out = {"metric": "c3 per-shard step time (predicted strong scaling)", "mode": mode, "world": world,
            "shards": shards, "full_batch": full,
            "max_ms": max(ms), "mean_ms": float(np.mean(ms)), "max_over_mean": max(ms) / float(np.mean(ms)),
-           "predicted_efficiency": full["kernel_ms"] / (world * max(ms)) if spec[0] == "all" else None,
+           "predicted_efficiency": full["kernel_ms"] / (world * max(ms)) if spec[0] == "all" and full else None,
            "split": "sharding.shard_markets (equal signal counts)"}
     return out
 
