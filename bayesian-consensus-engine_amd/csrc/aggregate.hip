@@ -54,13 +54,77 @@ __device__ __forceinline__ double key_f64(uint64_t k) {
 // of LDS allows: 0.0860 vs 0.0943 ms (+median 0.173 vs 0.193, profiles/r04w/).  Dropping the
 // cons*conf LDS array so more groups fit (the product formed in the chain) ran 2x slower
 // (0.19-0.22 ms, profiles/r04v/; code reverted): the chains' loop is the critical path.
-// Round 5: the last chunk's chains moved after the chunk loop (its next-chunk registers dead)
-// as 4-term 16-B LDS batches with the next batch read during the adds ran 0.117 vs 0.0858 ms
-// (profiles/r05o/; 8- or 16-term batches there spilled 35 / 71 VGPRs); reverted.
+// Round 5: the same pipelining in C++ (4-term batches, the next read during the adds) ran 0.117
+// vs 0.0858 ms (profiles/r05o/; the compiler waited on every batch, 8- or 16-term batches
+// spilled 35 / 71 VGPRs) -- hence the asm chain below.
 constexpr int kAggWpe = 6;
+// The last chunk's ordered chains (kAggChainAsm): acc += src[0..ce) left to right in asm, four
+// 4-term batches in fixed registers v[48:79] (inside the 80-VGPR budget), each reloaded 16 terms
+// ahead right after its adds -- the compiler's own loop waits on every batch (it copies the
+// loop-carried batch behind an lgkmcnt(0)).  Run after the chunk loop, where the next chunk's
+// gather registers are dead; reads may run 16 past ce (inside the kernel's LDS).  f4 line:
+// 0.0723 ms against 0.0858 without it, 0.0764 with two batches, 0.0728 with six
+// (profiles/r05za/, r05zb/).
+constexpr bool kAggChainAsm = true;
+__device__ __forceinline__ void agg_chain_asm(double& acc, const double* src, int ce) {
+  const int steps = ce / 16;
+  const int nfull = steps * 16;
+  if (steps) {
+    unsigned addr = (unsigned)(uintptr_t)src;
+    int st = steps;
+    asm volatile(
+        "ds_read_b128 v[48:51], %[ad] offset:0\n"
+        "ds_read_b128 v[52:55], %[ad] offset:16\n"
+        "ds_read_b128 v[56:59], %[ad] offset:32\n"
+        "ds_read_b128 v[60:63], %[ad] offset:48\n"
+        "ds_read_b128 v[64:67], %[ad] offset:64\n"
+        "ds_read_b128 v[68:71], %[ad] offset:80\n"
+        "ds_read_b128 v[72:75], %[ad] offset:96\n"
+        "ds_read_b128 v[76:79], %[ad] offset:112\n"
+        "1:\n"
+        "s_waitcnt lgkmcnt(6)\n"
+        "v_add_f64 %[acc], %[acc], v[48:49]\n"
+        "v_add_f64 %[acc], %[acc], v[50:51]\n"
+        "v_add_f64 %[acc], %[acc], v[52:53]\n"
+        "v_add_f64 %[acc], %[acc], v[54:55]\n"
+        "ds_read_b128 v[48:51], %[ad] offset:128\n"
+        "ds_read_b128 v[52:55], %[ad] offset:144\n"
+        "s_waitcnt lgkmcnt(6)\n"
+        "v_add_f64 %[acc], %[acc], v[56:57]\n"
+        "v_add_f64 %[acc], %[acc], v[58:59]\n"
+        "v_add_f64 %[acc], %[acc], v[60:61]\n"
+        "v_add_f64 %[acc], %[acc], v[62:63]\n"
+        "ds_read_b128 v[56:59], %[ad] offset:160\n"
+        "ds_read_b128 v[60:63], %[ad] offset:176\n"
+        "s_waitcnt lgkmcnt(6)\n"
+        "v_add_f64 %[acc], %[acc], v[64:65]\n"
+        "v_add_f64 %[acc], %[acc], v[66:67]\n"
+        "v_add_f64 %[acc], %[acc], v[68:69]\n"
+        "v_add_f64 %[acc], %[acc], v[70:71]\n"
+        "ds_read_b128 v[64:67], %[ad] offset:192\n"
+        "ds_read_b128 v[68:71], %[ad] offset:208\n"
+        "s_waitcnt lgkmcnt(6)\n"
+        "v_add_f64 %[acc], %[acc], v[72:73]\n"
+        "v_add_f64 %[acc], %[acc], v[74:75]\n"
+        "v_add_f64 %[acc], %[acc], v[76:77]\n"
+        "v_add_f64 %[acc], %[acc], v[78:79]\n"
+        "ds_read_b128 v[72:75], %[ad] offset:224\n"
+        "ds_read_b128 v[76:79], %[ad] offset:240\n"
+        "v_add_u32 %[ad], 128, %[ad]\n"
+        "s_sub_u32 %[st], %[st], 1\n"
+        "s_cmp_lg_u32 %[st], 0\n"
+        "s_cbranch_scc1 1b\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        : [acc] "+v"(acc), [ad] "+v"(addr), [st] "+s"(st)
+        :
+        : "memory", "scc", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63", "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73", "v74", "v75", "v76", "v77", "v78", "v79");
+  }
+  for (int j = nfull; j < ce; ++j) acc = acc + src[j];
+}
 constexpr int kAggT = 256;
 constexpr int kAggPer = 4;                  // members per thread per chunk
 constexpr int kAggCh = kAggT * kAggPer;     // chunk = 1024 members, list order r-major
+
 
 __global__ __launch_bounds__(kAggT) __attribute__((amdgpu_waves_per_eu(kAggWpe, 8))) void aggregate_kernel(AggArgs a) {
   __shared__ double sV[3][kAggCh];  // conf, cons, cons*conf of the chunk's valid members
@@ -102,6 +166,7 @@ __global__ __launch_bounds__(kAggT) __attribute__((amdgpu_waves_per_eu(kAggWpe, 
     load_idx(b + kAggCh, idn);
     double chain = 0.0;  // lanes 0..2 of wave 0: sum(conf), sum(cons), sum(cons*conf)
     int64_t k = 0;
+    int last_cnt = 0;
     if (t == 0) sVotes = 0;
     for (int64_t c0 = b; c0 < e; c0 += kAggCh) {
       unsigned long long msk[kAggPer];
@@ -131,6 +196,11 @@ __global__ __launch_bounds__(kAggT) __attribute__((amdgpu_waves_per_eu(kAggWpe, 
       const int cnt = run;
       if (lane == 0 && votes) atomicAdd(&sVotes, (unsigned long long)votes);
       __syncthreads();
+      if (kAggChainAsm && c0 + kAggCh >= e) {  // the last chunk: its chains after the loop
+        k += cnt;
+        last_cnt = cnt;
+        break;
+      }
       gather(idn);                     // next chunk in flight during the chains
       load_idx(c0 + 2 * kAggCh, idn);
       if (t < 3) {
@@ -148,6 +218,7 @@ __global__ __launch_bounds__(kAggT) __attribute__((amdgpu_waves_per_eu(kAggWpe, 
       k += cnt;
       __syncthreads();  // chunk buffer reused
     }
+    if (kAggChainAsm && t < 3 && last_cnt > 0) agg_chain_asm(chain, sV[t], last_cnt);
     if (t < 3) sTot[t] = chain;
     __syncthreads();
     if (t == 0) {

@@ -64,6 +64,9 @@ VARIANTS = {
     # namespace pass without its nontemporal hints (0.1752 vs 0.1665 ms, r04t)
     "nsnont": [("elementwise.hip", "constexpr bool kNsNtLoad = true;", "constexpr bool kNsNtLoad = false;"),
                ("elementwise.hip", "constexpr bool kNsNtStore = true;", "constexpr bool kNsNtStore = false;")],
+    # f4: the last chunk's chains in the compiler's 8-term loop inside the chunk loop (shipped:
+    # after the loop, asm, four 4-term batches in flight)
+    "aggnoasm": [("aggregate.hip", "constexpr bool kAggChainAsm = true;", "constexpr bool kAggChainAsm = false;")],
     "aggw1": [("aggregate.hip", "constexpr int kAggWpe = 6;", "constexpr int kAggWpe = 1;")],
     "tab4w": [("consensus_tab.hip", "constexpr int kTabWaves = 8;", "constexpr int kTabWaves = 4;")],
     "tbkvsort": [("tiebreak.hip", "constexpr bool kTbFullKeysInLds = true;", "constexpr bool kTbFullKeysInLds = false;")],
