@@ -45,6 +45,14 @@ def test_world_size_mismatch_fails():
     assert "WORLD_SIZE=1" in (p.stderr + p.stdout)
 
 
+def test_mfma_mode_is_config5_only():
+    """--mode mfma names the config-5 matrix-core pass; any other config refuses it before
+    touching the GPU (C5's mode="fast" runs the exact kernel)."""
+    p = _run(["--mode", "mfma", "--config", "c2", "--stub"])
+    assert p.returncode != 0
+    assert "--mode mfma" in (p.stderr + p.stdout)
+
+
 def test_rank_parity_checker_on_host_outputs():
     """bench.rank_parity (each rank's own-shard check on N > 1 lines) against the restatement's
     own outputs: equal -> all_equal; one flipped weight bit -> not (CPU, no GPU)."""
