@@ -141,8 +141,8 @@ __global__ __launch_bounds__(256) void reestimate_agreement_kernel(const double*
                                            (unsigned long long)cntS[tid]);
 }
 
-// Pass 1 with votes.  Lane per market column m = 256*block + tid, so wave w of a block
-// covers the 64 markets of vote word k = 4*block + w.  Agents are streamed kVoteRows rows
+// Pass 1 with votes.  Lane per market column m = kVoteBlock*block + tid, so wave w of a block
+// covers the 64 markets of vote word k = (kVoteBlock / 64)*block + w.  Agents are streamed kVoteRows rows
 // at a time (coalesced 512-B row segments); the rows' vote ballots are spread over lanes
 // 0..kVoteRows-1 and stored as contiguous bytes of vote_bits[k][a ..].  Every lane also
 // carries the total weight in agent order (core.py:107-120: the same for every column,
@@ -168,7 +168,11 @@ __device__ __forceinline__ unsigned long long writelane_u64(unsigned long long v
   const unsigned hi = (unsigned)bce_writelane((int)(unsigned)(v >> 32), l, (int)(unsigned)(old >> 32));
   return ((unsigned long long)hi << 32) | lo;
 }
-__global__ __launch_bounds__(256) void reestimate_consensus_votes_kernel(
+// kVoteBlock: threads per workgroup -- its waves read neighbouring 512-B pieces of each row:
+// 1024 threads 22.74-22.98 ms per C5 iteration, 512 23.60-23.66, 256 23.61-23.79 (profiles/r05zh/,
+// r05zi/)
+constexpr int kVoteBlock = 1024;
+__global__ __launch_bounds__(kVoteBlock) void reestimate_consensus_votes_kernel(
     const double* __restrict__ P, int64_t A, int64_t M, int64_t ld, const double* __restrict__ w,
     double* __restrict__ cons, uint8_t* __restrict__ null_out, unsigned long long* __restrict__ vote_bits,
     unsigned long long* __restrict__ cvote_words, unsigned long long* __restrict__ ok_words,
@@ -289,6 +293,8 @@ constexpr bool kMfmaTwoAcc = false;  // even / odd agent rows on two accumulator
 constexpr int kMfmaRows = 8;         // agent rows per batch (the exact kernel: kVoteRows = 16)
 constexpr bool kMfmaPrefetch = true;
 constexpr int kMfmaWpe = kMfmaPrefetch ? 6 : 8;  // waves per SIMD the VGPR budget allows
+// 8-wave workgroups: three per CU at 6 waves per SIMD (1024 threads would fit only one)
+constexpr int kMfmaBlock = 512;
 
 __global__ __launch_bounds__(256) void reestimate_total_kernel(const double* __restrict__ w, int64_t A,
                                                                double* __restrict__ total_fast,
@@ -318,7 +324,7 @@ __global__ __launch_bounds__(256) void reestimate_total_kernel(const double* __r
   }
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMfmaWpe, kMfmaWpe))) void reestimate_votes_mfma_kernel(
+__global__ __launch_bounds__(kMfmaBlock) __attribute__((amdgpu_waves_per_eu(kMfmaWpe, kMfmaWpe))) void reestimate_votes_mfma_kernel(
     const double* __restrict__ P, int64_t A, int64_t M, int64_t ld, const double* __restrict__ w,
     const double* __restrict__ total_fast, double* __restrict__ cons, uint8_t* __restrict__ null_out,
     unsigned long long* __restrict__ vote_bits, unsigned long long* __restrict__ cvote_words,
@@ -530,7 +536,7 @@ extern "C" int bce_reestimate_consensus_votes(const double* P, int64_t A, int64_
   if (M == 0) return BCE_OK;
   BCE_REQUIRE(P && w && consensus && null_out && vote_bits && cvote_words && ok_words,
               "reestimate_votes: NULL argument");
-  hipLaunchKernelGGL(reestimate_consensus_votes_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0,
+  hipLaunchKernelGGL(reestimate_consensus_votes_kernel, dim3((unsigned)((M + kVoteBlock - 1) / kVoteBlock)), dim3(kVoteBlock), 0,
                      as_stream(stream), P, A, M, ld, w, consensus, null_out,
                      reinterpret_cast<unsigned long long*>(vote_bits), reinterpret_cast<unsigned long long*>(cvote_words),
                      reinterpret_cast<unsigned long long*>(ok_words), (const int32_t*)nullptr);
@@ -578,7 +584,7 @@ extern "C" int bce_reestimate_consensus_votes_mfma(const double* P, int64_t A, i
   hipLaunchKernelGGL(reestimate_total_kernel, dim3(1), dim3(256), 0, st, w, A, total, nflag);
   int rc = check_launch("reestimate_total_kernel");
   if (rc) return rc;
-  hipLaunchKernelGGL(reestimate_votes_mfma_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, P, A, M, ld,
+  hipLaunchKernelGGL(reestimate_votes_mfma_kernel, dim3((unsigned)((M + kMfmaBlock - 1) / kMfmaBlock)), dim3(kMfmaBlock), 0, st, P, A, M, ld,
                      w, total, consensus, null_out, reinterpret_cast<unsigned long long*>(vote_bits),
                      reinterpret_cast<unsigned long long*>(cvote_words), reinterpret_cast<unsigned long long*>(ok_words),
                      nflag, flags);
@@ -589,7 +595,7 @@ extern "C" int bce_reestimate_consensus_votes_mfma(const double* P, int64_t A, i
   rc = check_launch("reestimate_fixup_kernel");
   if (rc) return rc;
   // precondition fallback (weights negative / NaN / inf): exits at once unless nflag[1] != 0
-  hipLaunchKernelGGL(reestimate_consensus_votes_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, P, A, M,
+  hipLaunchKernelGGL(reestimate_consensus_votes_kernel, dim3((unsigned)((M + kVoteBlock - 1) / kVoteBlock)), dim3(kVoteBlock), 0, st, P, A, M,
                      ld, w, consensus, null_out, reinterpret_cast<unsigned long long*>(vote_bits),
                      reinterpret_cast<unsigned long long*>(cvote_words),
                      reinterpret_cast<unsigned long long*>(ok_words), (const int32_t*)(nflag + 1));

@@ -60,6 +60,9 @@ VARIANTS = {
     "nodeep": [("consensus_wide.hip", "constexpr bool kWideChainDeep = true;", "constexpr bool kWideChainDeep = false;")],
     # EXACT chains on every lane of the chain wave (lane % 3 picks the chain; shipped: lanes 0..2)
     "chain64": [("consensus_wide.hip", "constexpr bool kWideChain3 = true;", "constexpr bool kWideChain3 = false;")],
+    # C5 exact pass 1 on 256- / 512-thread workgroups (shipped: 1024)
+    "c5b256": [("stats.hip", "constexpr int kVoteBlock = 1024;", "constexpr int kVoteBlock = 256;")],
+    "c5b512": [("stats.hip", "constexpr int kVoteBlock = 1024;", "constexpr int kVoteBlock = 512;")],
     "wdiv": [("consensus_wide.hip", "constexpr bool kWideFastRecip = true;", "constexpr bool kWideFastRecip = false;")],
     # namespace pass without its nontemporal hints (0.1752 vs 0.1665 ms, r04t)
     "nsnont": [("elementwise.hip", "constexpr bool kNsNtLoad = true;", "constexpr bool kNsNtLoad = false;"),
