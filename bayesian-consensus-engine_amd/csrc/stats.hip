@@ -172,6 +172,7 @@ __device__ __forceinline__ unsigned long long writelane_u64(unsigned long long v
 // 1024 threads 22.74-22.98 ms per C5 iteration, 512 23.60-23.66, 256 23.61-23.79 (profiles/r05zh/,
 // r05zi/)
 constexpr int kVoteBlock = 1024;
+constexpr bool kVoteXcd = true;
 __global__ __launch_bounds__(kVoteBlock) void reestimate_consensus_votes_kernel(
     const double* __restrict__ P, int64_t A, int64_t M, int64_t ld, const double* __restrict__ w,
     double* __restrict__ cons, uint8_t* __restrict__ null_out, unsigned long long* __restrict__ vote_bits,
@@ -181,7 +182,14 @@ __global__ __launch_bounds__(kVoteBlock) void reestimate_consensus_votes_kernel(
   // kernel behind its own and lets the weight check pick one of the two on the device
   if (only_if && *only_if == 0) return;
   const int lane = lane_id();
-  const int64_t m = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  // kVoteXcd: workgroups are dealt round-robin to the 8 XCDs; block b takes column range
+  // xcd_block(b) so each XCD streams one contiguous slice of every row
+  int64_t blk = blockIdx.x;
+  if constexpr (kVoteXcd) {
+    const int64_t nb = gridDim.x, per = nb / 8, x = blk & 7, q = blk >> 3;
+    if (blk < per * 8) blk = x * per + q;  // the last nb % 8 blocks keep their own ranges
+  }
+  const int64_t m = blk * (int64_t)blockDim.x + threadIdx.x;
   const int64_t k = m >> 6;
   if ((k << 6) >= M) return;  // whole wave past the last market (wave-uniform)
   const bool in = m < M;

@@ -63,6 +63,9 @@ VARIANTS = {
     # C5 exact pass 1 on 256- / 512-thread workgroups (shipped: 1024)
     "c5b256": [("stats.hip", "constexpr int kVoteBlock = 1024;", "constexpr int kVoteBlock = 256;")],
     "c5b512": [("stats.hip", "constexpr int kVoteBlock = 1024;", "constexpr int kVoteBlock = 512;")],
+    # C5 exact pass 1: blocks in launch order over the columns (shipped: one contiguous column
+    # slice per XCD)
+    "c5noxcd": [("stats.hip", "constexpr bool kVoteXcd = true;", "constexpr bool kVoteXcd = false;")],
     "wdiv": [("consensus_wide.hip", "constexpr bool kWideFastRecip = true;", "constexpr bool kWideFastRecip = false;")],
     # namespace pass without its nontemporal hints (0.1752 vs 0.1665 ms, r04t)
     "nsnont": [("elementwise.hip", "constexpr bool kNsNtLoad = true;", "constexpr bool kNsNtLoad = false;"),
