@@ -339,7 +339,12 @@ __global__ __launch_bounds__(kMfmaBlock) __attribute__((amdgpu_waves_per_eu(kMfm
     unsigned long long* __restrict__ ok_words, int32_t* __restrict__ nflag, int32_t* __restrict__ flags) {
   if (nflag[1]) return;  // weights outside [0, inf): the gated exact kernel does this iteration
   const int lane = lane_id();
-  const int64_t m = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  int64_t blk = blockIdx.x;  // one contiguous column slice per XCD, as the exact pass (kVoteXcd)
+  if constexpr (kVoteXcd) {
+    const int64_t nb = gridDim.x, per = nb / 8, x = blk & 7, q = blk >> 3;
+    if (blk < per * 8) blk = x * per + q;
+  }
+  const int64_t m = blk * (int64_t)blockDim.x + threadIdx.x;
   const int64_t k = m >> 6;
   if ((k << 6) >= M) return;  // whole wave past the last market (wave-uniform)
   const bool in = m < M;

@@ -66,6 +66,8 @@ VARIANTS = {
     # C5 exact pass 1: blocks in launch order over the columns (shipped: one contiguous column
     # slice per XCD)
     "c5noxcd": [("stats.hip", "constexpr bool kVoteXcd = true;", "constexpr bool kVoteXcd = false;")],
+    # C5 exact and MFMA passes in launch order (shipped: one contiguous column slice per XCD)
+    "c5noxcd": [("stats.hip", "constexpr bool kVoteXcd = true;", "constexpr bool kVoteXcd = false;")],
     "wdiv": [("consensus_wide.hip", "constexpr bool kWideFastRecip = true;", "constexpr bool kWideFastRecip = false;")],
     # namespace pass without its nontemporal hints (0.1752 vs 0.1665 ms, r04t)
     "nsnont": [("elementwise.hip", "constexpr bool kNsNtLoad = true;", "constexpr bool kNsNtLoad = false;"),
