@@ -154,6 +154,44 @@ class Plan:
         scratch = torch.empty(sb, dtype=torch.uint8, device=dev) if sb > 0 else None
         return cls(torch.from_numpy(order).to(dev), bins, int(mx[0]), scratch)
 
+    @classmethod
+    def build_device(cls, offsets: torch.Tensor) -> "Plan":
+        """The same plan built on the GPU from the device offsets (bce_plan_bins_device: a
+        stable radix sort by bin and LPT key, no D2H copy of the CSR).  One stream
+        synchronisation returns the bin boundaries to the host."""
+        L = N.require_gpu()
+        dev = offsets.device
+        M = offsets.numel() - 1
+        order = torch.empty(max(M, 1), dtype=torch.int32, device=dev)
+        sb = int(L.bce_plan_device_scratch_bytes(M))
+        work = torch.empty(max(sb, 1), dtype=torch.uint8, device=dev)
+        bins = np.zeros(N.NBINS + 1, np.int64)
+        mx = np.zeros(1, np.int32)
+        lsb = np.zeros(1, np.int64)
+        N.check(L.bce_plan_bins_device(N.ptr(offsets), M, N.ptr(order), N.ptr(bins), N.ptr(mx), N.ptr(lsb),
+                                       N.ptr(work), sb, N.stream(dev)), "plan_bins_device")
+        scratch = torch.empty(int(lsb[0]), dtype=torch.uint8, device=dev) if lsb[0] > 0 else None
+        return cls(order, bins, int(mx[0]), scratch)
+
+    @classmethod
+    def for_markets(cls, offsets_host: np.ndarray, markets: np.ndarray, device=None) -> "Plan":
+        """The plan of a market subset over the FULL CSR (a rank's markets of
+        sharding.shard_markets_planned left in place): the subset binned and LPT-ordered as
+        bce_plan_bins would, its order holding the full batch's market indices, so outputs land
+        at those markets and per-unique outputs at their absolute CSR offsets."""
+        from .sharding import gather_csr, plan_order
+        L = N.lib()
+        off = np.ascontiguousarray(offsets_host, np.int64)
+        mk = np.asarray(markets, np.int64)
+        loc = gather_csr(off, mk)[0]
+        lorder, bins = plan_order(loc)
+        order = np.ascontiguousarray(mk[lorder].astype(np.int32))
+        lens = np.diff(loc)
+        sb = int(L.bce_consensus_scratch_bytes(N.ptr(off), N.ptr(order), N.ptr(bins)))
+        dev = device or N.device()
+        scratch = torch.empty(sb, dtype=torch.uint8, device=dev) if sb > 0 else None
+        return cls(torch.from_numpy(order).to(dev), bins, int(lens.max(initial=0)), scratch)
+
 
 @dataclass
 class ConsensusResult:
@@ -189,7 +227,15 @@ def consensus(offsets: torch.Tensor, sid: torch.Tensor, prob: torch.Tensor, tabl
     """core.compute_consensus for every CSR market (+ the validation range check).
 
     Pass ``max_len`` (<= 64: one launch, no planning) or a prebuilt :class:`Plan` for
-    ragged batches; with neither, a plan is built from a host copy of ``offsets``.
+    ragged batches; with neither, a plan is built on the GPU (:meth:`Plan.build_device`, one
+    stream synchronisation).  A caller that reruns the same CSR should build the Plan once.
+
+    ``mode="fast"`` (fixed-order trees, <= 1e-9 absolute vs the reference order) is
+    deterministic per call shape but not invariant to batch composition: a small call (e.g. a
+    market shard) may run a length bin in the wider launch of the bin above it, which sums the
+    partial totals in another fixed order, so the same market's float outputs can differ in the
+    last bits between a full batch and a shard (within 1e-9; include/bce.h BCE_MODE_FAST).
+    ``mode="exact"`` is bit-identical in every launch shape.
 
     Raw CSR is trusted for speed: a ``sid`` outside ``[0, table.n)`` has its row read
     clamped and a market longer than ``max_len`` is left unprocessed; either raises the
@@ -213,7 +259,7 @@ def consensus(offsets: torch.Tensor, sid: torch.Tensor, prob: torch.Tensor, tabl
             N.check_faults(dev, "consensus")
         return res
     if plan is None:
-        plan = Plan.build(offsets.cpu().numpy(), dev)
+        plan = Plan.build_device(offsets)
     sb = plan.scratch.numel() if plan.scratch is not None else 0
     rc = L.bce_consensus_planned(*common, N.ptr(plan.order), N.ptr(plan.bin_start), md, *outs,
                                  N.ptr(plan.scratch), sb, N.stream(dev))
@@ -339,7 +385,9 @@ def tiebreak_plan(offsets_host: np.ndarray, device=None, force: bool = False) ->
     """Length buckets for batch.tiebreak (markets of <= 32 agents), when they cost less than
     the contiguous tiles by the kernels' relative tile costs (_TILE_COST), or always (force)."""
     lens = np.diff(np.asarray(offsets_host, np.int64))
-    if len(lens) == 0 or int(lens.max()) > 32:
+    if len(lens) == 0 or int(lens.max()) > 32 or int(lens.min()) < 0:
+        # a negative length (decreasing offsets) falls in no bucket: the contiguous kernel
+        # records it as a device fault (kFaultTooLong) instead of leaving outputs unwritten
         return TiePlan(None)
     M = len(lens)
     pad = (-M) % 64
@@ -373,7 +421,9 @@ def tiebreak(offsets: torch.Tensor, pred: torch.Tensor, conf: torch.Tensor, weig
 
     ``plan`` (optional, :func:`tiebreak_plan`): length buckets of a ragged batch of <= 32-agent
     markets, reused across calls on the same CSR (no host scan per call).  Without one, a
-    ragged batch scanned on the host is bucketed the same way when that pays."""
+    ragged batch scanned on the host is bucketed the same way when that pays -- an O(M) host
+    pass and up to three host-to-device list copies on EVERY call: a caller that reruns the
+    same CSR should build the TiePlan once with :func:`tiebreak_plan` and pass it in."""
     L = N.require_gpu()
     M = offsets.numel() - 1
     Nsig = pred.numel()

@@ -1,8 +1,10 @@
 """Multi-GPU partitioning: one process per GPU, torch.distributed over
 RCCL/xGMI (backend "nccl"; "gloo" for CPU tests).
 
-* Markets (configs 2/3) shard with ZERO communication: contiguous market ranges split at
-  equal signal counts (prefix sum of the CSR offsets), source table replicated (e1).
+* Markets (configs 2/3) shard with ZERO communication, source table replicated (e1): either
+  contiguous market ranges at equal signal counts (:func:`shard_markets`), or -- the config-3
+  split -- the length-binned plan order cut at equal measured cost (:func:`shard_markets_planned`),
+  so each rank launches whole length classes; :func:`gather_csr` builds a rank's own CSR.
 * Sources (config 4) shard by an owner hash; the only exchange is the per-source outcome
   flags produced by market shards, combined with one SUM all-reduce (e2) whose packing
   keeps the participate and correct counts apart, so a source flagged by two shards in
@@ -10,7 +12,7 @@ RCCL/xGMI (backend "nccl"; "gloo" for CPU tests).
 """
 from __future__ import annotations
 
-from typing import Tuple
+from typing import Optional, Tuple
 
 import numpy as np
 import torch
@@ -29,6 +31,101 @@ def shard_markets(offsets_host: np.ndarray, world: int, rank: int) -> Tuple[int,
     cuts[0], cuts[-1] = 0, M
     cuts = np.maximum.accumulate(np.clip(cuts, 0, M))
     return int(cuts[rank]), int(cuts[rank + 1])
+
+
+# Length bins of the planned consensus launch (consensus.hip kBinMax, BCE_NBINS = 13): bins 0..3
+# (n <= 64) run lane/segment kernels on the side stream, 4..11 the wide kernels, 12 (> 4096) the
+# long kernel.
+BIN_MAX = np.array([8, 16, 32, 64, 128, 256, 512, 1024, 1536, 2048, 3072, 4096], np.int64)
+_WIDE_LO, _WIDE_HI = 4, 11
+
+# Measured cost of one market in each bin's launch on the full config-3 batch (microseconds per
+# market: the bin launched ALONE / its market count; profiles/r06a/c3_bin_costs{,_exact}.json,
+# tools/c3_bins.py).  The wide kernels' per-market cost is set by the bin's sort size, not by the
+# market's own length, so a per-market figure per bin is the model.  Bin 12 (> 4096, the long
+# kernel: not in config 3) is an estimate.
+PLAN_BIN_COST_US = np.array([0.00075, 0.00280, 0.00329, 0.00312,
+                             0.00334, 0.00368, 0.00452, 0.00884, 0.01532, 0.02054, 0.03900, 0.04409,
+                             0.2], np.float64)
+PLAN_BIN_COST_US_EXACT = np.array([0.00074, 0.00277, 0.00332, 0.00312,
+                                   0.00348, 0.00392, 0.00495, 0.01167, 0.02182, 0.02766, 0.05328, 0.06472,
+                                   0.3], np.float64)
+_SIDE_LAST = 3  # bins 0..3 run on the planned launch's side stream, under the wide bins
+
+
+def market_bins(offsets_host: np.ndarray) -> np.ndarray:
+    """Length bin of every market (bce_plan_bins' bin_of)."""
+    lens = np.diff(np.asarray(offsets_host, np.int64))
+    return np.searchsorted(BIN_MAX, lens, side="left").astype(np.int64)
+
+
+def plan_order(offsets_host: np.ndarray):
+    """(order int32[M], bin_start int64[14]) exactly as bce_plan_bins builds them: markets grouped
+    by length bin in bin order, market order inside bins 0..3 and 12, longest first (LPT, ties
+    by market order) inside the wide bins 4..11 (consensus.hip bce_plan_bins)."""
+    off = np.asarray(offsets_host, np.int64)
+    lens = np.diff(off)
+    if len(lens) and int(lens.min()) < 0:
+        raise ValueError("plan_order: offsets not monotone")
+    b = market_bins(off)
+    wide = (b >= _WIDE_LO) & (b <= _WIDE_HI)
+    sec = np.where(wide, -lens, 0)
+    order = np.lexsort((np.arange(len(lens)), sec, b)).astype(np.int32)
+    bin_start = np.zeros(len(BIN_MAX) + 2, np.int64)
+    bin_start[1:] = np.cumsum(np.bincount(b, minlength=len(BIN_MAX) + 1))
+    return order, bin_start
+
+
+def _equal_cost_cut(c: np.ndarray, world: int) -> np.ndarray:
+    """Cut points of a cumulative cost array into ``world`` pieces of equal cost."""
+    n = len(c)
+    total = float(c[-1]) if n else 0.0
+    cuts = np.searchsorted(c, total * np.arange(world + 1, dtype=np.float64) / world, side="left")
+    cuts[0], cuts[-1] = 0, n
+    return np.maximum.accumulate(np.clip(cuts, 0, n))
+
+
+def shard_markets_planned(offsets_host: np.ndarray, world: int, rank: int, mode: str = "fast",
+                          cost_us: Optional[np.ndarray] = None) -> np.ndarray:
+    """The markets of ``rank`` when the plan order (:func:`plan_order`: length bins, longest
+    first inside the wide bins) is cut into ``world`` pieces of equal measured cost
+    (``cost_us`` per market of each bin; the mode's measured table by default).  Every rank
+    then holds whole length classes -- one to three full-size launches of its resident grid --
+    instead of every bin at 1/world of its size (:func:`shard_markets`), which pays each
+    launch's ramp and tail ``world`` times over.
+
+    The short bins (n <= 64) run on the planned launch's side stream underneath the wide bins,
+    so they are cut separately: rank r gets the r-th equal-cost piece of the short markets AND
+    the r-th equal-cost piece of the wide / long ones, and its short launches overlap its wide
+    ones as they do in the full batch.  Returns the market indices in ascending order (int64);
+    :func:`gather_csr` builds the rank's own CSR from them and the outputs scatter back by
+    market index."""
+    off = np.asarray(offsets_host, np.int64)
+    M = len(off) - 1
+    if world <= 1:
+        return np.arange(M, dtype=np.int64)
+    cost = np.asarray(cost_us if cost_us is not None else
+                      (PLAN_BIN_COST_US_EXACT if mode == "exact" else PLAN_BIN_COST_US), np.float64)
+    order, bin_start = plan_order(off)
+    out = []
+    for lo, hi in ((0, bin_start[_SIDE_LAST + 1]), (bin_start[_SIDE_LAST + 1], M)):
+        seq = order[lo:hi]
+        cuts = _equal_cost_cut(np.cumsum(cost[market_bins(off)[seq]]), world)
+        out.append(seq[cuts[rank]:cuts[rank + 1]])
+    return np.sort(np.concatenate(out)).astype(np.int64)
+
+
+def gather_csr(offsets_host: np.ndarray, markets: np.ndarray, *arrays):
+    """A market subset as its own CSR: (local offsets int64[m+1], signal index int64[n] into the
+    full arrays, each of ``arrays`` gathered).  Per-unique outputs of market j of the subset sit
+    at local offsets[j]; they belong at offsets_host[markets[j]] of the full batch."""
+    off = np.asarray(offsets_host, np.int64)
+    mk = np.asarray(markets, np.int64)
+    lens = off[mk + 1] - off[mk]
+    loc = np.zeros(len(mk) + 1, np.int64)
+    np.cumsum(lens, out=loc[1:])
+    idx = np.repeat(off[mk] - loc[:-1], lens) + np.arange(int(loc[-1]), dtype=np.int64)
+    return (loc, idx) + tuple(np.asarray(a)[idx] for a in arrays)
 
 
 def owner_of(source_ids: np.ndarray, world: int) -> np.ndarray:

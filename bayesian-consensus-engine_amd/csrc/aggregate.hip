@@ -127,7 +127,9 @@ constexpr int kAggCh = kAggT * kAggPer;     // chunk = 1024 members, list order 
 
 
 __global__ __launch_bounds__(kAggT) __attribute__((amdgpu_waves_per_eu(kAggWpe, 8))) void aggregate_kernel(AggArgs a) {
-  __shared__ double sV[3][kAggCh];  // conf, cons, cons*conf of the chunk's valid members
+  // conf, cons, cons*conf of the chunk's valid members; 16-B aligned rows padded by 16 doubles:
+  // agg_chain_asm's ds_read_b128 batches read up to 16 terms past last_cnt (never added)
+  __shared__ __attribute__((aligned(16))) double sV[3][kAggCh + 16];
   __shared__ int sWave[kAggPer][kAggT / 64];
   __shared__ int sHist[256];
   __shared__ int sWsum[kAggT / 64];

@@ -148,7 +148,8 @@ __device__ __forceinline__ double py_round_nd_fast(double x, double scale, doubl
   const double k = rint(hi);
   const double d = hi - k;
   const bool in = fabs(x) < thresh;
-  slow = in & ((fabs(d) == 0.5) | ((d == 0.0) & (fabs(lo) == 0.5)));
+  // int operands: branch-free, and no -Wbitwise-instead-of-logical on bools
+  slow = ((int)in & ((int)(fabs(d) == 0.5) | ((int)(d == 0.0) & (int)(fabs(lo) == 0.5)))) != 0;
   const double q = k * rinv;
   double r = __builtin_fma(__builtin_fma(-q, scale, k), rinv, q);
   r = (r == 0.0) ? copysign(0.0, x) : r;

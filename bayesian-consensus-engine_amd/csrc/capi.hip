@@ -14,15 +14,6 @@
 
 namespace bce {
 
-static thread_local char g_err[512] = "";
-
-void set_error(const char* fmt, ...) {
-  va_list ap;
-  va_start(ap, fmt);
-  vsnprintf(g_err, sizeof g_err, fmt, ap);
-  va_end(ap);
-}
-
 int check_launch(const char* what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
@@ -49,6 +40,7 @@ struct DevCtx {
   hipEvent_t ev_fork = nullptr, ev_join[kSideStreams] = {};
   int* split = nullptr;               // kQueueSlots blocks of kSplitWords tie-break ticket words
   std::atomic<unsigned> split_next{0};
+  std::atomic<int> split_last[64] = {};  // per slot: the ticket of the last pair that took it
 };
 constexpr int kQueueSlots = 64;
 DevCtx g_dev[kMaxDev];
@@ -97,12 +89,20 @@ int cu_count() {
   return c ? c->cus : 256;
 }
 
-int* split_slot() {
+int* split_slot(int ticket, hipStream_t st) {
   DevCtx* c = dev_ctx();
   if (!c || !c->split) return nullptr;
+  static_assert(kQueueSlots == 64, "split_last size");
   // tickets make reuse safe, on any stream: PART 1 raises a word to its ticket (atomicMax) and
   // PART 2 runs whenever the word holds its own or a newer pair's ticket (tiebreak.hip)
-  return c->split + (size_t)(c->split_next.fetch_add(1) % kQueueSlots) * kSplitWords;
+  const unsigned k = c->split_next.fetch_add(1) % kQueueSlots;
+  int* w = c->split + (size_t)k * kSplitWords;
+  // After the 30-bit ticket counter wraps, the slot's words still hold the old, larger tickets
+  // and would make every later PART 2 launch run all its waves: clear the slot on
+  // this stream, ahead of this pair's PART 1, once per wrap.
+  if (ticket < c->split_last[k].exchange(ticket) && hipMemsetAsync(w, 0, kSplitWords * sizeof(int), st) != hipSuccess)
+    return nullptr;
+  return w;
 }
 
 int* fault_word() {
@@ -200,7 +200,6 @@ extern "C" int bce_debug_set_spin_cap(int cap) {
 }
 
 extern "C" int bce_abi_version(void) { return BCE_ABI_VERSION; }
-extern "C" const char* bce_last_error(void) { return bce::g_err; }
 extern "C" int bce_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;

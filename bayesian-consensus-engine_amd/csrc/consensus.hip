@@ -1724,6 +1724,293 @@ extern "C" int64_t bce_consensus_scratch_bytes(const int64_t* offsets_host, cons
   return (int64_t)grid * 4 * next_pow2(mx) * 8;
 }
 
+// ======================================================================================
+// The device planner (bce_plan_bins_device): the plan of bce_plan_bins built from device
+// offsets, no D2H copy of the CSR.  A market's bin and its LPT position are one 12-bit key
+//   bins 0..3 (n <= 64)           key = bin                (market order inside the bin)
+//   wide bin b, lengths lo..hi    key = 4 + (lo - 65) + (hi - n)   (bins ascending, longest first)
+//   n > 4096                      key = kPlanKeys - 1
+// so the plan is a STABLE sort of the market indices by key: two LSD passes of 6-bit digits,
+// each a per-chunk digit count, one exclusive scan of the [digit][chunk] counts and a stable
+// scatter (the rank inside a chunk from a [thread][digit] count matrix in LDS).  Stable at
+// every pass, hence market order inside equal keys: exactly bce_plan_bins' order.
+// ======================================================================================
+namespace bce {
+constexpr int kPlanKeys = 4 + (4096 - 65 + 1) + 1;  // 4037 < 2^12
+constexpr int kPlanThreads = 256;
+constexpr int kPlanPer = 4;                          // markets per thread
+constexpr int kPlanChunk = kPlanThreads * kPlanPer;  // markets per workgroup
+constexpr int kPlanDigits = 64;                      // 6-bit digits, two passes
+constexpr int kPlanScanThreads = 1024;
+static_assert(kPlanKeys <= kPlanDigits * kPlanDigits, "two 6-bit passes");
+
+struct PlanInfo {
+  unsigned long long bins[BCE_NBINS];
+  unsigned long long max_len;
+  unsigned long long long_max;  // longest market of the > 4096 bin (scratch sizing)
+  unsigned long long badrev;    // M - (first market whose offsets decrease), 0 = none
+};
+
+__device__ __forceinline__ int plan_bin(int64_t n) {
+  return n <= 8 ? 0 : n <= 16 ? 1 : n <= 32 ? 2 : n <= 64 ? 3 : n <= 128 ? 4 : n <= 256 ? 5 : n <= 512 ? 6
+       : n <= 1024 ? 7 : n <= 1536 ? 8 : n <= 2048 ? 9 : n <= 3072 ? 10 : n <= 4096 ? 11 : 12;
+}
+
+__device__ __forceinline__ int plan_key(int64_t n, int b) {
+  if (b <= 3) return b;
+  if (b == 12) return kPlanKeys - 1;
+  const int lo = b == 4 ? 65 : b == 5 ? 129 : b == 6 ? 257 : b == 7 ? 513 : b == 8 ? 1025 : b == 9 ? 1537
+               : b == 10 ? 2049 : 3073;
+  const int hi = b == 4 ? 128 : b == 5 ? 256 : b == 6 ? 512 : b == 7 ? 1024 : b == 8 ? 1536 : b == 9 ? 2048
+               : b == 10 ? 3072 : 4096;
+  return 4 + (lo - 65) + (hi - (int)n);
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_max_u64(T v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    const T o = (T)__shfl_xor((unsigned long long)v, m);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
+// Pass PASS digit counts of chunk blockIdx.x -> counts[digit * nchunks + chunk].  Pass 0 reads
+// the offsets (striped: coalesced) and also fills PlanInfo (bin counts, longest markets, the
+// first decreasing offset).
+template <int PASS>
+__global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(const int64_t* __restrict__ offsets, int64_t M,
+                                                                  const uint16_t* __restrict__ keys_in,
+                                                                  int32_t* __restrict__ counts, int64_t nchunks,
+                                                                  PlanInfo* info) {
+  __shared__ int cnt[kPlanDigits];
+  __shared__ int bincnt[BCE_NBINS];
+  const int t = threadIdx.x;
+  const int64_t c = blockIdx.x;
+  if (t < kPlanDigits) cnt[t] = 0;
+  if (PASS == 0 && t < BCE_NBINS) bincnt[t] = 0;
+  __syncthreads();
+  unsigned long long mx = 0, lmx = 0, badrev = 0;
+#pragma unroll
+  for (int k = 0; k < kPlanPer; ++k) {
+    const int64_t i = c * kPlanChunk + k * kPlanThreads + t;
+    if (i < M) {
+      int key;
+      if constexpr (PASS == 0) {
+        const int64_t n = offsets[i + 1] - offsets[i];
+        if (n < 0) badrev = (unsigned long long)(M - i) > badrev ? (unsigned long long)(M - i) : badrev;
+        const int b = plan_bin(n);
+        key = plan_key(n < 0 ? 0 : n, n < 0 ? 0 : b);
+        atomicAdd(&bincnt[n < 0 ? 0 : b], 1);
+        const unsigned long long un = n < 0 ? 0ull : (unsigned long long)n;
+        mx = un > mx ? un : mx;
+        if (b == 12) lmx = un > lmx ? un : lmx;
+      } else {
+        key = keys_in[i];
+      }
+      atomicAdd(&cnt[(key >> (6 * PASS)) & (kPlanDigits - 1)], 1);
+    }
+  }
+  __syncthreads();
+  if (t < kPlanDigits) counts[(int64_t)t * nchunks + c] = cnt[t];
+  if constexpr (PASS == 0) {
+    if (t < BCE_NBINS && bincnt[t]) atomicAdd(&info->bins[t], (unsigned long long)bincnt[t]);
+    mx = wave_max_u64(mx);
+    lmx = wave_max_u64(lmx);
+    badrev = wave_max_u64(badrev);
+    if (lane_id() == 0) {
+      if (mx) atomicMax(&info->max_len, mx);
+      if (lmx) atomicMax(&info->long_max, lmx);
+      if (badrev) atomicMax(&info->badrev, badrev);
+    }
+  }
+}
+
+// In-place exclusive scan of counts[0..E) by one workgroup (E = 64 x chunks: small).
+__global__ __launch_bounds__(kPlanScanThreads) void plan_scan_kernel(int32_t* __restrict__ counts, int64_t E) {
+  __shared__ int64_t wsum[kPlanScanThreads / kWave];
+  const int t = threadIdx.x;
+  const int64_t per = (E + kPlanScanThreads - 1) / kPlanScanThreads;
+  const int64_t a = t * per, b = (a + per < E) ? a + per : E;
+  int64_t s = 0;
+  for (int64_t i = a; i < b; ++i) s += counts[i];
+  // block exclusive scan of s
+  int64_t inc = s;
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const int64_t o = __shfl_up(inc, d);
+    if (lane_id() >= d) inc += o;
+  }
+  const int w = t / kWave;
+  if (lane_id() == kWave - 1) wsum[w] = inc;
+  __syncthreads();
+  if (t == 0) {
+    int64_t run = 0;
+    for (int k = 0; k < kPlanScanThreads / kWave; ++k) {
+      const int64_t v = wsum[k];
+      wsum[k] = run;
+      run += v;
+    }
+  }
+  __syncthreads();
+  int64_t run = wsum[w] + inc - s;
+  for (int64_t i = a; i < b; ++i) {
+    const int v = counts[i];
+    counts[i] = (int32_t)run;
+    run += v;
+  }
+}
+
+// Stable scatter of chunk blockIdx.x by its pass-PASS digit.  Thread t holds markets
+// 4t..4t+3 of the chunk (blocked: thread order == input order); mat[t][d] counts thread t's
+// items of digit d, and its exclusive scan in (d, t) order gives every item its rank among the
+// chunk's items of smaller digit or equal digit and earlier position.
+template <int PASS>
+__global__ __launch_bounds__(kPlanThreads) void plan_scatter_kernel(const int64_t* __restrict__ offsets, int64_t M,
+                                                                    const uint16_t* __restrict__ keys_in,
+                                                                    const int32_t* __restrict__ idx_in,
+                                                                    const int32_t* __restrict__ base, int64_t nchunks,
+                                                                    uint16_t* __restrict__ keys_out,
+                                                                    int32_t* __restrict__ idx_out) {
+  __shared__ int mat[kPlanThreads * kPlanDigits];  // [t][d], 64 KB
+  __shared__ int part[kPlanThreads];
+  const int t = threadIdx.x;
+  const int64_t c = blockIdx.x;
+#pragma unroll 8
+  for (int j = 0; j < kPlanDigits; ++j) mat[j * kPlanThreads + t] = 0;
+  int key[kPlanPer], idx[kPlanPer], before[kPlanPer];
+  const int64_t i0 = c * kPlanChunk + (int64_t)t * kPlanPer;
+#pragma unroll
+  for (int k = 0; k < kPlanPer; ++k) {
+    const int64_t i = i0 + k;
+    key[k] = -1;
+    idx[k] = 0;
+    if (i < M) {
+      if constexpr (PASS == 0) {
+        int64_t n = offsets[i + 1] - offsets[i];
+        n = n < 0 ? 0 : n;
+        key[k] = plan_key(n, plan_bin(n));
+        idx[k] = (int)i;
+      } else {
+        key[k] = keys_in[i];
+        idx[k] = idx_in[i];
+      }
+    }
+  }
+  __syncthreads();
+  int* row = mat + t * kPlanDigits;
+#pragma unroll
+  for (int k = 0; k < kPlanPer; ++k) {
+    if (key[k] >= 0) {
+      const int d = (key[k] >> (6 * PASS)) & (kPlanDigits - 1);
+      before[k] = row[d];
+      row[d] = before[k] + 1;
+    }
+  }
+  __syncthreads();
+  // column sums: thread j = (q, d) sums mat[64q .. 64q+63][d] (a wave reads consecutive words)
+  const int d = t & (kPlanDigits - 1), q = t / kPlanDigits;
+  int s = 0;
+#pragma unroll 8
+  for (int r = 0; r < kPlanDigits; ++r) s += mat[(q * kPlanDigits + r) * kPlanDigits + d];
+  part[d * (kPlanThreads / kPlanDigits) + q] = s;
+  __syncthreads();
+  if (t < kWave) {  // exclusive scan of part[] (256 values, 4 per lane) by one wave
+    int v[4], sum = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { v[k] = part[4 * t + k]; sum += v[k]; }
+    int inc = sum;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const int y = __shfl_up(inc, o);
+      if (lane_id() >= o) inc += y;
+    }
+    int run = inc - sum;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { part[4 * t + k] = run; run += v[k]; }
+  }
+  __syncthreads();
+  int run = part[d * (kPlanThreads / kPlanDigits) + q];
+#pragma unroll 8
+  for (int r = 0; r < kPlanDigits; ++r) {
+    int* p = &mat[(q * kPlanDigits + r) * kPlanDigits + d];
+    const int v = *p;
+    *p = run;
+    run += v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kPlanPer; ++k) {
+    if (key[k] >= 0) {
+      const int dg = (key[k] >> (6 * PASS)) & (kPlanDigits - 1);
+      const int64_t pos = (int64_t)base[(int64_t)dg * nchunks + c] + (row[dg] - mat[dg]) + before[k];
+      if constexpr (PASS == 0) keys_out[pos] = (uint16_t)key[k];
+      idx_out[pos] = idx[k];
+    }
+  }
+}
+}  // namespace bce
+
+static int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
+
+extern "C" int64_t bce_plan_device_scratch_bytes(int64_t n_markets) {
+  if (n_markets <= 0) return 0;
+  const int64_t chunks = (n_markets + kPlanChunk - 1) / kPlanChunk;
+  return align256(sizeof(PlanInfo)) + align256(2 * n_markets) + align256(4 * n_markets) +
+         align256(4 * kPlanDigits * chunks);
+}
+
+extern "C" int bce_plan_bins_device(const int64_t* offsets, int64_t n_markets, int32_t* order,
+                                    int64_t* bin_start_host, int32_t* max_len_host,
+                                    int64_t* long_scratch_bytes_host, void* scratch, int64_t scratch_bytes,
+                                    void* stream) {
+  BCE_REQUIRE(n_markets >= 0 && n_markets < ((int64_t)1 << 31), "plan_bins_device: bad n_markets %lld",
+              (long long)n_markets);
+  BCE_REQUIRE(bin_start_host, "plan_bins_device: bin_start_host NULL");
+  if (long_scratch_bytes_host) *long_scratch_bytes_host = 0;
+  if (max_len_host) *max_len_host = 0;
+  for (int b = 0; b <= BCE_NBINS; ++b) bin_start_host[b] = 0;
+  if (n_markets == 0) return BCE_OK;
+  BCE_REQUIRE(offsets && order && scratch, "plan_bins_device: NULL argument");
+  BCE_REQUIRE(scratch_bytes >= bce_plan_device_scratch_bytes(n_markets), "plan_bins_device: scratch too small");
+  hipStream_t st = as_stream(stream);
+  const int64_t chunks = (n_markets + kPlanChunk - 1) / kPlanChunk;
+  char* p = static_cast<char*>(scratch);
+  PlanInfo* info = reinterpret_cast<PlanInfo*>(p);
+  p += align256(sizeof(PlanInfo));
+  uint16_t* keys = reinterpret_cast<uint16_t*>(p);
+  p += align256(2 * n_markets);
+  int32_t* idx = reinterpret_cast<int32_t*>(p);
+  p += align256(4 * n_markets);
+  int32_t* counts = reinterpret_cast<int32_t*>(p);
+  BCE_HIP(hipMemsetAsync(info, 0, sizeof(PlanInfo), st));
+  const dim3 g((unsigned)chunks), blk(kPlanThreads);
+  hipLaunchKernelGGL((plan_count_kernel<0>), g, blk, 0, st, offsets, n_markets, nullptr, counts, chunks, info);
+  hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(kPlanScanThreads), 0, st, counts, kPlanDigits * chunks);
+  hipLaunchKernelGGL((plan_scatter_kernel<0>), g, blk, 0, st, offsets, n_markets, nullptr, nullptr, counts, chunks,
+                     keys, idx);
+  hipLaunchKernelGGL((plan_count_kernel<1>), g, blk, 0, st, offsets, n_markets, keys, counts, chunks, info);
+  hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(kPlanScanThreads), 0, st, counts, kPlanDigits * chunks);
+  hipLaunchKernelGGL((plan_scatter_kernel<1>), g, blk, 0, st, offsets, n_markets, keys, idx, counts, chunks,
+                     nullptr, order);
+  int rc = check_launch("plan_bins_device");
+  if (rc) return rc;
+  PlanInfo h{};
+  BCE_HIP(hipMemcpyAsync(&h, info, sizeof h, hipMemcpyDeviceToHost, st));
+  BCE_HIP(hipStreamSynchronize(st));
+  BCE_REQUIRE(h.badrev == 0, "plan_bins: offsets not monotone at market %lld",
+              (long long)(n_markets - (int64_t)h.badrev));
+  for (int b = 0; b < BCE_NBINS; ++b) bin_start_host[b + 1] = bin_start_host[b] + (int64_t)h.bins[b];
+  if (max_len_host) *max_len_host = (int32_t)(h.max_len > 0x7fffffffull ? 0x7fffffff : h.max_len);
+  const int64_t n_long = (int64_t)h.bins[BCE_NBINS - 1];
+  if (long_scratch_bytes_host && n_long > 0) {
+    const int grid = (int)(n_long < kHugeGrid ? n_long : kHugeGrid);
+    *long_scratch_bytes_host = (int64_t)grid * 4 * next_pow2((int64_t)h.long_max) * 8;
+  }
+  return BCE_OK;
+}
+
 extern "C" int bce_consensus_planned(const int64_t* offsets, int64_t n_markets, const int32_t* sid,
                                      const double* prob, int64_t n_signals, const double* relconf,
                                      const uint32_t* present_bits, int32_t n_sources,

@@ -175,6 +175,6 @@ int64_t wide_resident(int64_t max_len, int32_t mode, int32_t n_sources);
 // kSplitWords words (one per wave of the grid) for a tie-break FULL/rest launch pair
 // (tiebreak.hip; written with a per-launch ticket)
 constexpr int kSplitWords = 4096;
-int* split_slot();
+int* split_slot(int ticket, hipStream_t st);  // clears the slot on `st` when the ticket counter wrapped
 
 }  // namespace bce

@@ -1030,7 +1030,7 @@ extern "C" int bce_jsonl_render(void* handle, const int32_t* err_idx, const int6
   }
   memcpy(out, B->out.data(), B->out.size());
   if (text_off) memcpy(text_off, B->out_off.data(), (size_t)(L + 1) * sizeof(int64_t));
-  if (ok) memcpy(ok, B->out_ok.data(), (size_t)L);
+  if (ok && L > 0) memcpy(ok, B->out_ok.data(), (size_t)L);  // L == 0: data() may be NULL (UBSan)
   *n_bytes = (int64_t)B->out.size();
   return BCE_OK;
 }

@@ -107,7 +107,7 @@ __device__ __forceinline__ double tb_div_small(double x, int c, const double* rc
   const double b = (double)c;
   const double q0 = x * rc;
   const double q = __builtin_fma(__builtin_fma(-q0, b, x), rc, q0);
-  const bool ok = (fabs(x) >= 0x1p-1000) & (fabs(x) <= 0x1p1000);
+  const bool ok = ((int)(fabs(x) >= 0x1p-1000) & (int)(fabs(x) <= 0x1p1000)) != 0;
   return ballot(!ok) ? (ok ? q : x / b) : q;
 }
 
@@ -412,7 +412,7 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
   // streams: PART 1 raises its word to its ticket with atomicMax, and PART 2 runs when the word
   // holds its own ticket or a NEWER pair's (then it may run for nothing -- it skips FULL tiles
   // itself -- but never skips a tile its own PART 1 left).  Tickets are positive and
-  // increase; after a wrap a stale larger ticket only makes PART 2 run for nothing.
+  // increase; after a wrap split_slot clears the slot before the first pair that reuses it.
   if constexpr (PART == 2) run = a.split[wave] >= a.ticket;
   bool left = false;  // PART 1: this wave left a tile to PART 2
   for (int64_t tile = wave; run && tile * 64 < n_list; tile += nwaves) {
@@ -1296,9 +1296,9 @@ static int launch_tb_short(const TbArgs& a, const int32_t* market_list, int64_t 
     } else if (split) {
       static std::atomic<int> tickets{0};
       TbArgs b = a;
-      b.split = split_slot();
-      // positive; after a wrap, older (larger) tickets left in words only make PART 2 run
+      // positive; after a wrap split_slot clears the slot's stale (larger) tickets
       b.ticket = (tickets.fetch_add(1) & 0x3fffffff) + 1;
+      b.split = split_slot(b.ticket, st);
       if (!b.split) {
         set_error("tiebreak: no device split words");
         return BCE_EHIP;

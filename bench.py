@@ -27,8 +27,10 @@ Also measured here:
 Before the W warmup steps the device runs the step for --prewarm-s seconds so the clocks
 have ramped (a 20-step run then matches a 200-step one); that time is reported.
 Other configs (--config c3|c4|c5|ns|agg|tb) are secondary bench lines; the default is c2,
-and at N=1 the default run also appends c3, c3 over a 10M-source table, c4, tb and c5 (reduced
-steps, each with its roofline, CPU baseline and full-size parity) under "secondary"
+and at N=1 the default run also appends c3 (pre-planned), c3_fresh (planned on the GPU in the
+step), c3_shard8 (the 8-rank split's shards timed one by one: predicted strong scaling), c3 over
+a 10M-source table, c4, tb, tb_ragged, ns (f3), agg (f4) and c5 (reduced steps, each with its
+roofline, CPU baseline where a restatement exists and full-size parity) under "secondary"
 (--no-secondary skips them).
 """
 from __future__ import annotations
@@ -88,9 +90,16 @@ def parse(argv=None):
     p.add_argument("--shard", default=None,
                    help="c3 only: R/N or all/N -- time rank R's (or every rank's) market shard of an N-rank "
                         "run in this one process, no process group (predicted strong scaling)")
+    p.add_argument("--split", default="planned", choices=["planned", "contiguous"],
+                   help="c3 with N > 1 ranks or --shard: planned = sharding.shard_markets_planned (the plan "
+                        "order cut at equal measured cost: whole length classes per rank), contiguous = "
+                        "sharding.shard_markets (market ranges at equal signal counts)")
     p.add_argument("--single-mode", action="store_true",
                    help="c3 / c5: time only the line's own summation mode (profiling runs: every "
                         "dispatch of a kernel then belongs to that mode)")
+    p.add_argument("--fresh", action="store_true",
+                   help="c3: plan every step's batch on the GPU inside the timed step (a fresh batch: "
+                        "bce_plan_bins_device + one stream synchronisation) instead of a plan built once")
     p.add_argument("--graph", action="store_true",
                    help="c3: replay each step as a captured HIP graph (one launch per step)")
     p.add_argument("--no-secondary", action="store_true",
@@ -443,9 +452,16 @@ def rank_parity(res, offsets, sid, prob, rel, conf, present, unique, rank, m_sam
 
 
 # (line, config, steps, warmup, clock ramp s, extra args): the clock ramp as in each config's own
-# line; c3_S10M = config 3 over C4's 10M-source table (64-bit sort keys, verdict r04 item 4)
-SECONDARY = (("c3", "c3", 20, 3, 1.0, {}), ("c3_S10M", "c3", 10, 2, 0.5, {"c3_sources": 10_000_000}),
-             ("c4", "c4", 100, 10, 1.0, {}), ("tb", "tb", 10, 2, 1.0, {}), ("c5", "c5", 4, 1, 0.5, {}))
+# line; c3_fresh = config 3 planned on the GPU inside every step (a fresh batch); c3_shard8 = the
+# 8-rank planned split's shards timed one by one + the full batch (predicted strong scaling);
+# c3_S10M = config 3 over C4's 10M-source table (64-bit sort keys); tb_ragged = the tie-break
+# over 1M markets of 1..32 agents; ns / agg = SURVEY §8(f) f3 / f4
+SECONDARY = (("c3", "c3", 20, 3, 1.0, {}), ("c3_fresh", "c3", 20, 3, 0.5, {"fresh": True, "single_mode": True}),
+             ("c3_shard8", "c3", 20, 3, 0.3, {"shard": "all/8", "single_mode": True}),
+             ("c3_S10M", "c3", 10, 2, 0.5, {"c3_sources": 10_000_000}),
+             ("c4", "c4", 100, 10, 1.0, {}), ("tb", "tb", 10, 2, 1.0, {}),
+             ("tb_ragged", "tb", 10, 2, 0.5, {"ragged": True}), ("ns", "ns", 50, 5, 0.5, {}),
+             ("agg", "agg", 50, 5, 0.5, {}), ("c5", "c5", 4, 1, 0.5, {}))
 
 
 def run_secondary(args, world, rank) -> dict:
@@ -466,6 +482,19 @@ def run_secondary(args, world, rank) -> dict:
             setattr(a2, k, v)
         t0 = time.perf_counter()
         try:
+            if getattr(a2, "shard", None):
+                from bench_extra import c3_shards
+                j = c3_shards(a2)
+                out[line] = {k: j.get(k) for k in ("metric", "value", "unit", "mode", "world", "max_ms", "mean_ms",
+                                                  "max_over_mean", "predicted_efficiency", "split", "full_batch")}
+                out[line]["shards"] = [{k: x[k] for k in ("rank", "markets", "signals", "kernel_ms")}
+                                       for x in j["shards"]]
+                out[line]["steps"] = steps
+                out[line]["wall_s"] = round(time.perf_counter() - t0, 1)
+                gc.collect()
+                torch.cuda.empty_cache()
+                print(f"[bench] secondary {line}: {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
+                continue
             j = run_extra(a2, world, rank)
             r = j.get("roofline") or {}
             cb = j.get("cpu_baseline") or {}

@@ -197,12 +197,17 @@ def _cpu_c5(P, args, m_sample=1024):
 
 
 # ---------------------------------------------------------------------------------------
-def make_c3(world=1, rank=0, total=100_000_000, S=1_000_000):
-    """Config 3: ragged CSR with log-uniform lengths on [1, 4096] and Zipf(1.1)
-    sources over S ranks; this rank's market shard.  Returns (M, offsets, sid, prob, table
-    arrays (rel, conf, present) as interned on the host)."""
-    from bayesian_engine.sharding import shard_markets
+_C3_CACHE = {}
 
+
+def make_c3_full(total=100_000_000, S=1_000_000):
+    """Config 3, the whole batch: ragged CSR with log-uniform lengths on
+    [1, 4096] and Zipf(1.1) sources over S ranks.  Returns (offsets, sid, prob, table arrays
+    (rel, conf, present) as interned on the host).  Cached per process (one batch at a time)."""
+    key = (total, S)
+    if key in _C3_CACHE:
+        return _C3_CACHE[key]
+    _C3_CACHE.clear()
     rng = np.random.default_rng(3)
     lens = np.floor(np.exp(rng.uniform(0, np.log(4097), size=total // 400))).astype(np.int64)
     cs = np.cumsum(lens)
@@ -211,10 +216,8 @@ def make_c3(world=1, rank=0, total=100_000_000, S=1_000_000):
     lens[-1] -= int(cs[M - 1] - total)
     offsets = np.zeros(M + 1, np.int64)
     offsets[1:] = np.cumsum(lens)
-    m0, m1 = shard_markets(offsets, world, rank)
-    off = offsets[m0:m1 + 1] - offsets[m0]
-    n = int(off[-1])
-    r2 = np.random.default_rng(1000 + m0)
+    n = int(offsets[-1])
+    r2 = np.random.default_rng(1000)
     perm = np.random.default_rng(33).permutation(S).astype(np.int32)
     # Zipf(1.1) truncated to S ranks (rejection: redraw values > S; clamping them to rank S
     # would pile the ~24% tail mass onto one artificial hot source)
@@ -224,12 +227,35 @@ def make_c3(world=1, rank=0, total=100_000_000, S=1_000_000):
         z[bad] = r2.zipf(1.1, size=bad.size)
         bad = bad[z[bad] > S]
     sid = perm[z - 1]
+    del z
     prob = r2.random(n)
     rt = np.random.default_rng(34)
     rel, conf = rt.uniform(0.1, 1.0, S), rt.random(S)
     present = (rt.random(S) < 0.9).astype(np.uint8)
     rel_h, conf_h = np.where(present == 1, rel, 0.5), np.where(present == 1, conf, 0.25)
-    return M, off, sid, prob, (rel_h, conf_h, present)
+    _C3_CACHE[key] = (offsets, sid, prob, (rel_h, conf_h, present))
+    return _C3_CACHE[key]
+
+
+def make_c3(world=1, rank=0, total=100_000_000, S=1_000_000, split="planned", mode="fast"):
+    """This rank's market shard of the config-3 batch as its own CSR: (M of the whole batch,
+    offsets, sid, prob, table arrays, the shard's market indices).  ``split`` = "planned"
+    (sharding.shard_markets_planned: the plan order cut at equal measured cost, whole length
+    classes per rank) or "contiguous" (sharding.shard_markets: market ranges at equal signal
+    counts)."""
+    from bayesian_engine.sharding import gather_csr, shard_markets, shard_markets_planned
+
+    offsets, sid, prob, table = make_c3_full(total, S)
+    M = len(offsets) - 1
+    if world <= 1:
+        return M, offsets, sid, prob, table, np.arange(M, dtype=np.int64)
+    if split == "planned":
+        mk = shard_markets_planned(offsets, world, rank, mode=mode)
+    else:
+        m0, m1 = shard_markets(offsets, world, rank)
+        mk = np.arange(m0, m1, dtype=np.int64)
+    loc, _, s, p = gather_csr(offsets, mk, sid, prob)
+    return M, loc, s, p, table, mk
 
 
 def _graphed(step, dev):
@@ -255,7 +281,8 @@ def _c3(args, world, rank, barrier, max_over, sum_over):
 
     S = getattr(args, "c3_sources", 1_000_000)
     total = 100_000_000
-    M, off, sid, prob, table_host = make_c3(world, rank, total, S)
+    split = getattr(args, "split", "planned")
+    M, off, sid, prob, table_host, mk = make_c3(world, rank, total, S, split=split, mode=args.mode or "fast")
     n = int(off[-1])
     rel_h, conf_h, present = table_host
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -267,9 +294,12 @@ def _c3(args, world, rank, barrier, max_over, sum_over):
 
     mode = args.mode or "fast"
     other = "exact" if mode == "fast" else "fast"
+    fresh = getattr(args, "fresh", False)
 
     def step():
-        batch.consensus(d_off, d_sid, d_prob, table, plan=plan, mode=mode, out=res)
+        # fresh: every step plans its batch on the GPU (batch.consensus(plan=None) ->
+        # bce_plan_bins_device + one stream synchronisation), as for an incoming batch
+        batch.consensus(d_off, d_sid, d_prob, table, plan=None if fresh else plan, mode=mode, out=res)
 
     def step_other():
         batch.consensus(d_off, d_sid, d_prob, table, plan=plan, mode=other, out=res)
@@ -282,7 +312,7 @@ def _c3(args, world, rank, barrier, max_over, sum_over):
     a2 = copy.copy(args)
     a2.steps, a2.warmup, a2.prewarm_s = max(5, args.steps // 4), 3, 0.0
     wall2 = per2 = None
-    if not getattr(args, "single_mode", False):
+    if not getattr(args, "single_mode", False) and not fresh:
         wall2, per2 = _timed(step_other, a2, world, torch.cuda.current_stream(dev), barrier, max_over)
     wall, per = _timed(step, args, world, torch.cuda.current_stream(dev), barrier, max_over)
     from bayesian_engine import _native as N
@@ -325,11 +355,16 @@ def _c3(args, world, rank, barrier, max_over, sum_over):
         "value": sig / wall, "unit": "signals/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "f64", "data": "synthetic (SURVEY.md d3: log-uniform lengths, Zipf 1.1)",
-        "config": {"workload": f"c3: {M} markets, {total} signals total, Zipf over {S} sources, mode={mode}",
+        "config": {"workload": f"c3: {M} markets, {total} signals total, Zipf over {S} sources, mode={mode}, "
+                               f"{'fresh batch (planned on the GPU in the step)' if fresh else 'pre-planned'}",
                    "launch": "one captured HIP graph per step" if getattr(args, "graph", False) else
                              "stream launches (plan: one kernel per length bin)",
                    "markets_this_rank": Mloc, "signals_this_rank": n, "unique_per_market_mean": sum_u / max(Mloc, 1),
-                   "bins": plan.bin_start.tolist(), "parallelism": f"markets sharded over {world} rank(s), no collective"},
+                   "bins": plan.bin_start.tolist(),
+                   "plan": ("planned on the GPU inside every timed step (bce_plan_bins_device + one sync: a fresh "
+                            "batch)" if fresh else "pre-planned (Plan.build once, outside the timed steps)"),
+                   "parallelism": f"markets sharded over {world} rank(s), no collective" +
+                                  (f" (split: {'sharding.shard_markets_planned, whole length classes per rank' if split == 'planned' else 'sharding.shard_markets, contiguous ranges'})" if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": (_pmc("pmc_c3.json", signals_this_rank=n) if S == 1_000_000 else
                                  _pmc(f"pmc_c3_S{S // 1_000_000}M.json", signals_this_rank=n, sources=S)),
@@ -891,7 +926,8 @@ def _tb(args, world, rank, barrier, max_over, sum_over):
 # ---------------------------------------------------------------------------------------
 def c3_shards(args):
     """8-GPU C3 strong scaling predicted on one GPU (``bench.py --config c3 --shard all/N``):
-    every rank's market shard of make_c3(world=N, rank=R) (sharding.shard_markets) is
+    every rank's market shard of make_c3(world=N, rank=R) (--split: sharding.shard_markets_planned
+    by default, or sharding.shard_markets) is
     timed in turn in this one process, no process group, with the bench's own loop, then
     the full batch.  Predicted efficiency = t_full / (N * max_R t_R): a rank's step on its
     own GPU is its shard alone, and the step ends with the slowest rank."""
@@ -906,8 +942,11 @@ def c3_shards(args):
     mode = args.mode or "fast"
     a2 = copy.copy(args)
 
+    split = getattr(args, "split", "planned")
+
     def time_one(w, r):
-        M, off, sid, prob, (rel_h, conf_h, present) = make_c3(w, r, S=getattr(args, "c3_sources", 1_000_000))
+        M, off, sid, prob, (rel_h, conf_h, present), _ = make_c3(w, r, S=getattr(args, "c3_sources", 1_000_000),
+                                                                 split=split, mode=mode)
         T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
         table = batch.SourceTable.from_arrays(T(rel_h), T(conf_h), T(present))
         d_off, d_sid, d_prob = T(off), T(sid), T(prob)
@@ -937,11 +976,15 @@ def c3_shards(args):
         print(f"[c3 shards] {r}/{world}: {shards[-1]['kernel_ms']:.4f} ms", file=sys.stderr, flush=True)
     full = None if getattr(args, "shard_only", False) else time_one(1, 0)
     ms = [s["kernel_ms"] for s in shards]
-    out = {"metric": "c3 per-shard step time (predicted strong scaling)", "mode": mode, "world": world,
+    eff = full["kernel_ms"] / (world * max(ms)) if spec[0] == "all" and full else None
+    out = {"metric": f"c3 predicted {world}-GPU strong-scaling efficiency (full-batch step / ({world} x slowest "
+                     f"shard step), each shard timed alone on this GPU)",
+           "value": eff, "unit": "fraction of linear", "mode": mode, "world": world,
            "shards": shards, "full_batch": full,
            "max_ms": max(ms), "mean_ms": float(np.mean(ms)), "max_over_mean": max(ms) / float(np.mean(ms)),
-           "predicted_efficiency": full["kernel_ms"] / (world * max(ms)) if spec[0] == "all" and full else None,
-           "split": "sharding.shard_markets (equal signal counts)"}
+           "predicted_efficiency": eff,
+           "split": ("sharding.shard_markets_planned (plan order cut at equal measured cost)" if split == "planned"
+                     else "sharding.shard_markets (equal signal counts)")}
     return out
 
 

@@ -57,6 +57,15 @@ enum bce_mode {
     BCE_MODE_EXACT = 0, /* reference summation order: bit-exact outputs */
     BCE_MODE_FAST = 1   /* tree reductions for long markets (<= 1e-9 abs vs reference) */
 };
+/* BCE_MODE_FAST reproducibility: deterministic for a given call (the same launch reproduces
+ * every bit), but NOT invariant to batch composition.  bce_consensus_planned merges a small
+ * call's non-power-of-two bins (1025..1536, 2049..3072) into the launch of the bin above when a
+ * launch would fill fewer than 6 rounds of its resident grid (which depends on the market count
+ * and the GPU's CU count); the wider workgroup sums the partial totals over 8 instead of 6 (4
+ * instead of 3) waves.  So one market's consensus / confidence / total weight / normalizedWeight
+ * can differ in the last bits between a full batch, a shard of it, or another GPU model -- always
+ * within the 1e-9 bound.  Integer outputs, usid and weight are bit-exact in both modes, and
+ * BCE_MODE_EXACT is bit-identical in every launch shape. */
 
 /* Tie-break labels (tiebreak.py:123-133, 89-96). */
 enum bce_tb_label {
@@ -140,6 +149,20 @@ int bce_validate_csr(const int64_t* offsets, int64_t n_markets, const double* pr
 #define BCE_NBINS 13 /* n<=8, <=16, <=32, <=64, <=128, <=256, <=512, <=1024, <=1536, <=2048, <=3072, <=4096, >4096 */
 int bce_plan_bins(const int64_t* offsets_host, int64_t n_markets, int32_t* order_host,
                   int64_t* bin_start_host, int32_t* max_len_host);
+/* The same plan built on the GPU from DEVICE offsets (no D2H copy of the CSR, no host sort):
+ * a stable two-pass LSD radix sort of the market indices by a 12-bit key (bin, then longest
+ * first inside the wide bins), so `order` (device int32[n_markets]) is bit-identical to
+ * bce_plan_bins'.  Enqueued on `stream`; the call then SYNCHRONISES that stream to return the
+ * bin boundaries (host int64[BCE_NBINS+1]), the longest market (host, nullable) and the >4096
+ * bin's scratch bytes for bce_consensus_planned (host, nullable).  scratch: device buffer of
+ * bce_plan_device_scratch_bytes(n_markets) bytes (256-byte aligned).  Decreasing offsets ->
+ * BCE_EINVAL (as bce_plan_bins).  Replaces the per-call host planning of a fresh batch
+ * (the reference sorts each market's sources, core.py:103, inside its market loop,
+ * market.py:200-221). */
+int bce_plan_bins_device(const int64_t* offsets, int64_t n_markets, int32_t* order, int64_t* bin_start_host,
+                         int32_t* max_len_host, int64_t* long_scratch_bytes_host, void* scratch,
+                         int64_t scratch_bytes, void* stream);
+int64_t bce_plan_device_scratch_bytes(int64_t n_markets);
 /* Bytes of device scratch bce_consensus_planned needs for the >4096 bin. */
 int64_t bce_consensus_scratch_bytes(const int64_t* offsets_host, const int32_t* order_host,
                                     const int64_t* bin_start_host);

@@ -1135,3 +1135,23 @@ def test_tiebreak_full_tiles_round_edges(precision):
     for m in range(M):
         a, g = int(off[m]), int(exp["n_groups"][m])
         assert gk[a:a + g].tobytes() == exp["g_key"][a:a + g].tobytes(), m
+
+
+def test_tiebreak_plan_declines_decreasing_offsets():
+    """a market with a negative length (decreasing offsets) in a batch of
+    <= 32-agent markets is not dropped by the length buckets: tiebreak_plan declines to bucket
+    and the contiguous lane kernel records the device fault."""
+    import torch
+    from bayesian_engine import _native as N
+    from bayesian_engine import batch
+    lens = np.full(64 * 8, 5, np.int64)
+    off, pred, conf, weight, rel = _tb_inputs(lens, 4242)
+    assert batch.tiebreak_plan(off, force=True).buckets is not None
+    bad = off.copy()
+    bad[100] = bad[99] - 2  # market 99 has length -2, market 100 a longer one
+    assert batch.tiebreak_plan(bad, force=True).buckets is None
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    N.check_faults(torch.device("cuda", 0), "clean slate")
+    batch.tiebreak(T(bad), T(pred), T(conf), T(weight), T(rel))
+    with pytest.raises(N.BCEError):
+        N.check_faults(torch.device("cuda", 0), "decreasing offsets")

@@ -131,3 +131,68 @@ def test_sharded_consensus_matches_unsharded_and_oracle(name, mode):
                     assert a_.tobytes() == b_.tobytes(), (world, how, k)
             # the shards against the oracle as well (FAST: the same 1e-9)
             _compare_vec(got, exp, off, exact=(mode == "exact"))
+
+
+def _call_list(off_h, sid_d, prob_d, table, N_sig, mode, markets, dev):
+    """One rank's markets of a planned split left in place: a plan over the full CSR."""
+    from bayesian_engine import batch
+    off_d = torch.from_numpy(np.ascontiguousarray(off_h)).to(dev)
+    res = batch._alloc(len(off_h) - 1, N_sig, dev, True, True)
+    batch.consensus(off_d, sid_d, prob_d, table, plan=batch.Plan.for_markets(off_h, markets, dev), mode=mode,
+                    out=res)
+    torch.cuda.synchronize()
+    return {k: getattr(res, k).cpu().numpy() for k in KEYS_M + KEYS_U}
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("mode", ["exact", "fast"])
+@pytest.mark.parametrize("name", ["c3_slice", "c3_like", "c2_1M"])
+def test_planned_shards_match_unsharded_and_oracle(name, mode):
+    """sharding.shard_markets_planned (the plan order cut at equal measured cost: whole length
+    classes per rank, the C3 split of the N > 1 bench line) for N = 2 and 8, as each rank's own
+    gathered CSR (sharding.gather_csr, its own plan; outputs scattered back by market index) and
+    as a market subset of the full CSR (batch.Plan.for_markets): EXACT bit for bit, FAST within
+    1e-9 on the float outputs, against the unsharded call and the oracle."""
+    from bayesian_engine import _native as N
+    from bayesian_engine import batch
+    from bayesian_engine.sharding import gather_csr, shard_markets_planned
+    g = _case(name)
+    off = g["offsets"]
+    M, n = len(off) - 1, int(off[-1])
+    uniform = name == "c2_1M"
+    dev = torch.device("cuda", 0)
+    table = batch.SourceTable.from_arrays(_dev(g["rel"]), _dev(g["conf"]), _dev(g["present"]))
+    sid_d, prob_d = _dev(g["sid"], np.int32), _dev(g["prob"])
+    full = _call(off, sid_d, prob_d, table, n, mode, uniform, dev)
+    exp = orc.consensus_csr(off, g["sid"], g["prob"], g["rel"], g["conf"], g["present"])
+    u = exp["n_unique"].astype(np.int64)
+    pos = np.repeat(off[:-1], u) + (np.arange(int(u.sum())) - np.repeat(np.cumsum(u) - u, u))
+    for world in (2, 8):
+        cat = {k: np.zeros_like(full[k]) for k in KEYS_M + KEYS_U}
+        view = {k: np.zeros_like(full[k]) for k in KEYS_M + KEYS_U}
+        seen = np.zeros(M, np.int64)
+        for r in range(world):
+            mk = shard_markets_planned(off, world, r)
+            seen[mk] += 1
+            loc, idx, s, p = gather_csr(off, mk, g["sid"], g["prob"])
+            o = _call(loc, _dev(s, np.int32), _dev(p), table, len(idx), mode, uniform, dev)
+            for k in KEYS_M:
+                cat[k][mk] = o[k][:len(mk)]
+            for k in KEYS_U:
+                cat[k][idx] = o[k][:len(idx)]
+            o = _call_list(off, sid_d, prob_d, table, n, mode, mk, dev)
+            for k in KEYS_M:
+                view[k][mk] = o[k][mk]
+            for k in KEYS_U:
+                view[k][idx] = o[k][idx]
+        assert (seen == 1).all(), "every market on exactly one rank"
+        N.check_faults(dev, f"{name} {world} planned shards")
+        floats = ("consensus", "confidence", "total_weight", "nweight")
+        for got, how in ((cat, "gathered"), (view, "market subset")):
+            for k in KEYS_M + KEYS_U:
+                a_, b_ = (got[k][pos], full[k][pos]) if k in KEYS_U else (got[k], full[k])
+                if mode == "fast" and k in floats:
+                    np.testing.assert_allclose(a_, b_, rtol=0, atol=1e-9, equal_nan=True, err_msg=f"{world} {how} {k}")
+                else:
+                    assert a_.tobytes() == b_.tobytes(), (world, how, k)
+            _compare_vec(got, exp, off, exact=(mode == "exact"))

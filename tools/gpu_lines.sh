@@ -6,6 +6,7 @@
 #   smoke=         __graft_entry__.smoke() > gpurun_out/<tag>/smoke.txt
 #   sq:NAME=ARGS   SQ counters of bench ARGS (tools/gpu_sq.sh), summary -> <tag>/NAME_sq_counters.txt
 #   prof:NAME=KERNEL|META|ARGS   rocprof stats + PMC (tools/gpu_profile.sh) -> <tag>/NAME_*.json
+#   py:NAME=SCRIPT ARGS  timeout 600 python3 SCRIPT ARGS > gpurun_out/<tag>/NAME.json (a tools/ probe)
 # (replaces round 4's one-off gpu_r04*.sh scripts, verdict r04 item 7)
 set -u
 tag=$1; shift
@@ -23,6 +24,7 @@ for step in "$@"; do
     prof:*) n=${name#prof:}; IFS='|' read -r kern meta bargs <<< "$args"
             bash tools/gpu_profile.sh ${tag}_$n "$kern" $meta -- $bargs || exit $?
             for f in stats_summary.json pmc.json kernel_stats.csv; do cp gpurun_out/prof_${tag}_$n/$f $o/${n}_$f 2>/dev/null; done ;;
+    py:*) n=${name#py:}; timeout -k 10 600 python3 -u $args > $o/$n.json 2> $o/$n.err || exit $? ;;
     *) timeout -k 10 300 python3 bench.py $args > $o/$name.json 2> $o/$name.err || exit $? ;;
   esac
 done

@@ -107,7 +107,7 @@ def one(name, mode, reps):
     from bayesian_engine import _native as N, batch
     from bench_extra import make_c3
 
-    M, off, sid, prob, (rel, conf, present) = make_c3()
+    M, off, sid, prob, (rel, conf, present), _ = make_c3()
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
     table = batch.SourceTable.from_arrays(T(rel), T(conf), T(present))
     d = [T(off), T(sid), T(prob)]
