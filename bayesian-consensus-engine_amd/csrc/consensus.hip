@@ -2069,11 +2069,28 @@ extern "C" int bce_consensus_planned(const int64_t* offsets, int64_t n_markets, 
   bool merged_away[BCE_NBINS] = {};
   for (int b = 0; b < BCE_NBINS; ++b)
     for (int k = lo[b]; k < b; ++k) merged_away[k] = true;
-  // Longest bins first, except that the 2049..3072 bin precedes the 3073..4096 one: its
-  // 6-wave workgroups leave 4 of a CU's 16 wave slots free (two per CU at 128 VGPRs), which
-  // the side stream's short-market kernels then fill (C3 fast -1.3%,
-  // profiles/r03x/order_ab.txt).
-  static const int kOrder[BCE_NBINS] = {12, 10, 11, 9, 8, 7, 6, 5, 4, 3, 2, 1, 0};
+  // Launch order: longest bins first, except that the 2049..3072 bin precedes the 3073..4096
+  // one: its 6-wave workgroups leave 4 of a CU's 16 wave slots free (two per CU at 128 VGPRs),
+  // which the side stream's short-market kernels then fill (C3 fast -1.3%,
+  // profiles/archive/r03x/order_ab.txt) -- and every main-stream launch that fills fewer than
+  // kMergeRounds rounds of its resident grid (a shard's cut piece of a bin) moves behind the
+  // full ones.  A small launch first ends while the side stream still holds CUs, and the big
+  // persistent launch behind it, whose workgroups stride statically over its markets, then
+  // starts part of its grid late and drags a tail (a planned C3 shard: 0.226 vs 0.15 ms for the
+  // same bin-11 markets, profiles/r06c/).  Ordering every launch by estimated work instead cost
+  // the full C3 batch 2% (1.325 vs 1.298 ms, profiles/r06e/).
+  static const int kClassic[BCE_NBINS] = {12, 10, 11, 9, 8, 7, 6, 5, 4, 3, 2, 1, 0};
+  int kOrder[BCE_NBINS];
+  {
+    int k = 0;
+    for (int pass = 0; pass < 3; ++pass)
+      for (int oi = 0; oi < BCE_NBINS; ++oi) {
+        const int b = kClassic[oi];
+        const bool side = b <= side_last;
+        const bool small = !side && b < BCE_NBINS - 1 && !merged_away[b] && few(lo[b], b);
+        if ((pass == 0 && !side && !small) || (pass == 1 && small) || (pass == 2 && side)) kOrder[k++] = b;
+      }
+  }
   for (int oi = 0; oi < BCE_NBINS && !rc; ++oi) {
     const int b = kOrder[oi];
     if (merged_away[b]) continue;

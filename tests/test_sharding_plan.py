@@ -48,32 +48,33 @@ def test_plan_order_rejects_decreasing_offsets():
         plan_order(np.array([0, 5, 3], np.int64))
 
 
+@pytest.mark.parametrize("mode", ["fast", "exact"])
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
-def test_planned_split_is_a_balanced_partition_of_length_classes(world):
+def test_planned_split_is_a_balanced_partition_of_length_classes(world, mode):
+    from bayesian_engine.sharding import PLAN_BIN_COST_US_EXACT, _rank_main_us
     off = _offsets(7, M=60000, edges=False)
     M = len(off) - 1
     b = market_bins(off)
-    lens = np.diff(off)
+    cost = PLAN_BIN_COST_US_EXACT if mode == "exact" else PLAN_BIN_COST_US
     seen = np.zeros(M, np.int64)
-    costs, spans = [], []
+    main, side, bins_of = [], [], []
     for r in range(world):
-        mk = shard_markets_planned(off, world, r)
+        mk = shard_markets_planned(off, world, r, mode=mode)
         assert np.all(np.diff(mk) > 0), "ascending market indices"
         seen[mk] += 1
-        costs.append(float(PLAN_BIN_COST_US[b[mk]].sum()))
-        spans.append((lens[mk].min(initial=0), lens[mk].max(initial=0)))
+        cnt = np.bincount(b[mk], minlength=13).astype(np.float64)
+        main.append(_rank_main_us(cnt, mode, cost))
+        side.append(float((cost[:4] * cnt[:4]).sum()))
+        bins_of.append(set(np.unique(b[mk]).tolist()))
     assert (seen == 1).all()
-    costs = np.array(costs)
-    # equal modelled cost (short and wide parts cut apart) up to one market of each part's
-    # dearest bin
-    assert costs.max() - costs.min() <= 2 * (PLAN_BIN_COST_US[:4].max() + PLAN_BIN_COST_US.max())
+    # the short bins at equal cost up to one market; the wide ones at equal modelled time up to
+    # one market's and one launch's worth
+    assert max(side) - min(side) <= 2 * cost[:4].max()
     if world > 1:
+        assert max(main) - min(main) <= 2 * cost.max() + 8.0, main
+    if world == 8:
         # length classes: a rank holds a few whole (or cut) bins, not a slice of every bin
-        bins_of = [set(np.unique(b[shard_markets_planned(off, world, r)]).tolist()) for r in range(world)]
-        # at most two short bins and three wide bins per rank at 8 ranks
-        if world == 8:
-            assert all(len([b for b in s if b <= 3]) <= 2 and len([b for b in s if b > 3]) <= 3
-                       for s in bins_of), bins_of
+        assert all(len([x for x in s if x <= 3]) <= 2 and len([x for x in s if x > 3]) <= 4 for s in bins_of), bins_of
 
 
 def test_gather_csr_rebuilds_the_rank_batch():
