@@ -1,8 +1,8 @@
 #!/bin/bash
 # Interleaved same-box A/B of library variants through one bench command (GPU box, repo root):
 #   tools/gpu_ab.sh <tag> <reps> <variant,variant,...> -- <bench.py args>
-# variant "ship" = the in-tree library; any other name = tools/bin/variants/<name>/libbce_hip.so
-# (built on the CPU beforehand by tools/tab_variants.py / tools/wide_variants.py).  Every rep runs
+# variant "ship" = the in-tree library; any other name = tools/ab/<name>/libbce_hip.so
+# (built on the CPU beforehand; tools/ab/ travels with the snapshot, delete it after the A/B).  Every rep runs
 # every variant once, in order, into gpurun_out/<tag>/<variant>_<rep>.json; a summary of each
 # variant's ms_per_step (and roofline.avg_launch_ms) over the reps lands in <tag>/summary.txt.
 # Claim discipline: a change is promoted only when >= 3 interleaved reps beat the
@@ -16,7 +16,7 @@ export TMPDIR=/tmp
 IFS=',' read -ra VS <<< "$variants"
 for rep in $(seq 1 $reps); do
   for v in "${VS[@]}"; do
-    if [ "$v" = ship ]; then unset BCE_LIB; else export BCE_LIB=tools/bin/variants/$v/libbce_hip.so; fi
+    if [ "$v" = ship ]; then unset BCE_LIB; else export BCE_LIB=tools/ab/$v/libbce_hip.so; fi
     echo "[gpu_ab] $(date +%T) $v rep $rep" >&2
     timeout -k 10 300 python3 bench.py "$@" > $o/${v}_$rep.json 2> $o/${v}_$rep.err || exit $?
   done
