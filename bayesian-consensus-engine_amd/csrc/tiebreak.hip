@@ -1038,391 +1038,13 @@ constexpr int kTbThreads = 256;
 constexpr int kTbMax = 4096;
 constexpr unsigned long long kNanKey = 0xFFFFFFFFFFFFF000ull;
 
-// ======================================================================================
-// FULL tiles on a quad of lanes per market (round 6).
-// The lane-per-market FULL body holds 32 agents of state per lane (256 VGPRs) and a 16.5-KB
-// staging buffer per wave: two waves per SIMD, latency-bound (VALU active 24%, waits 52%).  Here
-// four lanes share a market (lane l: market l >> 2 of the wave's 16, agents 8q..8q+7, q = l & 3):
-// a wave takes a 64-market tile as four sub-tiles of 16 markets, each lane loads its 8 agents of
-// every array straight from global memory (one 64-B segment: lane l reads agents 8l..8l+7 of
-// the sub-tile), and a 33-double LDS row per market is the quad's shared medium.
-//   1. keys: round(pred, 6) (fast path + exact redo), written to the row; every own agent finds
-//      its first equal key (s <= t, == semantics: -0.0 == 0.0, NaN never equal) -> its leader;
-//      the market's 32-bit leader mask (quad DPP broadcasts) gives each group its first-seen
-//      ordinal; g_of leaves as two 16-B stores per lane;
-//   2. keys (ordinal << 5 | agent) bitonic-sorted across the quad (in-lane stages on registers,
-//      the lane-crossing ones by quad_perm DPP): every group a run, groups in first-seen order,
-//      members in input order;
-//   3. every ordered chain -- the group weight / confidence sums and max reliabilities in input
-//      order, the winner / tie fold over groups in dict order, the confidence mean and the
-//      variance sum in input order -- is each lane's 8-element walk seeded with the previous
-//      lane's tail state, run four times (after pass k lanes 0..k hold final values), so the
-//      arithmetic and its order are exactly the lane-per-market body's;
-//   4. per-group outputs go to slot g of the row at the run's end and leave as 16-B stores.
-// The same TbArgs / output contract as PART 1 of tiebreak_lpm_kernel; tiles that are not FULL
-// raise split[T % split_waves] for PART 2 (whose wave w takes tiles w, w + waves, ...).
-#ifndef BCE_TB_QUAD
-#define BCE_TB_QUAD 0
-#endif
-constexpr bool kTbQuad = BCE_TB_QUAD != 0;  // FULL tiles: quad kernel (1) or lane-per-market PART 1 (0)
-constexpr int kTbQuadWaves = 4;
-constexpr int kTbQuadRow = 33;                     // doubles per market row (32 + pad)
-constexpr int kTbQuadBuf = 16 * kTbQuadRow;        // per wave: 16 market rows
-#ifndef BCE_TB_QUAD_WPE
-#define BCE_TB_QUAD_WPE 4
-#endif
-
-template <int CTRL>
-__device__ __forceinline__ unsigned q_dpp(unsigned v) {
-  return (unsigned)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
-}
-template <int CTRL>
-__device__ __forceinline__ double q_dpp(double v) {
-  const int2 x = __builtin_bit_cast(int2, v);
-  int2 y;
-  y.x = __builtin_amdgcn_mov_dpp(x.x, CTRL, 0xF, 0xF, false);
-  y.y = __builtin_amdgcn_mov_dpp(x.y, CTRL, 0xF, 0xF, false);
-  return __builtin_bit_cast(double, y);
-}
-constexpr int kQPrev = 0x90;  // quad_perm [0,0,1,2]: lane q reads lane q-1 (lane 0 itself)
-constexpr int kQNext = 0xF9;  // quad_perm [1,2,3,3]: lane q reads lane q+1 (lane 3 itself)
-constexpr int kQX1 = 0xB1;    // [1,0,3,2]
-constexpr int kQX2 = 0x4E;    // [2,3,0,1]
-template <int K>
-constexpr int kQB = K * 0x55;  // broadcast lane K of the quad
-
-__global__ __launch_bounds__(64 * kTbQuadWaves) __attribute__((amdgpu_waves_per_eu(BCE_TB_QUAD_WPE, BCE_TB_QUAD_WPE))) void tiebreak_quad_kernel(TbArgs a, int64_t n_list, int split_waves) {
-  __shared__ double sBuf[kTbQuadWaves][kTbQuadBuf];
-  __shared__ double sRc[kTbLpmMax + 1];
-  if (threadIdx.x <= (unsigned)kTbLpmMax) sRc[threadIdx.x] = 1.0 / (double)(threadIdx.x ? threadIdx.x : 1);
-  __syncthreads();
-  const int lane = lane_id();
-  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int q = lane & 3, mk = lane >> 2;
-  double* const row = sBuf[wv] + kTbQuadRow * mk;
-  int32_t* const irow = reinterpret_cast<int32_t*>(row);
-  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t tile = wave; tile * 64 < n_list; tile += nwaves) {
-    // the 64-market tile is FULL (every market 32 agents, 16-B aligned) exactly as PART 1 decides
-    const int64_t li = tile * 64 + lane;
-    const bool has = li < n_list;
-    const int64_t o0 = has ? a.offsets[li] : 0, o1 = has ? a.offsets[li + 1] : 0;
-    const int64_t B = ((int64_t)__builtin_amdgcn_readfirstlane((int)(o0 >> 32)) << 32) |
-                      (uint32_t)__builtin_amdgcn_readfirstlane((int)o0);
-    const bool full = ballot(has && o1 - o0 == kTbLpmMax) == ~0ull && (B & 1) == 0;
-    if (!full) {
-      if (lane == 0) atomicMax(&a.split[tile % split_waves], a.ticket);
-      continue;
-    }
-#pragma unroll 1
-    for (int sub = 0; sub < 4; ++sub) {
-      const int64_t m = tile * 64 + 16 * sub + mk;       // (STAGED tiles: market = list index)
-      const int64_t base = B + 512 * sub + 8 * lane;      // this lane's first agent
-      const int t0 = 8 * q;                               // its position in the market
-      auto load8 = [&](const double* src, double (&v)[8]) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const double2 x = tb_ld2(src + base + 2 * k);
-          v[2 * k] = x.x;
-          v[2 * k + 1] = x.y;
-        }
-      };
-      auto store8 = [&](double* dst, const double (&v)[8]) {
-        if (((uintptr_t)dst & 15) == 0) {  // (uniform) outputs may be only 8-B aligned
-#pragma unroll
-          for (int k = 0; k < 4; ++k) tb_st2(dst + base + 2 * k, v[2 * k], v[2 * k + 1]);
-        } else {
-#pragma unroll
-          for (int k = 0; k < 8; ++k) dst[base + k] = v[k];
-        }
-      };
-      auto store8_i32 = [&](int32_t* dst, const int (&v)[8]) {  // (4-B alignment only)
-#pragma unroll
-        for (int k = 0; k < 8; ++k) dst[base + k] = v[k];
-      };
-      // row slots 8q..8q+7 (this lane's) as 16-B LDS accesses
-      auto row_put8 = [&](const double (&v)[8]) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) row[t0 + i] = v[i];
-      };
-      auto row_get8 = [&](double (&v)[8]) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = row[t0 + i];
-      };
-
-      // ---- 1. keys, leaders, first-seen ordinals ----------------------------------------
-      double kp[8];
-      {
-        double pr[8];
-        load8(a.pred, pr);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          bool slow;
-          kp[i] = py_round_nd_fast(pr[i], a.rscale, a.rinv, a.rthresh, slow);
-          if (ballot(slow)) kp[i] = slow ? py_round_nd_sel(pr[i], a.rscale, a.rinv, a.rthresh) : kp[i];
-        }
-      }
-      wave_sync_lds();  // the previous sub-tile's readers of the row are done
-      row_put8(kp);
-      wave_sync_lds();
-      int first[8];  // the smallest s <= t with key[s] == key[t] (t itself when none: NaN)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) first[i] = t0 + i;
-#pragma unroll
-      for (int s2 = 31; s2 >= 0; --s2) {
-        const double ks = row[s2];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) first[i] = (s2 - i <= t0 && key_eq(ks, kp[i])) ? s2 : first[i];
-      }
-      unsigned lb = 0;  // own leaders (bit i: agent t0 + i)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) lb |= (first[i] == t0 + i) ? (1u << i) : 0u;
-      const unsigned L = q_dpp<kQB<0>>(lb) | (q_dpp<kQB<1>>(lb) << 8) | (q_dpp<kQB<2>>(lb) << 16) |
-                         (q_dpp<kQB<3>>(lb) << 24);
-      const int ng = __popc(L);
-      unsigned u[8];
-      double gk[8];  // each own agent's group key: its leader's rounded key (tiebreak.py:54-55)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const unsigned ord = (unsigned)__popc(L & ((1u << first[i]) - 1u));
-        u[i] = (ord << 5) | (unsigned)(t0 + i);
-        gk[i] = row[first[i]];
-      }
-      if (a.g_of) {
-        int go[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) go[i] = (int)(u[i] >> 5);
-        store8_i32(a.g_of, go);
-      }
-      // ---- 2. bitonic sort of the 32 (ordinal, agent) keys over the quad -----------------
-#pragma unroll
-      for (int k = 2; k <= 32; k <<= 1) {
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1) {
-          if (j >= 8) {  // partner in lane q ^ (j / 8)
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-              const unsigned v = (j == 8) ? q_dpp<kQX1>(u[i]) : q_dpp<kQX2>(u[i]);
-              const int p = t0 + i;
-              const bool asc = (p & k) == 0, lower = (p & j) == 0;
-              const unsigned mn = u[i] < v ? u[i] : v, mx = u[i] < v ? v : u[i];
-              u[i] = (asc == lower) ? mn : mx;
-            }
-          } else {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-              if (i & j) continue;
-              const int p = t0 + i;
-              const bool asc = (p & k) == 0;
-              const unsigned x = u[i], y = u[i | j];
-              const unsigned mn = x < y ? x : y, mx = x < y ? y : x;
-              u[i] = asc ? mn : mx;
-              u[i | j] = asc ? mx : mn;
-            }
-          }
-        }
-      }
-      // run boundaries: bit i of stb / enb = a run starts / ends at sorted position t0 + i
-      unsigned stb = 0, enb = 0;
-      {
-        const unsigned prv = q_dpp<kQPrev>(u[7]), nxt = q_dpp<kQNext>(u[0]);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const unsigned g = u[i] >> 5;
-          const bool st = (i == 0) ? (q == 0 || (prv >> 5) != g) : ((u[i - 1] >> 5) != g);
-          const bool en = (i == 7) ? (q == 3 || (nxt >> 5) != g) : ((u[i + 1] >> 5) != g);
-          stb |= st ? (1u << i) : 0u;
-          enb |= en ? (1u << i) : 0u;
-        }
-      }
-      // group keys in sorted order (the row now takes the group keys of the own agents)
-      double ks[8];
-      wave_sync_lds();
-      row_put8(gk);
-      wave_sync_lds();
-#pragma unroll
-      for (int i = 0; i < 8; ++i) ks[i] = row[u[i] & 31u];
-      // per-group outputs: value of the run ending at sorted position t0 + i -> slot g
-      auto flush_groups = [&](double* dst, const double (&v)[8]) {
-        wave_sync_lds();
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          if ((enb >> i) & 1u) row[u[i] >> 5] = v[i];
-        wave_sync_lds();
-        double o[8];
-        row_get8(o);
-        store8(dst, o);
-      };
-      if (a.g_key) flush_groups(a.g_key, ks);
-      // ---- 3. ordered walks: the lane's 8 sorted positions, seeded by the previous lane --
-      // weight sums and counts per group (tiebreak.py:60, sum from int 0 == +0.0 + w)
-      double dens[8];
-      int cnt[8];
-      {
-        double w[8], wv8[8];
-        load8(a.weight, w);
-        wave_sync_lds();
-        row_put8(w);
-        wave_sync_lds();
-#pragma unroll
-        for (int i = 0; i < 8; ++i) wv8[i] = row[u[i] & 31u];
-        double tot[8];
-        double ctot = 0.0;
-        int ccnt = 0;
-#pragma unroll
-        for (int pass = 0; pass < 4; ++pass) {
-          double t = ctot;
-          int c = ccnt;
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const bool st = (stb >> i) & 1u;
-            t = (st ? 0.0 : t) + wv8[i];
-            c = (st ? 0 : c) + 1;
-            tot[i] = t;
-            cnt[i] = c;
-          }
-          ctot = q_dpp<kQPrev>(t);
-          ccnt = (int)q_dpp<kQPrev>((unsigned)c);
-        }
-#pragma unroll
-        for (int i = 0; i < 8; ++i) dens[i] = tb_div_small(tot[i], cnt[i], sRc);
-      }
-      if (a.g_count) {
-        wave_sync_lds();
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          if ((enb >> i) & 1u) irow[u[i] >> 5] = cnt[i];
-        wave_sync_lds();
-        int co[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) co[i] = irow[t0 + i];
-        store8_i32(a.g_count, co);
-      }
-      if (a.g_density) flush_groups(a.g_density, dens);
-      // max reliability per group (builtin max: the first maximum), and the winner / tie fold
-      // over the groups in dict order (tiebreak.py:113-133), both seeded across the quad
-      double bd = 0.0, bm = 0.0, bk = 0.0;
-      bool tie = false;
-      {
-        double r[8], rv[8], mxs[8];
-        load8(a.rel, r);
-        wave_sync_lds();
-        row_put8(r);
-        wave_sync_lds();
-#pragma unroll
-        for (int i = 0; i < 8; ++i) rv[i] = row[u[i] & 31u];
-        double cmx = 0.0, cbd = 0.0, cbm = 0.0, cbk = 0.0;
-        bool ctie = false;
-#pragma unroll
-        for (int pass = 0; pass < 4; ++pass) {
-          double mxv = cmx, d_ = cbd, m_ = cbm, k_ = cbk;
-          bool ti = ctie;
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const unsigned g = u[i] >> 5;
-            mxv = ((stb >> i) & 1u) ? rv[i] : ((rv[i] > mxv) ? rv[i] : mxv);  // tiebreak.py:62
-            mxs[i] = mxv;
-            const bool en = (enb >> i) & 1u;
-            const bool same = (dens[i] == d_) && (mxv == m_);
-            const bool better = (g == 0) | tb_better_sel(dens[i], mxv, ks[i], d_, m_, k_);
-            ti = en ? (better ? ((g != 0) && same) : (ti || same)) : ti;
-            const bool upd = en && better;
-            d_ = upd ? dens[i] : d_;
-            m_ = upd ? mxv : m_;
-            k_ = upd ? ks[i] : k_;
-          }
-          cmx = q_dpp<kQPrev>(mxv);
-          cbd = q_dpp<kQPrev>(d_);
-          cbm = q_dpp<kQPrev>(m_);
-          cbk = q_dpp<kQPrev>(k_);
-          ctie = q_dpp<kQPrev>((unsigned)ti) != 0u;
-          bd = d_;
-          bm = m_;
-          bk = k_;
-          tie = ti;
-        }
-        if (a.g_maxrel) flush_groups(a.g_maxrel, mxs);
-      }
-      // variance (tiebreak.py:108-110: mean, then the squares summed in input order) and the
-      // per-group mean confidences (tiebreak.py:61)
-      double variance;
-      {
-        double c[8];
-        load8(a.conf, c);
-        double ccs = 0.0, cs = 0.0;
-#pragma unroll
-        for (int pass = 0; pass < 4; ++pass) {
-          double x = (q == 0) ? 0.0 : ccs;
-#pragma unroll
-          for (int i = 0; i < 8; ++i) x += c[i];
-          cs = x;
-          ccs = q_dpp<kQPrev>(x);
-        }
-        const double mean = q_dpp<kQB<3>>(cs) / (double)kTbLpmMax;
-        double sq[8];
-        bool anyslow = false;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          bool ok;
-          sq[i] = bce_pow::pow2_fast(c[i] - mean, ok);
-          anyslow |= !ok;
-        }
-        if (ballot(anyslow)) {
-#pragma unroll 1
-          for (int i = 0; i < 8; ++i) {
-            bool ok;
-            (void)bce_pow::pow2_fast(c[i] - mean, ok);
-            if (!ok) sq[i] = tb_pow2_full(c[i] - mean);
-          }
-        }
-        double cvs = 0.0, vs = 0.0;
-#pragma unroll
-        for (int pass = 0; pass < 4; ++pass) {
-          double x = (q == 0) ? 0.0 : cvs;
-#pragma unroll
-          for (int i = 0; i < 8; ++i) x += sq[i];
-          vs = x;
-          cvs = q_dpp<kQPrev>(x);
-        }
-        variance = q_dpp<kQB<3>>(vs) / (double)kTbLpmMax;
-        if (a.g_avgconf) {
-          double cv[8], avg[8];
-          wave_sync_lds();
-          row_put8(c);
-          wave_sync_lds();
-#pragma unroll
-          for (int i = 0; i < 8; ++i) cv[i] = row[u[i] & 31u];
-          double cg = 0.0;
-#pragma unroll
-          for (int pass = 0; pass < 4; ++pass) {
-            double x = cg;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-              x = (((stb >> i) & 1u) ? 0.0 : x) + cv[i];
-              avg[i] = x;
-            }
-            cg = q_dpp<kQPrev>(x);
-          }
-#pragma unroll
-          for (int i = 0; i < 8; ++i) avg[i] = tb_div_small(avg[i], cnt[i], sRc);
-          flush_groups(a.g_avgconf, avg);
-        }
-      }
-      // the winner state is final in lane 3 (the last group's fold)
-      const double win = q_dpp<kQB<3>>(bk);
-      const bool tie3 = q_dpp<kQB<3>>((unsigned)tie) != 0u;
-      (void)bd;
-      (void)bm;
-      if (q == 0) {
-        a.winner[m] = win;
-        a.label[m] = (ng == 1) ? BCE_TB_UNANIMOUS : tie3 ? BCE_TB_PREDICTION_VALUE_SMALLEST : BCE_TB_WEIGHT_DENSITY;
-        a.n_groups[m] = ng;
-        a.variance[m] = variance;
-      }
-    }
-  }
-}
+// (Round 6, VERDICT r05 item 4: FULL tiles on a quad of lanes per market -- 4 lanes x 8 agents,
+// 16 markets per wave, rows loaded straight into registers, O(n^2) leader search over the LDS row,
+// a quad-wide bitonic sort, every ordered chain run as four seeded passes -- parity green but
+// 1.46-1.49 ms against 0.663-0.665 ms for this lane-per-market FULL body on the same box
+// (profiles/r06p/; 128 VGPRs, 4 waves per SIMD): the per-market sequential chains cost four
+// instruction slots per market instead of one and the leader search 2.7x the compares.  Removed;
+// the kernel is in git history, commit "Tie-break: quad-of-lanes-per-market FULL kernel".)
 
 template <bool IN_LDS, bool EXOTIC>
 __global__ __launch_bounds__(kTbThreads) void tiebreak_block_kernel(TbArgs a, const int32_t* list,
@@ -1689,18 +1311,8 @@ static int launch_tb_short(const TbArgs& a, const int32_t* market_list, int64_t 
         set_error("tiebreak: no device split words");
         return BCE_EHIP;
       }
-      if (kTbQuad) {  // FULL tiles on a quad of lanes per market, its own (higher-occupancy) grid
-        const void* qf = reinterpret_cast<const void*>(&tiebreak_quad_kernel);
-        const int64_t qcap = (int64_t)cu_count() * blocks_per_cu(qf, 64 * kTbQuadWaves, 0, 1, "tiebreak_quad_kernel");
-        int64_t qblocks = (tiles + kTbQuadWaves - 1) / kTbQuadWaves;
-        if (qblocks > qcap) qblocks = qcap;
-        hipLaunchKernelGGL(tiebreak_quad_kernel, dim3((int)qblocks), dim3(64 * kTbQuadWaves), 0, st, b, nl,
-                           (int)(blocks * kTbLpmWaves));
-        if (int rc = check_launch("tiebreak_quad_kernel")) return rc;
-      } else {
-        hipLaunchKernelGGL((tiebreak_lpm_kernel<true, false, 1>), grid, block, 0, st, b, market_list, nl, fault_word());
-        if (int rc = check_launch("tiebreak_lpm_kernel<full>")) return rc;
-      }
+      hipLaunchKernelGGL((tiebreak_lpm_kernel<true, false, 1>), grid, block, 0, st, b, market_list, nl, fault_word());
+      if (int rc = check_launch("tiebreak_lpm_kernel<full>")) return rc;
       hipLaunchKernelGGL((tiebreak_lpm_kernel<true, false, 2>), grid, block, 0, st, b, market_list, nl, fault_word());
     } else {
       hipLaunchKernelGGL((tiebreak_lpm_kernel<true, EXOTIC>), grid, block, 0, st, a, market_list, nl, fault_word());
