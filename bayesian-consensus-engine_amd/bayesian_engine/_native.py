@@ -65,6 +65,9 @@ _SIGS = {
     "bce_consensus_scratch_bytes": (C.c_int64, [_vp, _vp, _vp]),
     "bce_plan_bins_device": (C.c_int, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
     "bce_plan_device_scratch_bytes": (_i64, [_i64]),
+    "bce_plan_bins_device_async": (C.c_int, [_vp, _i64, _vp, _vp, _vp, _i64, _vp]),
+    "bce_consensus_planned_device": (C.c_int, [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _i32, _vp, _vp, _i32,
+                                               _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "bce_consensus_planned": (C.c_int, [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _i32, _vp, _vp, _i32,
                                         _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
     "bce_decay_view": (C.c_int, [_i64, _vp, _vp, _vp, _i64, _f64, _f64, _f64, _vp, _vp]),

@@ -227,8 +227,12 @@ def consensus(offsets: torch.Tensor, sid: torch.Tensor, prob: torch.Tensor, tabl
     """core.compute_consensus for every CSR market (+ the validation range check).
 
     Pass ``max_len`` (<= 64: one launch, no planning) or a prebuilt :class:`Plan` for
-    ragged batches; with neither, a plan is built on the GPU (:meth:`Plan.build_device`, one
-    stream synchronisation).  A caller that reruns the same CSR should build the Plan once.
+    ragged batches.  Without a plan, the batch is planned on the GPU: with a ``max_len`` bound
+    of 65..4096 entirely on the device, with no host synchronisation
+    (bce_plan_bins_device_async + bce_consensus_planned_device; a market longer than the bound
+    raises the device fault word), else by :meth:`Plan.build_device` (one stream
+    synchronisation returns the bin boundaries).  A caller that reruns the same CSR should
+    build the Plan once.
 
     ``mode="fast"`` (fixed-order trees, <= 1e-9 absolute vs the reference order) is
     deterministic per call shape but not invariant to batch composition: a small call (e.g. a
@@ -255,6 +259,21 @@ def consensus(offsets: torch.Tensor, sid: torch.Tensor, prob: torch.Tensor, tabl
     if plan is None and max_len is not None and 0 < max_len <= 64:
         rc = L.bce_consensus_csr(*common, N.ptr(None), 0, int(max_len), md, *outs, N.stream(dev))
         N.check(rc, "bce_consensus_csr")
+        if check:
+            N.check_faults(dev, "consensus")
+        return res
+    if plan is None and max_len is not None and 64 < max_len <= 4096 and table.n <= (1 << 25):
+        # a fresh ragged batch under the caller's bound: planned on the device and launched with
+        # no host synchronisation (bce_plan_bins_device_async + bce_consensus_planned_device)
+        order = torch.empty(max(M, 1), dtype=torch.int32, device=dev)
+        sb = int(L.bce_plan_device_scratch_bytes(M))
+        work = torch.empty(max(sb, 1), dtype=torch.uint8, device=dev)
+        bins = torch.empty(N.NBINS + 1, dtype=torch.int64, device=dev)
+        st = N.stream(dev)
+        N.check(L.bce_plan_bins_device_async(N.ptr(offsets), M, N.ptr(order), N.ptr(bins), N.ptr(work), sb, st),
+                "bce_plan_bins_device_async")
+        N.check(L.bce_consensus_planned_device(*common, N.ptr(order), N.ptr(bins), md, *outs, st),
+                "bce_consensus_planned_device")
         if check:
             N.check_faults(dev, "consensus")
         return res

@@ -171,6 +171,7 @@ static const char* fault_text(int code) {
     case kFaultTooLong: return "consensus: a market is longer than the launch's max_len (left unprocessed)";
     case kFaultSpinChain: return "consensus_wide_kernel: exact-mode chain hand-off timed out";
     case 6: return "tiebreak round(): rounded value too large to represent";
+    case kFaultOffsets: return "plan_bins: offsets not monotone (device planner; nothing was computed)";
     default: return "unknown device fault";
   }
 }

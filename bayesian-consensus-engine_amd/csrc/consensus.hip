@@ -42,6 +42,7 @@ namespace bce {
 template <int G, int TM>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kSegWPE, 8)))
 void consensus_seg_kernel(ConsArgs a) {
+  dev_range(a);
   static_assert(G == 8 || G == 16 || G == 32 || G == 64, "segment width");
   constexpr int SPR = kWave / G;   // segments (markets) per round
   constexpr int R = TM / SPR;      // rounds per tile
@@ -314,6 +315,7 @@ __device__ __forceinline__ void dma4(const void* g, void* lds) {
 
 template <int G>
 __global__ __launch_bounds__(64) void consensus_lpm_kernel(ConsArgs a) {
+  dev_range(a);
   static_assert(G == 8 || G == 16 || G == 32, "lane-per-market widths");
   constexpr int LOGG = (G == 8) ? 3 : (G == 16) ? 4 : 5;
   constexpr int SST = G + 1;       // sid / usid row stride (dwords): conflict-free b32 reads
@@ -1777,15 +1779,18 @@ __device__ __forceinline__ T wave_max_u64(T v) {
 }
 
 // Pass PASS digit counts of chunk blockIdx.x -> counts[digit * nchunks + chunk].  Pass 0 reads
-// the offsets (striped: coalesced) and also fills PlanInfo (bin counts, longest markets, the
-// first decreasing offset).
-template <int PASS>
+// the offsets (striped: coalesced) and also writes the chunk's record for PlanInfo (bin counts,
+// longest market, longest > 4096 market, first decreasing offset) -- no global atomics: the
+// pass-0 scan reduces the records (800 same-address atomicMax per call cost ~10 us).
+constexpr int kPlanRec = 16;  // int64 per chunk record: bins[13], max_len, long_max, badrev
+template <int PASS, bool CM>
 __global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(const int64_t* __restrict__ offsets, int64_t M,
                                                                   const uint16_t* __restrict__ keys_in,
                                                                   int32_t* __restrict__ counts, int64_t nchunks,
-                                                                  PlanInfo* info) {
+                                                                  int64_t* __restrict__ crec) {
   __shared__ int cnt[kPlanDigits];
   __shared__ int bincnt[BCE_NBINS];
+  __shared__ unsigned long long wmax[kPlanThreads / kWave][3];
   const int t = threadIdx.x;
   const int64_t c = blockIdx.x;
   if (t < kPlanDigits) cnt[t] = 0;
@@ -1812,53 +1817,139 @@ __global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(const int64_t*
       atomicAdd(&cnt[(key >> (6 * PASS)) & (kPlanDigits - 1)], 1);
     }
   }
-  __syncthreads();
-  if (t < kPlanDigits) counts[(int64_t)t * nchunks + c] = cnt[t];
   if constexpr (PASS == 0) {
-    if (t < BCE_NBINS && bincnt[t]) atomicAdd(&info->bins[t], (unsigned long long)bincnt[t]);
     mx = wave_max_u64(mx);
     lmx = wave_max_u64(lmx);
     badrev = wave_max_u64(badrev);
     if (lane_id() == 0) {
-      if (mx) atomicMax(&info->max_len, mx);
-      if (lmx) atomicMax(&info->long_max, lmx);
-      if (badrev) atomicMax(&info->badrev, badrev);
+      wmax[t / kWave][0] = mx;
+      wmax[t / kWave][1] = lmx;
+      wmax[t / kWave][2] = badrev;
+    }
+  }
+  __syncthreads();
+  if (t < kPlanDigits) counts[CM ? c * kPlanDigits + t : (int64_t)t * nchunks + c] = cnt[t];
+  if constexpr (PASS == 0) {
+    int64_t* r = crec + c * kPlanRec;
+    if (t < BCE_NBINS) r[t] = bincnt[t];
+    if (t >= BCE_NBINS && t < BCE_NBINS + 3) {
+      unsigned long long v = 0;
+      for (int w = 0; w < kPlanThreads / kWave; ++w) v = wmax[w][t - BCE_NBINS] > v ? wmax[w][t - BCE_NBINS] : v;
+      r[t] = (int64_t)v;
     }
   }
 }
 
-// In-place exclusive scan of counts[0..E) by one workgroup (E = 64 x chunks: small).
-__global__ __launch_bounds__(kPlanScanThreads) void plan_scan_kernel(int32_t* __restrict__ counts, int64_t E) {
-  __shared__ int64_t wsum[kPlanScanThreads / kWave];
-  const int t = threadIdx.x;
-  const int64_t per = (E + kPlanScanThreads - 1) / kPlanScanThreads;
-  const int64_t a = t * per, b = (a + per < E) ? a + per : E;
-  int64_t s = 0;
-  for (int64_t i = a; i < b; ++i) s += counts[i];
-  // block exclusive scan of s
-  int64_t inc = s;
+// Reduce the count pass's chunk records into PlanInfo; with bin_start_dev also the device bin
+// boundaries and the device-driven faults (decreasing offsets: every bin empty + kFaultOffsets;
+// raise_long: a market > 4096 raises kFaultTooLong).  Called by one whole workgroup.
+__device__ __forceinline__ void plan_reduce_info(const int64_t* __restrict__ crec, int64_t nchunks, PlanInfo* info,
+                                                 int64_t* bin_start_dev, int* fault, int raise_long,
+                                                 unsigned long long* sacc, int t, int nthreads) {
+  if (t < BCE_NBINS + 3) sacc[t] = 0;
+  __syncthreads();
+  unsigned long long b[BCE_NBINS] = {}, m0 = 0, m1 = 0, m2 = 0;
+  for (int64_t c = t; c < nchunks; c += nthreads) {
+    const int64_t* r = crec + c * kPlanRec;
 #pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    const int64_t o = __shfl_up(inc, d);
-    if (lane_id() >= d) inc += o;
+    for (int k = 0; k < BCE_NBINS; ++k) b[k] += (unsigned long long)r[k];
+    m0 = (unsigned long long)r[BCE_NBINS] > m0 ? (unsigned long long)r[BCE_NBINS] : m0;
+    m1 = (unsigned long long)r[BCE_NBINS + 1] > m1 ? (unsigned long long)r[BCE_NBINS + 1] : m1;
+    m2 = (unsigned long long)r[BCE_NBINS + 2] > m2 ? (unsigned long long)r[BCE_NBINS + 2] : m2;
   }
-  const int w = t / kWave;
-  if (lane_id() == kWave - 1) wsum[w] = inc;
+  // wave reductions first: one LDS atomic per wave and counter
+#pragma unroll
+  for (int k = 0; k < BCE_NBINS; ++k) {
+    unsigned long long v = b[k];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += (unsigned long long)__shfl_xor((long long)v, o);
+    b[k] = v;
+  }
+  m0 = wave_max_u64(m0);
+  m1 = wave_max_u64(m1);
+  m2 = wave_max_u64(m2);
+  if (lane_id() == 0) {
+#pragma unroll
+    for (int k = 0; k < BCE_NBINS; ++k)
+      if (b[k]) atomicAdd(&sacc[k], b[k]);
+    if (m0) atomicMax(&sacc[BCE_NBINS], m0);
+    if (m1) atomicMax(&sacc[BCE_NBINS + 1], m1);
+    if (m2) atomicMax(&sacc[BCE_NBINS + 2], m2);
+  }
   __syncthreads();
   if (t == 0) {
-    int64_t run = 0;
-    for (int k = 0; k < kPlanScanThreads / kWave; ++k) {
-      const int64_t v = wsum[k];
-      wsum[k] = run;
-      run += v;
+    for (int k = 0; k < BCE_NBINS; ++k) info->bins[k] = sacc[k];
+    info->max_len = sacc[BCE_NBINS];
+    info->long_max = sacc[BCE_NBINS + 1];
+    info->badrev = sacc[BCE_NBINS + 2];
+    if (bin_start_dev) {
+      const bool bad = sacc[BCE_NBINS + 2] != 0;
+      int64_t run = 0;
+      bin_start_dev[0] = 0;
+      for (int k = 0; k < BCE_NBINS; ++k) {
+        run += bad ? 0 : (int64_t)sacc[k];
+        bin_start_dev[k + 1] = run;
+      }
+      if (fault && bad) atomicCAS(fault, 0, kFaultOffsets);
+      if (fault && !bad && raise_long && sacc[BCE_NBINS - 1]) atomicCAS(fault, 0, kFaultTooLong);
     }
   }
-  __syncthreads();
-  int64_t run = wsum[w] + inc - s;
-  for (int64_t i = a; i < b; ++i) {
-    const int v = counts[i];
-    counts[i] = (int32_t)run;
-    run += v;
+}
+
+// In-place exclusive scan of counts[0..E) by one workgroup (E = 64 x chunks), in tiles of 8
+// consecutive counts per thread (the loads of a tile in flight together).  INFO (pass 0): also
+// reduces the chunk records into PlanInfo and, with bin_start_dev, writes the device bin
+// boundaries (decreasing offsets: every bin empty + kFaultOffsets; raise_long: a market > 4096
+// raises kFaultTooLong -- the device-driven launch does not compute those).
+template <bool INFO>
+__global__ __launch_bounds__(kPlanScanThreads) void plan_scan_kernel(int32_t* __restrict__ counts, int64_t E,
+                                                                     const int64_t* __restrict__ crec, int64_t nchunks,
+                                                                     PlanInfo* info, int64_t* bin_start_dev, int* fault,
+                                                                     int raise_long) {
+  constexpr int V = 8;
+  constexpr int NW = kPlanScanThreads / kWave;
+  __shared__ int64_t wsum[NW];
+  __shared__ int64_t tile_total;
+  __shared__ unsigned long long sacc[BCE_NBINS + 3];
+  const int t = threadIdx.x;
+  const int w = t / kWave;
+  if constexpr (INFO) plan_reduce_info(crec, nchunks, info, bin_start_dev, fault, raise_long, sacc, t, kPlanScanThreads);
+  int64_t carry = 0;
+  for (int64_t base = 0; base < E; base += (int64_t)kPlanScanThreads * V) {
+    const int64_t i0 = base + (int64_t)t * V;
+    int v[V];
+    int64_t s = 0;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      v[k] = (i0 + k < E) ? counts[i0 + k] : 0;
+      s += v[k];
+    }
+    int64_t inc = s;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const int64_t o = __shfl_up(inc, d);
+      if (lane_id() >= d) inc += o;
+    }
+    if (lane_id() == kWave - 1) wsum[w] = inc;
+    __syncthreads();
+    if (t == 0) {
+      int64_t run = 0;
+      for (int k = 0; k < NW; ++k) {
+        const int64_t x = wsum[k];
+        wsum[k] = run;
+        run += x;
+      }
+      tile_total = run;
+    }
+    __syncthreads();
+    int64_t run = carry + wsum[w] + inc - s;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      if (i0 + k < E) counts[i0 + k] = (int32_t)run;
+      run += v[k];
+    }
+    carry += tile_total;
+    __syncthreads();  // wsum / tile_total are rewritten by the next tile
   }
 }
 
@@ -1866,17 +1957,58 @@ __global__ __launch_bounds__(kPlanScanThreads) void plan_scan_kernel(int32_t* __
 // 4t..4t+3 of the chunk (blocked: thread order == input order); mat[t][d] counts thread t's
 // items of digit d, and its exclusive scan in (d, t) order gives every item its rank among the
 // chunk's items of smaller digit or equal digit and earlier position.
-template <int PASS>
+// INKB (<= kPlanInkbMax chunks): the counts are chunk-major [chunk][digit] and every workgroup
+// derives its own 64 bases from all of them (a wave reads one 256-B chunk row per step), so no
+// scan launch sits between the passes; PASS 0 runs one extra workgroup that reduces the chunk
+// records (plan_reduce_info) alongside.  Otherwise `base` is the digit-major exclusive scan of plan_scan_kernel.
+constexpr int64_t kPlanInkbMax = 1024;
+template <int PASS, bool INKB>
 __global__ __launch_bounds__(kPlanThreads) void plan_scatter_kernel(const int64_t* __restrict__ offsets, int64_t M,
                                                                     const uint16_t* __restrict__ keys_in,
                                                                     const int32_t* __restrict__ idx_in,
                                                                     const int32_t* __restrict__ base, int64_t nchunks,
                                                                     uint16_t* __restrict__ keys_out,
-                                                                    int32_t* __restrict__ idx_out) {
+                                                                    int32_t* __restrict__ idx_out,
+                                                                    const int64_t* __restrict__ crec, PlanInfo* info,
+                                                                    int64_t* bin_start_dev, int* fault, int raise_long) {
   __shared__ int mat[kPlanThreads * kPlanDigits];  // [t][d], 64 KB
   __shared__ int part[kPlanThreads];
+  __shared__ int sTot[kPlanDigits], sPre[kPlanDigits];
+  __shared__ unsigned long long sacc[BCE_NBINS + 3];
   const int t = threadIdx.x;
   const int64_t c = blockIdx.x;
+  if constexpr (INKB) {
+    if (PASS == 0 && c == nchunks) {  // the extra workgroup of pass 0: PlanInfo, in parallel with the scatter
+      plan_reduce_info(crec, nchunks, info, bin_start_dev, fault, raise_long, sacc, t, kPlanThreads);
+      return;
+    }
+    if (t < kPlanDigits) {
+      sTot[t] = 0;
+      sPre[t] = 0;
+    }
+    __syncthreads();
+    const int dd = t & (kPlanDigits - 1), qq = t / kPlanDigits;
+    int tot = 0, pre = 0;
+#pragma unroll 4
+    for (int64_t c2 = qq; c2 < nchunks; c2 += kPlanThreads / kPlanDigits) {
+      const int v = base[c2 * kPlanDigits + dd];
+      tot += v;
+      pre += (c2 < c) ? v : 0;
+    }
+    atomicAdd(&sTot[dd], tot);
+    atomicAdd(&sPre[dd], pre);
+    __syncthreads();
+    if (t < kWave) {  // exclusive scan of the digit totals (one wave, lane = digit), + this chunk's prefix
+      const int v = sTot[t];
+      int inc = v;
+#pragma unroll
+      for (int o = 1; o < kWave; o <<= 1) {
+        const int y = __shfl_up(inc, o);
+        if (lane_id() >= o) inc += y;
+      }
+      sPre[t] += inc - v;
+    }
+  }
 #pragma unroll 8
   for (int j = 0; j < kPlanDigits; ++j) mat[j * kPlanThreads + t] = 0;
   int key[kPlanPer], idx[kPlanPer], before[kPlanPer];
@@ -1944,7 +2076,8 @@ __global__ __launch_bounds__(kPlanThreads) void plan_scatter_kernel(const int64_
   for (int k = 0; k < kPlanPer; ++k) {
     if (key[k] >= 0) {
       const int dg = (key[k] >> (6 * PASS)) & (kPlanDigits - 1);
-      const int64_t pos = (int64_t)base[(int64_t)dg * nchunks + c] + (row[dg] - mat[dg]) + before[k];
+      const int64_t pos = (INKB ? (int64_t)sPre[dg] : (int64_t)base[(int64_t)dg * nchunks + c]) + (row[dg] - mat[dg]) +
+                          before[k];
       if constexpr (PASS == 0) keys_out[pos] = (uint16_t)key[k];
       idx_out[pos] = idx[k];
     }
@@ -1953,12 +2086,14 @@ __global__ __launch_bounds__(kPlanThreads) void plan_scatter_kernel(const int64_
 }  // namespace bce
 
 static int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
+static int plan_device_launch(const int64_t* offsets, int64_t n_markets, int32_t* order, void* scratch,
+                              hipStream_t st, PlanInfo** info_out, int64_t* bin_start_dev, int raise_long);
 
 extern "C" int64_t bce_plan_device_scratch_bytes(int64_t n_markets) {
   if (n_markets <= 0) return 0;
   const int64_t chunks = (n_markets + kPlanChunk - 1) / kPlanChunk;
   return align256(sizeof(PlanInfo)) + align256(2 * n_markets) + align256(4 * n_markets) +
-         align256(4 * kPlanDigits * chunks);
+         align256(4 * kPlanDigits * chunks) + align256(8 * kPlanRec * chunks);
 }
 
 extern "C" int bce_plan_bins_device(const int64_t* offsets, int64_t n_markets, int32_t* order,
@@ -1975,26 +2110,8 @@ extern "C" int bce_plan_bins_device(const int64_t* offsets, int64_t n_markets, i
   BCE_REQUIRE(offsets && order && scratch, "plan_bins_device: NULL argument");
   BCE_REQUIRE(scratch_bytes >= bce_plan_device_scratch_bytes(n_markets), "plan_bins_device: scratch too small");
   hipStream_t st = as_stream(stream);
-  const int64_t chunks = (n_markets + kPlanChunk - 1) / kPlanChunk;
-  char* p = static_cast<char*>(scratch);
-  PlanInfo* info = reinterpret_cast<PlanInfo*>(p);
-  p += align256(sizeof(PlanInfo));
-  uint16_t* keys = reinterpret_cast<uint16_t*>(p);
-  p += align256(2 * n_markets);
-  int32_t* idx = reinterpret_cast<int32_t*>(p);
-  p += align256(4 * n_markets);
-  int32_t* counts = reinterpret_cast<int32_t*>(p);
-  BCE_HIP(hipMemsetAsync(info, 0, sizeof(PlanInfo), st));
-  const dim3 g((unsigned)chunks), blk(kPlanThreads);
-  hipLaunchKernelGGL((plan_count_kernel<0>), g, blk, 0, st, offsets, n_markets, nullptr, counts, chunks, info);
-  hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(kPlanScanThreads), 0, st, counts, kPlanDigits * chunks);
-  hipLaunchKernelGGL((plan_scatter_kernel<0>), g, blk, 0, st, offsets, n_markets, nullptr, nullptr, counts, chunks,
-                     keys, idx);
-  hipLaunchKernelGGL((plan_count_kernel<1>), g, blk, 0, st, offsets, n_markets, keys, counts, chunks, info);
-  hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(kPlanScanThreads), 0, st, counts, kPlanDigits * chunks);
-  hipLaunchKernelGGL((plan_scatter_kernel<1>), g, blk, 0, st, offsets, n_markets, keys, idx, counts, chunks,
-                     nullptr, order);
-  int rc = check_launch("plan_bins_device");
+  PlanInfo* info = nullptr;
+  int rc = plan_device_launch(offsets, n_markets, order, scratch, st, &info, nullptr, 0);
   if (rc) return rc;
   PlanInfo h{};
   BCE_HIP(hipMemcpyAsync(&h, info, sizeof h, hipMemcpyDeviceToHost, st));
@@ -2009,6 +2126,62 @@ extern "C" int bce_plan_bins_device(const int64_t* offsets, int64_t n_markets, i
     *long_scratch_bytes_host = (int64_t)grid * 4 * next_pow2((int64_t)h.long_max) * 8;
   }
   return BCE_OK;
+}
+
+
+static int plan_device_launch(const int64_t* offsets, int64_t n_markets, int32_t* order, void* scratch,
+                              hipStream_t st, PlanInfo** info_out, int64_t* bin_start_dev, int raise_long) {
+  const int64_t chunks = (n_markets + kPlanChunk - 1) / kPlanChunk;
+  char* p = static_cast<char*>(scratch);
+  PlanInfo* info = reinterpret_cast<PlanInfo*>(p);
+  p += align256(sizeof(PlanInfo));
+  uint16_t* keys = reinterpret_cast<uint16_t*>(p);
+  p += align256(2 * n_markets);
+  int32_t* idx = reinterpret_cast<int32_t*>(p);
+  p += align256(4 * n_markets);
+  int32_t* counts = reinterpret_cast<int32_t*>(p);
+  p += align256(4 * kPlanDigits * chunks);
+  int64_t* crec = reinterpret_cast<int64_t*>(p);
+  const dim3 g((unsigned)chunks), blk(kPlanThreads), sg(1), sblk(kPlanScanThreads);
+  int* fw = fault_word();
+  if (chunks <= kPlanInkbMax) {  // 4 launches: bases derived inside the scatter kernels
+    hipLaunchKernelGGL((plan_count_kernel<0, true>), g, blk, 0, st, offsets, n_markets, nullptr, counts, chunks, crec);
+    hipLaunchKernelGGL((plan_scatter_kernel<0, true>), dim3((unsigned)chunks + 1), blk, 0, st, offsets, n_markets,
+                       nullptr, nullptr, counts, chunks, keys, idx, crec, info, bin_start_dev, fw, raise_long);
+    hipLaunchKernelGGL((plan_count_kernel<1, true>), g, blk, 0, st, offsets, n_markets, keys, counts, chunks, nullptr);
+    hipLaunchKernelGGL((plan_scatter_kernel<1, true>), g, blk, 0, st, offsets, n_markets, keys, idx, counts, chunks,
+                       nullptr, order, nullptr, nullptr, nullptr, nullptr, 0);
+  } else {  // huge batches: one digit-major scan launch per pass
+    hipLaunchKernelGGL((plan_count_kernel<0, false>), g, blk, 0, st, offsets, n_markets, nullptr, counts, chunks, crec);
+    hipLaunchKernelGGL((plan_scan_kernel<true>), sg, sblk, 0, st, counts, kPlanDigits * chunks, crec, chunks, info,
+                       bin_start_dev, fw, raise_long);
+    hipLaunchKernelGGL((plan_scatter_kernel<0, false>), g, blk, 0, st, offsets, n_markets, nullptr, nullptr, counts,
+                       chunks, keys, idx, nullptr, nullptr, nullptr, nullptr, 0);
+    hipLaunchKernelGGL((plan_count_kernel<1, false>), g, blk, 0, st, offsets, n_markets, keys, counts, chunks, nullptr);
+    hipLaunchKernelGGL((plan_scan_kernel<false>), sg, sblk, 0, st, counts, kPlanDigits * chunks, nullptr, (int64_t)0,
+                       nullptr, nullptr, nullptr, 0);
+    hipLaunchKernelGGL((plan_scatter_kernel<1, false>), g, blk, 0, st, offsets, n_markets, keys, idx, counts, chunks,
+                       nullptr, order, nullptr, nullptr, nullptr, nullptr, 0);
+  }
+  *info_out = info;
+  return check_launch("plan_bins_device");
+}
+
+extern "C" int bce_plan_bins_device_async(const int64_t* offsets, int64_t n_markets, int32_t* order,
+                                          int64_t* bin_start_dev, void* scratch, int64_t scratch_bytes,
+                                          void* stream) {
+  BCE_REQUIRE(n_markets >= 0 && n_markets < ((int64_t)1 << 31), "plan_bins_device_async: bad n_markets %lld",
+              (long long)n_markets);
+  BCE_REQUIRE(bin_start_dev, "plan_bins_device_async: bin_start_dev NULL");
+  hipStream_t st = as_stream(stream);
+  if (n_markets == 0) {
+    BCE_HIP(hipMemsetAsync(bin_start_dev, 0, (BCE_NBINS + 1) * sizeof(int64_t), st));
+    return BCE_OK;
+  }
+  BCE_REQUIRE(offsets && order && scratch, "plan_bins_device_async: NULL argument");
+  BCE_REQUIRE(scratch_bytes >= bce_plan_device_scratch_bytes(n_markets), "plan_bins_device_async: scratch too small");
+  PlanInfo* info = nullptr;
+  return plan_device_launch(offsets, n_markets, order, scratch, st, &info, bin_start_dev, 1);
 }
 
 extern "C" int bce_consensus_planned(const int64_t* offsets, int64_t n_markets, const int32_t* sid,
@@ -2126,6 +2299,69 @@ extern "C" int bce_consensus_planned(const int64_t* offsets, int64_t n_markets, 
     if (rc) break;
   }
   const int rj = side_join(st, 1);  // join even after a failed launch: st must not run ahead
+  if (!rc) rc = rj;
+  return rc;
+}
+
+// The planned launch driven by device bin boundaries (bce_plan_bins_device_async): no host
+// sync between planning and consensus.  Every bin's kernel is launched with its resident grid
+// (its market count is not known on the host) and reads its range of the plan order at entry
+// (dev_range); an empty bin's launch exits at once.  The launch structure is the full batch's:
+// EXACT runs the non-power-of-two bins in the launch of the bin above, FAST gives every bin its
+// own launch (no small-call merges: the counts are on the device), longest bins first, bins
+// 0..3 on the side stream.  Markets longer than 4096 are not computed: they raise the device
+// fault word (a caller with such markets uses the host-synchronised plan).
+extern "C" int bce_consensus_planned_device(const int64_t* offsets, int64_t n_markets, const int32_t* sid,
+                                            const double* prob, int64_t n_signals, const double* relconf,
+                                            const uint32_t* present_bits, int32_t n_sources, const int32_t* order,
+                                            const int64_t* bin_start_dev, int32_t mode, double* consensus,
+                                            double* confidence, double* total_weight, int32_t* n_unique,
+                                            int32_t* err_idx, int32_t* usid, double* weight, double* nweight,
+                                            void* stream) {
+  int rc = check_common(offsets, n_markets, sid, prob, relconf, present_bits, n_sources, consensus,
+                        confidence, total_weight, n_unique);
+  if (rc) return rc;
+  if (n_markets == 0) return BCE_OK;
+  BCE_REQUIRE(bin_start_dev && order, "planned_device: missing plan");
+  BCE_REQUIRE(mode == BCE_MODE_EXACT || mode == BCE_MODE_FAST, "planned_device: bad mode %d", mode);
+  BCE_REQUIRE(n_signals == 0 || (sid && prob), "planned_device: sid/prob NULL");
+  hipStream_t st = as_stream(stream);
+  ConsArgs base{};
+  base.offsets = offsets; base.sid = sid; base.prob = prob;
+  base.relconf = reinterpret_cast<const double2*>(relconf); base.pbits = present_bits;
+  base.n_sources = n_sources; base.n_signals = n_signals; base.consensus = consensus; base.confidence = confidence;
+  base.total_weight = total_weight; base.n_unique = n_unique; base.err_idx = err_idx;
+  base.usid = usid; base.weight = weight; base.nweight = nweight; base.mode = mode;
+  base.fault = fault_word();
+  base.spin_cap = spin_cap();
+  base.list = order;           // the whole plan order: each launch's range is read on the device
+  base.n_list = n_markets;     // upper bound: sizes the launch grids
+  base.dev_bins = bin_start_dev;
+  const bool seg_ok = n_sources <= (1 << 25);
+  hipStream_t side = st;
+  std::unique_lock<std::mutex> fork_lock;
+  rc = side_fork(st, 1, &side, &fork_lock);
+  if (rc) return rc;
+  static const int kOrderDev[BCE_NBINS - 1] = {10, 11, 9, 8, 7, 6, 5, 4, 3, 2, 1, 0};
+  for (int oi = 0; oi < BCE_NBINS - 1 && !rc; ++oi) {
+    const int b = kOrderDev[oi];
+    const bool np2 = (b == kBinNp2Lo || b == kBinNp2Hi);
+    if (mode == BCE_MODE_EXACT && np2) continue;  // rides in the launch of the bin above
+    ConsArgs a = base;
+    a.dev_b1 = b;
+    a.dev_b0 = (mode == BCE_MODE_EXACT && (b == kBinNp2Lo + 1 || b == kBinNp2Hi + 1)) ? b - 1 : b;
+    hipStream_t sb = (b <= kPlanSideLast) ? side : st;
+    if (b <= 3 && seg_ok) {
+      static const int lens[4] = {8, 16, 32, 64};
+      rc = launch_seg_for_len(lens[b], a, sb);
+    } else if (b <= 3) {
+      rc = BCE_EUNSUPPORTED;  // (n_sources > 2^25: the long-LDS kernel has no device range)
+      set_error("planned_device: more than 2^25 sources -- use bce_consensus_planned");
+    } else {
+      rc = launch_wide_for_len(kBinMax[b], a, sb);
+    }
+  }
+  const int rj = side_join(st, 1);
   if (!rc) rc = rj;
   return rc;
 }

@@ -37,7 +37,27 @@ struct ConsArgs {
   int* fault;         // device word: set to a kFault* code by a wave that gave up
   int spin_cap;       // bounded waits of the persistent pipe kernel (polls before giving up)
   int32_t tab_rows;   // tab kernel, hybrid table: rows [0, tab_rows) staged in LDS, the rest read from relconf
+  // Device-driven planned launch (bce_consensus_planned_device): the bin boundaries live on the
+  // device (int64[BCE_NBINS + 1]); the kernel takes plan positions [dev_bins[dev_b0],
+  // dev_bins[dev_b1 + 1]) of `list` (the whole plan order), bin dev_b1's markets first when
+  // dev_b0 < dev_b1 (a merged launch, as list_hi / n_hi).  NULL: list / n_list as given.
+  const int64_t* dev_bins;
+  int32_t dev_b0, dev_b1;
 };
+
+// Resolve a device-driven launch's market range at kernel entry (uniform scalar loads).
+__device__ __forceinline__ void dev_range(ConsArgs& a) {
+  if (a.dev_bins) {
+    const int64_t lo = a.dev_bins[a.dev_b0], mid = a.dev_bins[a.dev_b1], hi = a.dev_bins[a.dev_b1 + 1];
+    const int32_t* order = a.list;
+    a.list = order + lo;
+    a.n_list = hi - lo;
+    if (a.dev_b0 != a.dev_b1) {
+      a.list_hi = order + mid;
+      a.n_hi = hi - mid;
+    }
+  }
+}
 
 // Device fault codes (bce_fault_check reports them).
 constexpr int kFaultSpinLoader = 1;   // pipe kernel: loader never saw a slot released
@@ -45,6 +65,7 @@ constexpr int kFaultSpinCompute = 2;  // pipe kernel: compute wave never saw its
 constexpr int kFaultSid = 3;          // a sid >= n_sources (the row read was clamped)
 constexpr int kFaultTooLong = 4;      // a market longer than the launch's max_len (skipped)
 constexpr int kFaultSpinChain = 5;    // wide kernel, exact mode: chain / producer wait timed out
+constexpr int kFaultOffsets = 7;      // device planner: offsets decrease somewhere
 
 constexpr int kBitsLds = 512;  // present bitmask words staged in LDS (S <= 16384)
 

@@ -1042,6 +1042,7 @@ __device__ __forceinline__ void wide_market(const ConsArgs& a, const WideLds<NW,
 // list (one market per workgroup at a time, the next one's loads issued during this one).
 template <int NW, int R, bool FAST, int NN = NW, class KT = unsigned>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WideCfg<NW, R, FAST, NN, KT>::WPE, 8))) void consensus_wide_kernel(ConsArgs a) {
+  dev_range(a);
   using LD = WideLds<NW, R, FAST, NN, KT>;
   __shared__ __attribute__((aligned(16))) unsigned char smem[LD::BYTES];
   const LD L(smem);

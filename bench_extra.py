@@ -299,7 +299,10 @@ def _c3(args, world, rank, barrier, max_over, sum_over):
     def step():
         # fresh: every step plans its batch on the GPU (batch.consensus(plan=None) ->
         # bce_plan_bins_device + one stream synchronisation), as for an incoming batch
-        batch.consensus(d_off, d_sid, d_prob, table, plan=None if fresh else plan, mode=mode, out=res)
+        if fresh:  # planned on the device, no host sync (the caller's bound: C3 markets <= 4096)
+            batch.consensus(d_off, d_sid, d_prob, table, max_len=4096, mode=mode, out=res)
+        else:
+            batch.consensus(d_off, d_sid, d_prob, table, plan=plan, mode=mode, out=res)
 
     def step_other():
         batch.consensus(d_off, d_sid, d_prob, table, plan=plan, mode=other, out=res)
@@ -361,8 +364,9 @@ def _c3(args, world, rank, barrier, max_over, sum_over):
                              "stream launches (plan: one kernel per length bin)",
                    "markets_this_rank": Mloc, "signals_this_rank": n, "unique_per_market_mean": sum_u / max(Mloc, 1),
                    "bins": plan.bin_start.tolist(),
-                   "plan": ("planned on the GPU inside every timed step (bce_plan_bins_device + one sync: a fresh "
-                            "batch)" if fresh else "pre-planned (Plan.build once, outside the timed steps)"),
+                   "plan": ("planned on the GPU inside every timed step, no host sync (bce_plan_bins_device_async + "
+                            "bce_consensus_planned_device: a fresh batch)" if fresh else
+                            "pre-planned (Plan.build once, outside the timed steps)"),
                    "parallelism": f"markets sharded over {world} rank(s), no collective" +
                                   (f" (split: {'sharding.shard_markets_planned, whole length classes per rank' if split == 'planned' else 'sharding.shard_markets, contiguous ranges'})" if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -163,6 +163,22 @@ int bce_plan_bins_device(const int64_t* offsets, int64_t n_markets, int32_t* ord
                          int32_t* max_len_host, int64_t* long_scratch_bytes_host, void* scratch,
                          int64_t scratch_bytes, void* stream);
 int64_t bce_plan_device_scratch_bytes(int64_t n_markets);
+/* The same plan without any host synchronisation: the bin boundaries stay on the device
+ * (bin_start_dev, device int64[BCE_NBINS+1]); decreasing offsets raise the device fault word
+ * (bce_fault_check) and leave every bin empty.  Pair with bce_consensus_planned_device. */
+int bce_plan_bins_device_async(const int64_t* offsets, int64_t n_markets, int32_t* order, int64_t* bin_start_dev,
+                               void* scratch, int64_t scratch_bytes, void* stream);
+/* bce_consensus_planned over a device-resident plan: every bin's kernel reads its range of the
+ * plan order on the device, so planning + consensus of a fresh batch enqueue with no host sync.
+ * Launch structure of a full batch (no small-call merges).  Markets longer than 4096 signals are
+ * not computed and raise the device fault word (use bce_plan_bins_device + bce_consensus_planned
+ * for them); n_sources must be <= 2^25. */
+int bce_consensus_planned_device(const int64_t* offsets, int64_t n_markets, const int32_t* sid, const double* prob,
+                                 int64_t n_signals, const double* relconf, const uint32_t* present_bits,
+                                 int32_t n_sources, const int32_t* order, const int64_t* bin_start_dev,
+                                 int32_t mode, double* consensus, double* confidence, double* total_weight,
+                                 int32_t* n_unique, int32_t* err_idx, int32_t* usid, double* weight,
+                                 double* nweight, void* stream);
 /* Bytes of device scratch bce_consensus_planned needs for the >4096 bin. */
 int64_t bce_consensus_scratch_bytes(const int64_t* offsets_host, const int32_t* order_host,
                                     const int64_t* bin_start_host);
