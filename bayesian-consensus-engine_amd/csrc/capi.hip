@@ -55,11 +55,14 @@ DevCtx* dev_ctx() {
     int* p = nullptr;
     hipError_t e = hipMalloc((void**)&p, sizeof(int));
     if (e == hipSuccess) e = hipMemset(p, 0, sizeof(int));  // synchronous: done before first use
+    // the fork / join events only order the side streams against the caller's stream on this
+    // device: no system-scope fence (each shard step 1.3% shorter, profiles/r06y/)
+    const unsigned evf = hipEventDisableTiming | hipEventDisableSystemFence;
     for (int k = 0; k < kSideStreams; ++k) {
       if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side[k], hipStreamNonBlocking);
-      if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join[k], hipEventDisableTiming);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join[k], evf);
     }
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, evf);
     int* sw = nullptr;
     if (e == hipSuccess) e = hipMalloc((void**)&sw, (size_t)kQueueSlots * kSplitWords * sizeof(int));
     if (e == hipSuccess) e = hipMemset(sw, 0, (size_t)kQueueSlots * kSplitWords * sizeof(int));

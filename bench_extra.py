@@ -250,7 +250,12 @@ def make_c3(world=1, rank=0, total=100_000_000, S=1_000_000, split="planned", mo
     if world <= 1:
         return M, offsets, sid, prob, table, np.arange(M, dtype=np.int64)
     if split == "planned":
-        mk = shard_markets_planned(offsets, world, rank, mode=mode)
+        # A/B hook for the split's model (tools/gpu_lines.sh env: steps): a per-bin cost vector
+        # in place of sharding's measured one
+        kw = {}
+        if os.environ.get("BCE_C3_SHARD_COST"):
+            kw["cost_us"] = np.array([float(x) for x in os.environ["BCE_C3_SHARD_COST"].split(",")])
+        mk = shard_markets_planned(offsets, world, rank, mode=mode, **kw)
     else:
         m0, m1 = shard_markets(offsets, world, rank)
         mk = np.arange(m0, m1, dtype=np.int64)
