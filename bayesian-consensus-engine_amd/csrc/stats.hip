@@ -278,9 +278,8 @@ __global__ __launch_bounds__(256) void reestimate_agreement_votes_kernel(
 // each market's sum in agent order (the MFMA's own rounding of the product; the three zero
 // products are exact).  Accumulator r of lane l then holds D[4 (l >> 4) + r][l & 15], i.e.
 // market m0 + 16 r + (l & 15): lane l's own sum is accumulator l >> 4.  One accumulator
-// chain (the MFMA's dependent issue is hidden by the other waves): 59 VGPRs, 8 waves per
-// SIMD, as many row loads in flight as the exact kernel (kMfmaTwoAcc: even / odd agents on
-// two chains, 80 VGPRs / 6 waves, or 64 with 4 spilled at 8 waves).
+// chain (the MFMA's dependent issue is hidden by the other waves), 8 waves per SIMD, as many
+// row loads in flight as the exact kernel (kMfmaTwoAcc: even / odd agents on two chains).
 // A zero operand times a NaN / inf cell would leak NaN into the other three markets of the
 // column, so the B operand carries non-finite cells as 0 and the lane keeps its own
 // column's flags: a NaN cell makes the consensus NaN (as in every order), any cell outside
@@ -298,11 +297,15 @@ __global__ __launch_bounds__(256) void reestimate_agreement_votes_kernel(
 // profiles/r05f/.)
 typedef double mfma_d4 __attribute__((ext_vector_type(4)));
 constexpr bool kMfmaTwoAcc = false;  // even / odd agent rows on two accumulator chains
-constexpr int kMfmaRows = 8;         // agent rows per batch (the exact kernel: kVoteRows = 16)
-constexpr bool kMfmaPrefetch = true;
+// The exact kernel's load schedule: 16 agent rows per batch, no prefetch of the next batch,
+// 1024-thread workgroups at 8 waves per SIMD (64 VGPRs, 9 spilled): 24.15-24.23 ms per C5
+// iteration against 25.41-25.60 for 8 rows + prefetch on 512-thread workgroups at 6 waves,
+// 8 rows / 1024 threads 25.74-25.76, 16 rows / 512 threads 24.30-24.36 (three interleaved reps,
+// profiles/r06ab1/; the exact pass 23.59-23.88 on that box)
+constexpr int kMfmaRows = 16;        // agent rows per batch (the exact kernel: kVoteRows = 16)
+constexpr bool kMfmaPrefetch = false;
 constexpr int kMfmaWpe = kMfmaPrefetch ? 6 : 8;  // waves per SIMD the VGPR budget allows
-// 8-wave workgroups: three per CU at 6 waves per SIMD (1024 threads would fit only one)
-constexpr int kMfmaBlock = 512;
+constexpr int kMfmaBlock = 1024;
 
 __global__ __launch_bounds__(256) void reestimate_total_kernel(const double* __restrict__ w, int64_t A,
                                                                double* __restrict__ total_fast,
