@@ -612,15 +612,15 @@ def reestimate(P: torch.Tensor, iters: int, w0: float = 0.5, w: Optional[torch.T
 
     Each round reads P once: the consensus pass records every cell's vote as one bit and the
     agreement pass counts from those bits (bce_reestimate_consensus_votes /
-    bce_reestimate_agreement_votes; A*ceil(M/64)*8 bytes of scratch).  ``mode="fast"``
-    runs the same exact agent-order kernel: it already streams P at the HBM rate, and the
-    matrix-core form measured slower, so the exact sums are also the
-    fastest ones within FAST's 1e-9.  ``mode="mfma"`` runs the consensus pass on the matrix
-    cores (bce_reestimate_consensus_votes_mfma: consensus within 4*A*2^-53, votes and
-    agreement counts identical to exact) -- the config-5 MFMA form the north star reports
-    utilisation for.  Its summation order needs every weight finite and >= 0; the library
-    checks that on the device and runs the exact kernel for an iteration whose weights
-    break it."""
+    bce_reestimate_agreement_votes; A*ceil(M/64)*8 bytes of scratch).  ``mode="exact"`` sums
+    in agent order on the vector ALUs (bit-identical to the reference); ``mode="fast"`` runs the
+    same kernel -- it streams P at the HBM rate and is the fastest form.  ``mode="mfma"`` runs
+    the consensus pass on the matrix cores (bce_reestimate_consensus_votes_mfma,
+    v_mfma_f64_4x4x4_4b_f64: consensus within 4*A*2^-53, votes, agreement counts and weights
+    identical to exact) -- the config-5 MFMA contraction, 1.3-1.8% behind the vector pass
+    (DESIGN.md §4.6).  Its summation order needs every weight finite and >= 0; the library
+    checks that on the device and runs the exact kernel for an iteration whose weights break
+    it."""
     L = N.require_gpu()
     A, M = P.shape
     dev = P.device

@@ -14,6 +14,8 @@
 //                          (P >= 0.5) as one bit, 64 markets per word, plus the consensus
 //                          votes and resolved masks per word; pass 2 then counts agreement
 //                          from the bits (A*M/8 bytes) instead of re-reading P (8*A*M).
+#include <type_traits>
+
 #include "bce_device.hpp"
 #include "bce_internal.hpp"
 
@@ -296,6 +298,24 @@ __global__ __launch_bounds__(256) void reestimate_agreement_votes_kernel(
 // the exact kernel's 23.2-23.6; round 5's transposed variant of it took 28.7 ms,
 // profiles/r05f/.)
 typedef double mfma_d4 __attribute__((ext_vector_type(4)));
+// kMfma4x4: v_mfma_f64_4x4x4_4b_f64 instead -- four 4x4x4 blocks; lane l = 16 r + 4 b + c holds
+// A[i = c][k = r], B[k = r][j = c] and D[i = r][j = c] of block b (probed on the GPU: an A lane
+// one-hot reaches D lanes 16 i + 4 b + j from B lanes 16 k + 4 b + j).  With A on the same
+// diagonal as the 16x16x4 form ((l & 3) == (l >> 4): i == k) lane l's D accumulates w_a times
+// its OWN cell: one f64 accumulator per lane (2 VGPRs instead of 8), a shorter dependent chain
+constexpr bool kMfma4x4 = true;
+using mfma_acc = std::conditional_t<kMfma4x4, double, mfma_d4>;
+__device__ __forceinline__ double mfma_f64(double a, double b, double c) {
+  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ mfma_d4 mfma_f64(double a, double b, mfma_d4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+// the lane's own market sum: the 4x4x4 accumulator, or accumulator r = lane >> 4 of the 16x16x4
+__device__ __forceinline__ double mfma_own(double acc, int) { return acc; }
+__device__ __forceinline__ double mfma_own(mfma_d4 acc, int r) {
+  return (r == 0) ? acc[0] : (r == 1) ? acc[1] : (r == 2) ? acc[2] : acc[3];
+}
 constexpr bool kMfmaTwoAcc = false;  // even / odd agent rows on two accumulator chains
 // The exact kernel's load schedule: 16 agent rows per batch, no prefetch of the next batch,
 // 1024-thread workgroups at 8 waves per SIMD (64 VGPRs, 9 spilled): 24.15-24.23 ms per C5
@@ -351,20 +371,21 @@ __global__ __launch_bounds__(kMfmaBlock) __attribute__((amdgpu_waves_per_eu(kMfm
   const int64_t k = m >> 6;
   if ((k << 6) >= M) return;  // whole wave past the last market (wave-uniform)
   const bool in = m < M;
-  const bool diag = (lane & 3) == (lane >> 4);  // A[i][k] with i = lane & 15, k = lane >> 4
+  // A[i][k] with i = lane & 15, k = lane >> 4 (16x16x4) or i = lane & 3, k = lane >> 4 (4x4x4)
+  const bool diag = (lane & 3) == (lane >> 4);
   const double* col = P + (in ? m : 0);  // every lane's column address is valid: loads unconditional
   unsigned long long* vb = vote_bits + k * A;
-  mfma_d4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+  mfma_acc acc0{}, acc1{};
   bool odd = false, hnan = false;
   const double dsel = diag ? 1.0 : 0.0;  // A = w_a * dsel: w_a or +0 (w finite >= 0)
   // b = the cell clamped to [0, 1], NaN -> 0 (IEEE maxNum): equal to v exactly for a cell in
   // [0, 1] (-0.0 compares equal), so b != v marks every other cell, NaN included; and
   // b >= 0.5 iff v >= 0.5 for every v (the vote)
-  auto row = [&](double v, double wq, mfma_d4& acc) {
+  auto row = [&](double v, double wq, mfma_acc& acc) {
     const double b = __builtin_fmin(__builtin_fmax(v, 0.0), 1.0);
     odd = odd || (b != v);
     hnan = hnan || (v != v);
-    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(wq * dsel, b, acc, 0, 0, 0);
+    acc = mfma_f64(wq * dsel, b, acc);
   };
   int64_t a = 0;
   // kMfmaPrefetch: the next batch's rows are issued before this batch's MFMA chain (whose
@@ -405,8 +426,8 @@ __global__ __launch_bounds__(kMfmaBlock) __attribute__((amdgpu_waves_per_eu(kMfm
     if (lane == 0) vb[a] = bq;
   }
   const int r = lane >> 4;
-  const double s0 = (r == 0) ? acc0[0] : (r == 1) ? acc0[1] : (r == 2) ? acc0[2] : acc0[3];
-  const double s1 = !kMfmaTwoAcc ? 0.0 : (r == 0) ? acc1[0] : (r == 1) ? acc1[1] : (r == 2) ? acc1[2] : acc1[3];
+  const double s0 = mfma_own(acc0, r);
+  const double s1 = kMfmaTwoAcc ? mfma_own(acc1, r) : 0.0;
   const double total = *total_fast;
   const bool isnull = (total == 0.0);  // w >= 0: zero in every order iff every weight is zero
   const double c = isnull ? 0.0 : hnan ? __builtin_nan("") : (kMfmaTwoAcc ? s0 + s1 : s0) / total;

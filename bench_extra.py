@@ -539,10 +539,10 @@ def _c5(args, world, rank, barrier, max_over, sum_over):
     ev_k = []
     nb = int(L.bce_reestimate_mfma_scratch_bytes(Mloc))
     scratch = torch.empty((nb + 7) // 8, dtype=torch.int64, device=dev)
-    # "fast" runs the exact kernel (batch.reestimate: it streams P at the HBM rate, the
-    # matrix-core form measured slower); "mfma" = w^T P on the matrix cores, timed beside
-    # the main mode for the MFMA utilisation report
-    mode = {"m": args.mode or "exact"}
+    # the line's mode: the agent-order vector pass ("exact"; "fast" runs it too, batch.reestimate)
+    # unless --mode mfma (w^T P on the matrix cores: votes and counts identical, consensus within
+    # 4*A*2^-53); the other form is timed beside it for the MFMA utilisation report
+    mode = {"m": "mfma" if args.mode == "mfma" else "exact"}
 
     def pass1():
         if mode["m"] == "mfma":  # w^T P on the matrix cores (near-0.5 markets redone exactly)
@@ -613,18 +613,19 @@ def _c5(args, world, rank, barrier, max_over, sum_over):
                      "kernel": "reestimate_consensus_votes + reestimate_agreement_votes (one iteration)",
                      "bytes_per_launch": bytes_iter, "avg_launch_ms": kern * 1e3,
                      f"{other['mode']}_mode": other,
-                     "mfma": {"used": "mode='mfma' pass 1 (v_mfma_f64_16x16x4_f64, one agent row of 64 "
-                                      "markets per MFMA on a diagonal A operand)",
+                     "mfma": {"used": "mode='mfma' pass 1 (v_mfma_f64_4x4x4_4b_f64, one agent row of 64 "
+                                      "markets per MFMA on a diagonal A operand: each lane's D accumulates "
+                                      "its own cell)",
                               "mode_of_this_line": main_mode,
                               "mfma_ms_per_iteration": t_mfma * 1e3,
                               "contraction_tflops_mfma": 2.0 * A * Mloc / t_mfma / 1e12,
                               "fp64_matrix_peak_tflops": 78.6,
                               "utilisation_useful": 2.0 * A * Mloc / t_mfma / 1e12 / 78.6,
-                              "utilisation_issued": 32.0 * A * Mloc / t_mfma / 1e12 / 78.6,
+                              "utilisation_issued": 8.0 * A * Mloc / t_mfma / 1e12 / 78.6,
                               "why": "w^T P is a GEMV at 0.25 flop/B: both forms stream P at the HBM rate; the "
-                                     "MFMA form issues 16x the useful flops (3 of 4 products per D element are "
-                                     "zeros, every D row 4x redundant) and measured slower, so mode='fast' runs "
-                                     "the exact agent-order kernel"}},
+                                     "MFMA form issues 4x the useful flops (3 of 4 products per D element are "
+                                     "zeros) and runs 1.3-1.8% behind the agent-order VALU pass, so mode='fast' "
+                                     "runs the VALU kernel"}},
         "cpu_baseline": _cpu_c5(P, args) if rank == 0 and world == 1 else None,
         "parity_vs_oracle": parity,
     }

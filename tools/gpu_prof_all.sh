@@ -14,11 +14,13 @@ bash tools/gpu_profile.sh c3 consensus signals_this_rank=100000000 steps_total=7
 python3 tools/pmc_summary.py span gpurun_out/prof_c3/stats "bce::" 12 > gpurun_out/prof_c3/step_span.json && \
 bash tools/gpu_profile.sh c3S10M consensus signals_this_rank=100000000 sources=10000000 steps_total=7 stream_read_bytes=1201627112 -- --config c3 --single-mode --c3-sources 10000000 && \
 bash tools/gpu_profile.sh tb "tiebreak_lpm_kernel<true, false, 1, 32, false>" markets=1000000 -- --config tb && \
-bash tools/gpu_profile.sh c5 reestimate_consensus_votes_kernel markets_this_rank=1000000 mode=exact -- --config c5 --steps 2 --warmup 1 --single-mode && \
-python3 tools/pmc_summary.py stats gpurun_out/prof_c5/stats reestimate_agreement_votes_kernel > gpurun_out/prof_c5/stats_agreement.json && \
-python3 tools/pmc_summary.py pmc gpurun_out/prof_c5/fetch gpurun_out/prof_c5/write reestimate_agreement_votes_kernel \
-  gpurun_out/prof_c5/pmc_agreement.json markets_this_rank=1000000 && \
-bash tools/gpu_profile.sh c5mfma reestimate_votes_mfma_kernel markets_this_rank=1000000 mode=mfma -- --config c5 --mode mfma --steps 2 --warmup 1 --single-mode && \
+for c5 in c5:reestimate_consensus_votes_kernel:exact c5mfma:reestimate_votes_mfma_kernel:mfma; do
+  IFS=: read -r tag kern md <<< "$c5"
+  bash tools/gpu_profile.sh $tag $kern markets_this_rank=1000000 mode=$md -- --config c5 --mode $md --steps 2 --warmup 1 --single-mode && \
+  python3 tools/pmc_summary.py stats gpurun_out/prof_$tag/stats reestimate_agreement_votes_kernel > gpurun_out/prof_$tag/stats_agreement.json && \
+  python3 tools/pmc_summary.py pmc gpurun_out/prof_$tag/fetch gpurun_out/prof_$tag/write reestimate_agreement_votes_kernel \
+    gpurun_out/prof_$tag/pmc_agreement.json markets_this_rank=1000000 || exit $?
+done && \
 bash tools/gpu_profile.sh ns namespace_resolve_kernel sources=10000000 -- --config ns && \
 bash tools/gpu_profile.sh agg aggregate_kernel groups=10000 -- --config agg --single-mode && \
 python3 tools/roofline_check.py gpurun_out > gpurun_out/roofline_check.txt && \
