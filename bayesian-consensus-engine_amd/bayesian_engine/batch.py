@@ -391,7 +391,7 @@ class TiePlan:
     buckets: Optional[list]  # [(device int32 list, max_len)], or None: contiguous tiles
 
 
-# relative cost of a 64-market tile, measured (profiles/r05f/, 1M markets): contiguous FULL
+# relative cost of a 64-market tile, measured (profiles/archive/r05f/, 1M markets): contiguous FULL
 # (every market 32 agents: 42 ns per tile) / contiguous ragged (the general 32-position body:
 # 46 ns) / gathered buckets of 8 / 16 / 32 positions (20 / 40 / 70 ns).  The lane kernels are
 # latency-bound by their stage -> compute -> flush phases, so fewer positions per lane save

@@ -51,11 +51,11 @@ __device__ __forceinline__ double key_f64(uint64_t k) {
 // One workgroup per group (no per-CU cap): -15% against 8 looping workgroups per CU.
 // kAggWpe: minimum waves per SIMD the VGPR budget must allow.  The compiler's own choice, 90
 // VGPRs, holds five groups per CU; 6 (78 VGPRs, 2 spilled) holds six -- as many as the 25.7 KB
-// of LDS allows: 0.0860 vs 0.0943 ms (+median 0.173 vs 0.193, profiles/r04w/).  Dropping the
+// of LDS allows: 0.0860 vs 0.0943 ms (+median 0.173 vs 0.193, profiles/archive/r04w/).  Dropping the
 // cons*conf LDS array so more groups fit (the product formed in the chain) ran 2x slower
-// (0.19-0.22 ms, profiles/r04v/; code reverted): the chains' loop is the critical path.
+// (0.19-0.22 ms, profiles/archive/r04v/; code reverted): the chains' loop is the critical path.
 // Round 5: the same pipelining in C++ (4-term batches, the next read during the adds) ran 0.117
-// vs 0.0858 ms (profiles/r05o/; the compiler waited on every batch, 8- or 16-term batches
+// vs 0.0858 ms (profiles/archive/r05o/; the compiler waited on every batch, 8- or 16-term batches
 // spilled 35 / 71 VGPRs) -- hence the asm chain below.
 constexpr int kAggWpe = 6;
 // The last chunk's ordered chains (kAggChainAsm): acc += src[0..ce) left to right in asm, four
@@ -64,7 +64,7 @@ constexpr int kAggWpe = 6;
 // loop-carried batch behind an lgkmcnt(0)).  Run after the chunk loop, where the next chunk's
 // gather registers are dead; reads may run 16 past ce (inside the kernel's LDS).  f4 line:
 // 0.0723 ms against 0.0858 without it, 0.0764 with two batches, 0.0728 with six
-// (profiles/r05za/, r05zb/).
+// (profiles/archive/r05za/, archive/r05zb/).
 constexpr bool kAggChainAsm = true;
 __device__ __forceinline__ void agg_chain_asm(double& acc, const double* src, int ce) {
   const int steps = ce / 16;

@@ -2213,8 +2213,8 @@ extern "C" int bce_consensus_planned(const int64_t* offsets, int64_t n_markets, 
   // on C3: 1.73 -> 1.65 ms; moving wide bins to the side stream too, or forking every bin
   // over 2-8 streams, was slower (profiles/r02_c3_plan_streams.jsonl); so was dealing every
   // bin over 2 or 4 streams with the resident grid shared out by estimated work (round 5,
-  // profiles/r05b/: one 8th of C3 0.233 -> 0.294 / 0.307 ms), and a small call's 65..1024
-  // launches on a second side stream (0.2188 -> 0.2325 ms, profiles/r05f/).
+  // profiles/archive/r05b/: one 8th of C3 0.233 -> 0.294 / 0.307 ms), and a small call's 65..1024
+  // launches on a second side stream (0.2188 -> 0.2325 ms, profiles/archive/r05f/).
   hipStream_t side = st;
   std::unique_lock<std::mutex> fork_lock;
   constexpr int side_last = kPlanSideLast;

@@ -58,7 +58,7 @@ namespace {
 constexpr int kTabWaves = 8;  // waves per workgroup (two per SIMD); one workgroup per CU (LDS-bound)
 // The next tile's metadata read at the top of a tile (true) or after its walk (false: no spill
 // stores left in the tile loop, but 1.7% slower -- 0.2143-0.2146 vs 0.2109-0.2129 ms,
-// profiles/r05d/)
+// profiles/archive/r05d/)
 constexpr bool kTabMetaEarly = true;
 constexpr int kPL = 8;         // lanes per 128-B piece of a market row (16 B each)
 constexpr int kLB = 3;         // log2 kPL

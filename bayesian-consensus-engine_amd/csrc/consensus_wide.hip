@@ -536,7 +536,7 @@ __device__ __forceinline__ void chain_add(double& acc, const double* src, int ce
 }
 // (four 4-term batches in fixed registers v[96, 127], each reloaded 16 terms ahead right after
 // its adds; six batches -- 24-term steps, 48 fixed VGPRs -- spilled 22 VGPRs in the 8-wave
-// kernel and ran C3 exact 2.00 vs 1.90 ms, profiles/r05r/)
+// kernel and ran C3 exact 2.00 vs 1.90 ms, profiles/archive/r05r/)
 __device__ __forceinline__ void chain_add_deep(double& acc, const double* src, int ce) {
   const int steps = ce / 16;
   const int nfull = steps * 16;
@@ -1141,7 +1141,7 @@ int launch_wide(const ConsArgs& a, hipStream_t st) {
 // 2048 / 4096-key network on 3 / 6 waves
 // (Round 5: a market shard's 513..1024 / 1025..2048 bins on 4 / 8 waves with R = 4 -- half the
 // latency per market, more rounds -- made one 8th of C3 slower, 0.2069-0.2072 -> 0.2274-0.2300
-// ms, profiles/r05g/; removed.)
+// ms, profiles/archive/r05g/; removed.)
 template <bool FAST>
 int launch_wide_mode(int64_t max_len, const ConsArgs& a, hipStream_t st) {
   if (max_len <= 128) return launch_wide<1, 2, FAST>(a, st);

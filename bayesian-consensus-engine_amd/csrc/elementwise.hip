@@ -213,7 +213,7 @@ struct NsArgs {
 };
 
 // nontemporal hints on the namespace pass (every byte is read / written once): both on 0.1665
-// ms, off 0.1752 (10M sources x 3 scopes, profiles/r04t/)
+// ms, off 0.1752 (10M sources x 3 scopes, profiles/archive/r04t/)
 constexpr bool kNsNtLoad = true;
 constexpr bool kNsNtStore = true;
 template <typename T>

@@ -171,8 +171,8 @@ __device__ __forceinline__ unsigned long long writelane_u64(unsigned long long v
   return ((unsigned long long)hi << 32) | lo;
 }
 // kVoteBlock: threads per workgroup -- its waves read neighbouring 512-B pieces of each row:
-// 1024 threads 22.74-22.98 ms per C5 iteration, 512 23.60-23.66, 256 23.61-23.79 (profiles/r05zh/,
-// r05zi/)
+// 1024 threads 22.74-22.98 ms per C5 iteration, 512 23.60-23.66, 256 23.61-23.79 (profiles/archive/r05zh/,
+// archive/r05zi/)
 constexpr int kVoteBlock = 1024;
 constexpr bool kVoteXcd = true;
 __global__ __launch_bounds__(kVoteBlock) void reestimate_consensus_votes_kernel(
@@ -296,7 +296,7 @@ __global__ __launch_bounds__(256) void reestimate_agreement_votes_kernel(
 // (Rounds 3-4 used A = w broadcast over 16 rows and B = a 4-agent x 16-market block --
 // 128-B row pieces and a 16-bit regrouping of four ballots per word, 25.0-26.0 ms against
 // the exact kernel's 23.2-23.6; round 5's transposed variant of it took 28.7 ms,
-// profiles/r05f/.)
+// profiles/archive/r05f/.)
 typedef double mfma_d4 __attribute__((ext_vector_type(4)));
 // kMfma4x4: v_mfma_f64_4x4x4_4b_f64 instead -- four 4x4x4 blocks; lane l = 16 r + 4 b + c holds
 // A[i = c][k = r], B[k = r][j = c] and D[i = r][j = c] of block b (probed on the GPU: an A lane

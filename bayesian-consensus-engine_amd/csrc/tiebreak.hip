@@ -260,23 +260,23 @@ constexpr int kTbStageIt = 64 * kTbLpmMax / 128;  // 16-B loads per lane for a f
 constexpr int kTbStageBatch = 4;                  // of them in flight together (2 x 8 VGPRs each)
 // A STAGED tile's arrays reach LDS as 16-B loads into registers, kTbStageBatch in flight, then
 // ds_writes (two workgroups of four waves per CU).  LDS-DMA staging into the one buffer (1.070 vs
-// 0.849-0.866 ms, profiles/r04f/) and two DMA-filled buffers per wave (one workgroup per CU:
-// 1.316 ms, profiles/r04e/) were measured and removed.
+// 0.849-0.866 ms, profiles/archive/r04f/) and two DMA-filled buffers per wave (one workgroup per CU:
+// 1.316 ms, profiles/archive/r04e/) were measured and removed.
 
 __device__ __forceinline__ int tb_pad(int i) { return i + (i >> 5); }
 constexpr bool kTbFullKeysInLds = true;  // FULL tiles: sort (ordinal, agent) alone, keys via LDS
 constexpr int kTbDump = 64;
 // FULL tiles: 16-B loads per lane in flight while staging the predictions / confidences and the
 // weights / reliabilities (8 for the latter spills ~10 VGPRs around those stages and still
-// wins: 0.662 vs 0.688 ms with stage()'s 4, profiles/r04q/)
+// wins: 0.662 vs 0.688 ms with stage()'s 4, profiles/archive/r04q/)
 constexpr int kTbFullBatchPC = 8;
 constexpr int kTbFullBatchWR = 8;
 constexpr bool kTbPrefetchMeta = true;
 // (FULL tiles, measured and removed: the next array's first batch issued before the phase's
-// output flushes -- 36 spilled VGPRs, 0.712-0.716 vs 0.664 ms, profiles/r04aa/; dword touches of
-// the next phase's array -- -0.5% time for +27% FETCH_SIZE, profiles/r04k/, r04m/.)
+// output flushes -- 36 spilled VGPRs, 0.712-0.716 vs 0.664 ms, profiles/archive/r04aa/; dword touches of
+// the next phase's array -- -0.5% time for +27% FETCH_SIZE, profiles/archive/r04k/, archive/r04m/.)
 // nontemporal hints on the staged input loads / the flushed output stores (both off: 0.727-0.730
-// ms vs 0.712 for the 1M x 32 line, profiles/r04j/)
+// ms vs 0.712 for the 1M x 32 line, profiles/archive/r04j/)
 constexpr bool kTbNtLoad = true;
 constexpr bool kTbNtStore = true;
 typedef double tb_d2 __attribute__((ext_vector_type(2)));

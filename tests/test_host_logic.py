@@ -278,7 +278,7 @@ def test_markstein_quotients_match_ieee_division(tmp_path):
 
 def test_tiebreak_plan_buckets_by_measured_tile_costs():
     """batch.tiebreak_plan (host only): buckets of <= 8 / 9..16 / 17..32 agents exactly when
-    they cost less than contiguous tiles by the measured per-tile costs (profiles/r05f/): a
+    they cost less than contiguous tiles by the measured per-tile costs (profiles/archive/r05f/): a
     uniform 1..32 ragged batch and a uniform 32 batch stay contiguous, a batch of short markets
     is bucketed, a batch with a market past 32 agents is never bucketed; every market lands in
     exactly one bucket."""

@@ -31,7 +31,7 @@ OUT = tab_variants.OUT
 # Round 5: the all-bins team kernel, the rotated sorted-probability layout (kWideSwz) and the
 # tie-break's LDS-DMA staging (kTbStageMode 1/2), pre-issued batches (kTbPreBatch) and next-array
 # touches (kTbTouchNext) were removed from csrc/ (verdict r04 item 7); their A/Bs are recorded in
-# DESIGN.md §4.2 / §4.9 and profiles/r04c, r04e, r04f, r04k, r04m, r04aa.
+# DESIGN.md §4.2 / §4.9 and profiles/archive/r04c, r04e, r04f, r04k, r04m, r04aa.
 VARIANTS = {
     "wbase": [],
     # small planned calls without the bin merges / merging below 3 resident rounds (shipped: 6)
