@@ -265,6 +265,7 @@ constexpr int kTbStageBatch = 4;                  // of them in flight together 
 
 __device__ __forceinline__ int tb_pad(int i) { return i + (i >> 5); }
 constexpr bool kTbFullKeysInLds = true;  // FULL tiles: sort (ordinal, agent) alone, keys via LDS
+constexpr bool kTbGeneralKeysInLds = true;  // the staged general body likewise
 constexpr int kTbDump = 64;
 // FULL tiles: 16-B loads per lane in flight while staging the predictions / confidences and the
 // weights / reliabilities (8 for the latter spills ~10 VGPRs around those stages and still
@@ -870,7 +871,20 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
         if constexpr (STAGED) flush_i32(a.g_of);
       }
     }
-    oem_sort_kv(u, kp);
+    // STAGED (kTbGeneralKeysInLds): as the FULL body, only the 32-bit (ordinal, agent) keys go
+    // through the network; the rounded keys wait in the lane's row (the predictions are
+    // consumed) and each sorted position reads its run head's key back
+    if constexpr (STAGED && kTbGeneralKeysInLds) {
+      wave_sync_lds();  // the row's readers (keys, g_of flush) are done
+      const unsigned vm3 = tb_bits(vm);
+#pragma unroll
+      for (int t = 0; t < NP; ++t)
+        if (vbit(vm3, t)) buf[tb_pad(lrow + t)] = kp[t];
+      wave_sync_lds();
+      oem_sort(u);
+    } else {
+      oem_sort_kv(u, kp);
+    }
     // run boundaries from the sorted keys alone (invalid positions hold 0xFFFFFFFF, sorted
     // last: the last valid position ends its run, no invalid position ends one)
     unsigned stm = 1u, enm = (u[NP - 1] != 0xFFFFFFFFu) ? (1u << (NP - 1)) : 0u;
@@ -883,8 +897,19 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     enm &= vm;
     // every member carries its run head's key: a group's dict key is its FIRST member's
     // rounded prediction (tiebreak.py:54-55), and -0.0 / 0.0 share a group with different bits
+    if constexpr (STAGED && kTbGeneralKeysInLds) {
+      // (an invalid position's head index is clamped into the lane's row: never used)
+      unsigned ht = u[0] & (unsigned)(NP - 1);
+      kp[0] = buf[tb_pad(lrow + (int)ht)];
 #pragma unroll
-    for (int p = 1; p < NP; ++p) kp[p] = vbit(stm, p) ? kp[p] : kp[p - 1];
+      for (int p = 1; p < NP; ++p) {
+        ht = vbit(stm, p) ? (u[p] & (unsigned)(NP - 1)) : ht;
+        kp[p] = buf[tb_pad(lrow + (int)ht)];
+      }
+    } else {
+#pragma unroll
+      for (int p = 1; p < NP; ++p) kp[p] = vbit(stm, p) ? kp[p] : kp[p - 1];
+    }
 
     // ---- 2. group keys and counts (registers only) ------------------------------------------
     if (a.g_key || a.g_count) {
