@@ -923,10 +923,13 @@ def _tb(args, world, rank, barrier, max_over, sum_over):
                                 f"tb: {M} markets x {L} agents, precision 6"), "groups_per_market_mean": sum_g / M,
                    "parallelism": f"markets sharded over {world} rank(s), no collective"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None if ragged else _pmc("pmc_tb.json", markets=M),
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": (_pmc("pmc_tb_ragged.json", markets=M, ragged=1) if ragged else
+                                 _pmc("pmc_tb.json", markets=M)),
                      "kernel": ("tiebreak_lpm_kernel<gather, 8 / 16 / 32 positions> (length buckets)"
                                 if plan is not None and plan.buckets is not None else
-                                "tiebreak_lpm_kernel" if L <= 32 else "tiebreak_wave_kernel"),
+                                "tiebreak_lpm_kernel (contiguous tiles: FULL + general body)" if L <= 32
+                                else "tiebreak_wave_kernel"),
                      "bytes_per_launch": bytes_step, "avg_launch_ms": per * 1e3},
         "cpu_baseline": cpu_line,
         "parity_vs_oracle": parity,

@@ -14,6 +14,7 @@ bash tools/gpu_profile.sh c3 consensus signals_this_rank=100000000 steps_total=7
 python3 tools/pmc_summary.py span gpurun_out/prof_c3/stats "bce::" 12 > gpurun_out/prof_c3/step_span.json && \
 bash tools/gpu_profile.sh c3S10M consensus signals_this_rank=100000000 sources=10000000 steps_total=7 stream_read_bytes=1201627112 -- --config c3 --single-mode --c3-sources 10000000 && \
 bash tools/gpu_profile.sh tb "tiebreak_lpm_kernel<true, false, 1, 32, false>" markets=1000000 -- --config tb && \
+bash tools/gpu_profile.sh tbr "tiebreak_lpm_kernel<true, false," markets=1000000 ragged=1 steps_total=8 -- --config tb --ragged && \
 for c5 in c5:reestimate_consensus_votes_kernel:exact c5mfma:reestimate_votes_mfma_kernel:mfma; do
   IFS=: read -r tag kern md <<< "$c5"
   bash tools/gpu_profile.sh $tag $kern markets_this_rank=1000000 mode=$md -- --config c5 --mode $md --steps 2 --warmup 1 --single-mode && \

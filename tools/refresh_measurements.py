@@ -10,7 +10,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # prof tag -> measurements file
 PMC = {"c2": "pmc_c2.json", "c3": "pmc_c3.json", "c3S10M": "pmc_c3_S10M.json", "c4": "pmc_c4.json",
-       "tb": "pmc_tb.json", "ns": "pmc_ns.json", "agg": "pmc_agg.json"}
+       "tb": "pmc_tb.json", "tbr": "pmc_tb_ragged.json", "ns": "pmc_ns.json", "agg": "pmc_agg.json"}
 # C5: pass 1 + the agreement pass, per mode (the line's own mode is exact)
 C5 = {"c5": "pmc_c5.json", "c5mfma": "pmc_c5_mfma.json"}
 FILES = ("kernel_stats.csv", "pmc.json", "stats_summary.json", "step_span.json", "pmc_agreement.json",
