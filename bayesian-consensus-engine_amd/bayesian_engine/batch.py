@@ -391,13 +391,15 @@ class TiePlan:
     buckets: Optional[list]  # [(device int32 list, max_len)], or None: contiguous tiles
 
 
-# relative cost of a 64-market tile, measured (profiles/archive/r05f/, 1M markets): contiguous FULL
-# (every market 32 agents: 42 ns per tile) / contiguous ragged (the general 32-position body:
-# 46 ns) / gathered buckets of 8 / 16 / 32 positions (20 / 40 / 70 ns).  The lane kernels are
-# latency-bound by their stage -> compute -> flush phases, so fewer positions per lane save
-# less than the arithmetic suggests, and a uniform 1..32 ragged batch stays contiguous
-# (buckets 0.788 vs 0.732 ms); a batch of mostly short markets is bucketed.
-_TILE_COST = {"full": 0.91, "ragged": 1.0, 8: 0.43, 16: 0.87, 32: 1.52}
+# relative cost of a 64-market tile, measured (kernel traces, 1M markets, profiles/r06gb/):
+# contiguous FULL (every market 32 agents: 42 ns per tile) / contiguous ragged (the general
+# 32-position body: 45.4 ns) / gathered buckets of 8 / 16 / 32 positions (20.7 / 34.9 / 58.3 ns,
+# since round 6's batched row loads: 20 / 40 / 70 before, profiles/archive/r05f/).  The lane
+# kernels are latency-bound by their stage -> compute -> flush phases, so fewer positions per
+# lane save less than the arithmetic suggests; a uniform 1..32 ragged batch is now bucketed
+# (0.674-0.680 vs 0.721 ms contiguous), a uniform 32 batch stays contiguous.
+_TILE_COST = {"full": 0.92, "ragged": 1.0, 8: 0.46, 16: 0.77, 32: 1.28}
+_BUCKET_GAIN = 0.97  # bucket when the model saves >= 3% (one launch more per call)
 
 
 def tiebreak_plan(offsets_host: np.ndarray, device=None, force: bool = False) -> TiePlan:
@@ -416,7 +418,7 @@ def tiebreak_plan(offsets_host: np.ndarray, device=None, force: bool = False) ->
     edges = ((0, 8), (9, 16), (17, 32))
     idx = [np.nonzero((lens >= lo) & (lens <= hi))[0].astype(np.int32) for lo, hi in edges]
     bucket = sum(_TILE_COST[hi] * ((len(i) + 63) // 64) for (lo, hi), i in zip(edges, idx))
-    if bucket >= 0.9 * contig and not force:
+    if bucket >= _BUCKET_GAIN * contig and not force:
         return TiePlan(None)
     dev = device or N.device()
     return TiePlan([(torch.from_numpy(i).to(dev), hi) for (lo, hi), i in zip(edges, idx) if len(i)])

@@ -268,6 +268,7 @@ constexpr bool kTbFullKeysInLds = true;  // FULL tiles: sort (ordinal, agent) al
 // the staged general body likewise: tie-break over 1M ragged markets 0.7347-0.7364 -> 0.7201-0.7218
 // ms, three interleaved reps (profiles/r06tb/)
 constexpr bool kTbGeneralKeysInLds = true;
+constexpr int kTbGatherBatch = 8;  // GATHER staging: passes whose row loads are in flight together
 constexpr int kTbDump = 64;
 // FULL tiles: 16-B loads per lane in flight while staging the predictions / confidences and the
 // weights / reliabilities (8 for the latter spills ~10 VGPRs around those stages and still
@@ -478,13 +479,32 @@ __global__ __launch_bounds__(64 * kTbLpmWaves) __attribute__((amdgpu_waves_per_e
     auto stage = [&](const double* src) {
       wave_sync_lds();  // the buffer's previous readers (this wave) are done
       if constexpr (GATHER) {
-        rows_copy([&](int r, int i, int64_t ro, int rn) {
-          if (i + 1 >= 0 && i < rn) {  // the pair [i, i + 1] touches the row
-            const double2 v = tb_ld2(src + ro + i);  // 16-B aligned: ro + i is even
-            if (i >= 0) buf[tb_pad(NP * r + i)] = v.x;
-            if (i + 1 < rn) buf[tb_pad(NP * r + i + 1)] = v.y;
+        // kTbGatherBatch passes' loads issued before any is written to LDS: the loads are
+        // unconditional (a pair outside its row reads agent 0 of the array, never used), so
+        // they leave back to back -- one memory round trip per batch instead of one per pass
+        constexpr int K = kGL < kTbGatherBatch ? kGL : kTbGatherBatch;
+#pragma unroll 1
+        for (int p0 = 0; p0 < kGL; p0 += K) {
+          double2 v[K];
+          int rr[K], ii[K], nn[K];
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            const int r = (p0 + k) * kGR + lane / kGL, c = lane % kGL;
+            const int64_t ro = sRowOff[wv][r];
+            const int rn = sRowN[wv][r];
+            const int i = 2 * c - (int)(ro & 1);
+            const bool touch = i + 1 >= 0 && i < rn;  // the pair [i, i + 1] touches the row
+            v[k] = tb_ld2(src + (touch ? ro + i : 0));  // 16-B aligned: ro + i is even
+            rr[k] = r;
+            ii[k] = i;
+            nn[k] = touch ? rn : 0;
           }
-        });
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            if (ii[k] >= 0 && ii[k] < nn[k]) buf[tb_pad(NP * rr[k] + ii[k])] = v[k].x;
+            if (ii[k] + 1 >= 0 && ii[k] + 1 < nn[k]) buf[tb_pad(NP * rr[k] + ii[k] + 1)] = v[k].y;
+          }
+        }
         rows_tail([&](int r, int i, int64_t ro) { buf[tb_pad(NP * r + i)] = src[ro + i]; });
         wave_sync_lds();
         return;

@@ -67,6 +67,8 @@ def parse(argv=None):
     p.add_argument("--ragged", action="store_true", help="tb: market lengths uniform on 1..--len")
     p.add_argument("--tb-contiguous", action="store_true",
                    help="tb: contiguous tiles only (no length-bucket plan), the A/B for batch.tiebreak_plan")
+    p.add_argument("--tb-buckets", action="store_true",
+                   help="tb: always the length-bucket plan (batch.tiebreak_plan force=True), the other side of that A/B")
     p.add_argument("--sources", type=int, default=10_000)
     p.add_argument("--mode", default=None, choices=["exact", "fast", "mfma"],
                    help="consensus summation mode (default: exact for c2, where it costs nothing; fast -- "

@@ -879,7 +879,8 @@ def _tb(args, world, rank, barrier, max_over, sum_over):
     d = [T(off), T(pred), T(conf), T(weight), T(rel)]
     # the length buckets of a ragged batch are planned once, outside the timed region (a
     # uniform batch gets no buckets: contiguous tiles, the FULL-tile kernel)
-    plan = batch.tiebreak_plan(off, dev) if L <= 32 and not getattr(args, "tb_contiguous", False) else None
+    plan = (batch.tiebreak_plan(off, dev, force=getattr(args, "tb_buckets", False))
+            if L <= 32 and not getattr(args, "tb_contiguous", False) else None)
     res = batch.tiebreak(*d, offsets_host=off, plan=plan)
 
     def step():  # every market has L <= 64 agents: no per-step host scan of the offsets

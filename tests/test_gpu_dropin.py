@@ -1018,8 +1018,11 @@ def test_tiebreak_length_buckets_vs_oracle(precision):
     d = [T(off), T(pred), T(conf), T(weight), T(rel)]
     plan = batch.tiebreak_plan(off, force=True)
     assert plan.buckets is not None and [hi for _, hi in plan.buckets] == [8, 16, 32]
-    # the cost model keeps a uniform 0..32 batch contiguous and buckets a batch of short markets
-    assert batch.tiebreak_plan(off).buckets is None
+    # the cost model buckets a large uniform 0..32 batch (since round 6's batched gather
+    # staging) and a batch of short markets
+    big = np.zeros(64001, np.int64)
+    big[1:] = np.cumsum(rng.integers(0, 33, 64000))
+    assert batch.tiebreak_plan(big).buckets is not None
     short = np.zeros(3001, np.int64)
     short[1:] = np.cumsum(rng.integers(0, 11, 3000))
     assert batch.tiebreak_plan(short).buckets is not None

@@ -278,10 +278,10 @@ def test_markstein_quotients_match_ieee_division(tmp_path):
 
 def test_tiebreak_plan_buckets_by_measured_tile_costs():
     """batch.tiebreak_plan (host only): buckets of <= 8 / 9..16 / 17..32 agents exactly when
-    they cost less than contiguous tiles by the measured per-tile costs (profiles/archive/r05f/): a
-    uniform 1..32 ragged batch and a uniform 32 batch stay contiguous, a batch of short markets
-    is bucketed, a batch with a market past 32 agents is never bucketed; every market lands in
-    exactly one bucket."""
+    they cost less than contiguous tiles by the measured per-tile costs (profiles/r06gb/): a
+    uniform 1..32 ragged batch and a batch of short markets are bucketed, a uniform 32 batch
+    stays contiguous, a batch with a market past 32 agents is never bucketed; every market lands
+    in exactly one bucket."""
     import torch
     from bayesian_engine import batch
     rng = np.random.default_rng(5)
@@ -292,8 +292,9 @@ def test_tiebreak_plan_buckets_by_measured_tile_costs():
         o[1:] = np.cumsum(lens)
         return o
 
-    assert batch.tiebreak_plan(off(rng.integers(1, 33, 20000)), cpu).buckets is None
+    assert batch.tiebreak_plan(off(rng.integers(1, 33, 20000)), cpu).buckets is not None
     assert batch.tiebreak_plan(off(np.full(20000, 32)), cpu).buckets is None
+    assert batch.tiebreak_plan(off(rng.integers(20, 33, 20000)), cpu).buckets is None  # mostly long
     assert batch.tiebreak_plan(off(np.append(rng.integers(0, 5, 1000), 33)), cpu).buckets is None
     lens = rng.integers(0, 13, 20000)
     p = batch.tiebreak_plan(off(lens), cpu)
